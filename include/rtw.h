@@ -1,0 +1,181 @@
+/*
+ * rtw.h -- C-ABI of the MI355X (gfx950) path tracer: the drop-in boundary for
+ * the reference's per-pixel / per-sample ray_colour loop.
+ *
+ * Reference interfaces replaced (paths relative to N9199/ray_tracing_weekend):
+ *   Camera::render(&self, world: &dyn Hittable, lights: &dyn Hittable)
+ *       -> Vec<Vec<SampledColour>>            shared/src/camera.rs:295-297
+ *   Camera::render_debug(...)                 shared/src/camera.rs:299-312
+ *   (both through render_internal            shared/src/camera.rs:315-388)
+ *   CameraBuilder::build(self) -> Camera      shared/src/camera.rs:114-218
+ *   scenes::simple() (the input producer)     scenes/src/lib.rs:155-233
+ *   SampledColour Display / PPM writer        shared/src/colour.rs:14-36,136-148;
+ *                                             bin/src/main.rs:89-104
+ *
+ * Plain C types only (no torch, no HIP types): pointers, sizes, POD structs.
+ * Every entry point returns 0 on success and a negative RTW_E* code on error
+ * (the reference panics instead; this library never aborts the caller).
+ * The rtw_ctx is reentrant across contexts; one context is single-threaded.
+ * The GPU work runs on gfx950 only; there is no CPU fallback in this library.
+ *
+ * Output convention (mirrors render_internal's Vec<Vec<Colour>> before it is
+ * wrapped in SampledColour): out[(j * W + i) * 3 + c] is the SUM of the
+ * samples of pixel (i, j) -- not the mean -- and j = 0 is the BOTTOM row
+ * (camera.rs:179-188: viewport_v = +v * h).  NaN samples are not scrubbed
+ * (the live integrator never calls fix_nan, camera.rs:459-522).
+ */
+#ifndef RTW_H
+#define RTW_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RTW_ABI_VERSION 1
+
+/* error codes */
+#define RTW_OK 0
+#define RTW_E_INVALID (-1)       /* bad argument / inconsistent scene */
+#define RTW_E_DEVICE (-2)        /* HIP runtime error (message in rtw_last_error) */
+#define RTW_E_NO_LIGHTS (-3)     /* Lambertian present, empty light list:
+                                    hittable_list.rs:417 panics there */
+#define RTW_E_NO_SCENE (-4)      /* render before a scene was set */
+#define RTW_E_UNSUPPORTED (-5)   /* scene/feature outside this build's scope */
+
+/* precision of the device arithmetic */
+#define RTW_F32 0                /* speed mode: f32 + FMA + native sqrt/rcp/sin/cos */
+#define RTW_F64 1                /* parity mode: f64, no FMA contraction, same op order
+                                    as the reference (bit-comparable with the oracle) */
+
+/* material kinds (shared/src/material.rs) */
+#define RTW_LAMBERTIAN 0         /* material.rs:327-376 (SolidColour texture) */
+#define RTW_METAL 1              /* material.rs:378-421 */
+#define RTW_DIELECTRIC 2         /* material.rs:423-488 ("Dialectric") */
+#define RTW_INVISIBLE 3          /* material.rs:321-325 */
+
+/* World acceleration used by the render kernel */
+#define RTW_ACCEL_AUTO 0         /* pick per scene */
+#define RTW_ACCEL_BRUTE 1        /* every ray tests every sphere, sphere list in LDS */
+#define RTW_ACCEL_BVH 2          /* device BVH (closest-hit semantics unchanged) */
+
+/* CameraBuilder (camera.rs:29-42).  has_* == 0 encodes Option::None. */
+typedef struct rtw_camera_builder {
+    int32_t has_aspect_ratio, has_image_width, has_image_height;
+    double aspect_ratio;
+    uint32_t image_width, image_height;
+    uint32_t samples_per_pixel;  /* u16 in the reference */
+    uint32_t max_depth;
+    double background[3];
+    double vfov;
+    double lookfrom[3], lookat[3], vup[3];
+    double defocus_angle, focus_dist;
+} rtw_camera_builder;
+
+/* The derived Camera fields the render loop reads (camera.rs:228-261). */
+typedef struct rtw_camera {
+    uint32_t image_width, image_height;
+    uint32_t samples_per_pixel, max_depth;
+    double background[3];
+    double defocus_angle;
+    double center[3], pixel00_loc[3], pixel_delta_u[3], pixel_delta_v[3];
+    double defocus_disk_u[3], defocus_disk_v[3];
+} rtw_camera;
+
+/* Flattened world + lights, struct-of-arrays, caller-owned host memory.
+ * world  = planes + spheres (closest hit over all of them, bvh.rs:164-188)
+ * lights = spheres (HittableList::pdf_value / random, hittable_list.rs:408-419) */
+typedef struct rtw_scene {
+    uint32_t n_spheres;
+    const double *spheres;        /* n_spheres x {cx, cy, cz, radius} */
+    const uint32_t *sphere_mat;   /* n_spheres material ids */
+    uint32_t n_planes;
+    const double *planes;         /* n_planes x {px, py, pz, nx, ny, nz}, unit normal */
+    const uint32_t *plane_mat;
+    uint32_t n_materials;
+    const uint32_t *mat_type;     /* RTW_LAMBERTIAN ... RTW_INVISIBLE */
+    const double *mat_params;     /* n_materials x {albedo r, g, b, fuzz, ior} */
+    uint32_t n_lights;
+    const double *lights;         /* n_lights x {cx, cy, cz, radius} */
+} rtw_scene;
+
+typedef struct rtw_stats {
+    uint64_t samples;             /* W*H*spp of the rendered tiles */
+    uint64_t segments;            /* world.hit calls */
+    uint64_t lambertian;          /* Scatter-branch bounces (light pdf loop) */
+    double kernel_ms;             /* device time of the last render (HIP events) */
+    uint32_t accel;               /* RTW_ACCEL_* actually used */
+    uint32_t chunk;               /* samples per work item */
+} rtw_stats;
+
+typedef struct rtw_ctx rtw_ctx;
+
+/* ---- context ---------------------------------------------------------- */
+int rtw_abi_version(void);
+rtw_ctx *rtw_create(int device, int precision);
+void rtw_destroy(rtw_ctx *ctx);
+const char *rtw_last_error(const rtw_ctx *ctx);
+int rtw_precision(const rtw_ctx *ctx);
+/* knobs: samples per work item (0 = auto), acceleration (RTW_ACCEL_*) */
+int rtw_set_chunk(rtw_ctx *ctx, uint32_t chunk);
+int rtw_set_accel(rtw_ctx *ctx, int accel);
+
+/* ---- CameraBuilder::build (camera.rs:114-218) ------------------------- */
+int rtw_camera_build(const rtw_camera_builder *builder, rtw_camera *out);
+/* CameraBuilder::new() defaults (camera.rs:45-60) */
+void rtw_camera_builder_default(rtw_camera_builder *out);
+
+/* ---- scene ------------------------------------------------------------ */
+/* Validate, convert to the device layout and upload (copied; the caller may
+ * free its arrays afterwards). */
+int rtw_set_scene(rtw_ctx *ctx, const rtw_scene *scene);
+
+/* ---- Camera::render (camera.rs:295-297) ------------------------------- */
+/* Synchronous drop-in: uploads `scene` (if non-NULL), renders every pixel and
+ * writes H*W*3 doubles (sums, j = 0 bottom row) to host `out_sum`. */
+int rtw_render(rtw_ctx *ctx, const rtw_camera *cam, const rtw_scene *scene,
+               uint64_t seed, double *out_sum, rtw_stats *stats);
+
+/* Device-resident form for benchmarking and multi-GPU sharding.
+ * Renders the 8-row tile rows t with t % nranks == rank into d_out, a device
+ * buffer of rtw_rows_for_rank(H, rank, nranks) * W * 3 elements of the
+ * context's precision (float or double), the rank's image rows packed in
+ * increasing order.  Asynchronous on `stream` (a hipStream_t; NULL = the
+ * context's own stream).  No host synchronisation inside. */
+int rtw_render_device(rtw_ctx *ctx, const rtw_camera *cam, uint64_t seed,
+                      uint32_t rank, uint32_t nranks, void *d_out, size_t out_bytes,
+                      void *stream);
+uint32_t rtw_tile_rows(void);                        /* rows per tile row (8) */
+uint32_t rtw_rows_for_rank(uint32_t image_height, uint32_t rank, uint32_t nranks);
+/* Counters of the last render (waits for it to finish). */
+int rtw_get_stats(rtw_ctx *ctx, rtw_stats *stats);
+/* Device times (HIP events) of the last min(max, 64) renders, oldest first:
+ * render_ms = the render kernel alone, total_ms = render + chunk reduction.
+ * Waits for them; returns how many were written. */
+int rtw_get_timings(rtw_ctx *ctx, float *render_ms, float *total_ms, int max);
+
+/* ---- scenes::simple (scenes/src/lib.rs:155-233) ----------------------- */
+/* The library owns the arrays; view them through rtw_world_scene(). grid_n =
+ * 11 is the reference scene; larger n gives the synthetic C3/C5 fields. */
+typedef struct rtw_world rtw_world;
+rtw_world *rtw_scene_simple(uint64_t seed, int grid_n);
+const rtw_scene *rtw_world_scene(const rtw_world *w);
+/* the camera builder scenes::simple returns (lib.rs:219-226) + main.rs's vfov */
+void rtw_world_camera_builder(const rtw_world *w, rtw_camera_builder *out);
+void rtw_world_free(rtw_world *w);
+
+/* ---- SampledColour / PPM (colour.rs:14-36; main.rs:89-104) ------------ */
+/* sums -> 8-bit RGB, rows flipped so that row 0 is the TOP row:
+ * (256 * clamp(sqrt(sum / spp), 0, 1)) as u8, saturating, NaN -> 0. */
+int rtw_encode_rgb8(const double *sums, uint32_t width, uint32_t height, uint32_t spp,
+                    uint8_t *out_rgb);
+/* Writes the reference's P3 "image.ppm" text; returns bytes written or < 0. */
+int rtw_write_ppm(const char *path, const double *sums, uint32_t width, uint32_t height,
+                  uint32_t spp);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RTW_H */

@@ -1,0 +1,149 @@
+/*
+ * rtw_oracle.h -- CPU restatement of the reference's per-pixel/per-sample
+ * ray_colour loop (N9199/ray_tracing_weekend), f64, plain C.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing in the product (ray_tracing_weekend_amd/)
+ * links or calls this.  Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load it, and there only as the checker / the timed
+ * CPU baseline ("kind": "port").
+ *
+ * Parity status: the Rust reference cannot be built or run here (no cargo /
+ * rustc) and its own tests pin no numeric output
+ * (integration-tests/src/lib.rs:7-112 has no asserts).  The restatement is
+ * pinned by hand-derived known-answer tests taken from the cited formulas
+ * (tests/test_oracle_kat.py) -- "parity unpinned" against the reference
+ * binary itself.
+ *
+ * Conventions shared with the GPU path (the C-ABI in include/rtw.h):
+ *   out[(j*W + i)*3 + c]: per-pixel SUM over samples (not a mean), j = 0 is
+ *   the bottom row (camera.rs:179-188, 381-387).
+ */
+#ifndef RTW_ORACLE_H
+#define RTW_ORACLE_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Material type codes (material.rs:321-488). */
+enum { RTWO_LAMBERTIAN = 0, RTWO_METAL = 1, RTWO_DIELECTRIC = 2, RTWO_INVISIBLE = 3 };
+
+/* World-acceleration choice for the closest-hit query.  All three return the
+ * same closest hit (bvh.rs:164-188 keeps "min t over every primitive").
+ *   0 = brute force over the flat primitive list (the checker)
+ *   1 = restatement of the reference BVH (bvh.rs:106-188, hittable_list.rs:
+ *       296-406) including its per-visit recursive node-AABB recomputation
+ *       (bvh.rs:147-152) -- the faithful CPU baseline
+ *   2 = the same BVH with node AABBs cached once (a kinder CPU baseline) */
+enum { RTWO_ACCEL_BRUTE = 0, RTWO_ACCEL_BVH_REF = 1, RTWO_ACCEL_BVH_CACHED = 2 };
+
+typedef struct rtwo_camera {
+    /* Derived fields of Camera (camera.rs:228-261) the render loop reads. */
+    uint32_t image_width, image_height;
+    uint32_t samples_per_pixel, max_depth;
+    double background[3];
+    double defocus_angle;
+    double center[3], pixel00_loc[3], pixel_delta_u[3], pixel_delta_v[3];
+    double defocus_disk_u[3], defocus_disk_v[3];
+} rtwo_camera;
+
+typedef struct rtwo_camera_builder {
+    /* CameraBuilder (camera.rs:29-42).  has_* = 0 means Option::None. */
+    int has_aspect_ratio, has_image_width, has_image_height;
+    double aspect_ratio;
+    uint32_t image_width, image_height;
+    uint32_t samples_per_pixel, max_depth;
+    double background[3];
+    double vfov;
+    double lookfrom[3], lookat[3], vup[3];
+    double defocus_angle, focus_dist;
+} rtwo_camera_builder;
+
+typedef struct rtwo_scene {
+    uint32_t n_spheres;
+    const double *spheres;      /* n x {cx, cy, cz, r} */
+    const uint32_t *sphere_mat; /* n material ids */
+    uint32_t n_planes;
+    const double *planes;       /* n x {px, py, pz, nx, ny, nz} (normal already normalized, plane.rs:175) */
+    const uint32_t *plane_mat;
+    uint32_t n_materials;
+    const uint32_t *mat_type;   /* n */
+    const double *mat_params;   /* n x {albedo r, g, b, fuzz, ior} */
+    uint32_t n_lights;
+    const double *lights;       /* n x {cx, cy, cz, r}  (HittableList of Spheres) */
+} rtwo_scene;
+
+typedef struct rtwo_stats {
+    uint64_t samples;
+    uint64_t segments;          /* world.hit calls (one per bounce) */
+    uint64_t lambertian;        /* Scatter-branch bounces (light-list pdf loop) */
+    uint64_t nan_samples;
+} rtwo_stats;
+
+/* CameraBuilder::build, camera.rs:114-218. Returns 0. */
+int rtwo_camera_build(const rtwo_camera_builder *b, rtwo_camera *out);
+
+/* Render a window of the image.  Rows j in [row_begin, row_end) stepping by
+ * row_step, columns [col_begin, col_end).  Untouched pixels are left as is.
+ * chunk: samples are summed in chunks of `chunk` (chunk >= spp = the
+ * reference's single fold, camera.rs:323-335); the per-pixel sum is
+ * ((0 + chunk_0) + chunk_1) + ..., each chunk ((0 + s_a) + s_a+1) + ...
+ * Returns 0 on success, -1 on invalid input (e.g. Lambertian with an empty
+ * light list: hittable_list.rs:417 panics there). */
+int rtwo_render(const rtwo_camera *cam, const rtwo_scene *sc, uint64_t seed,
+                uint32_t chunk, int accel, int nthreads,
+                uint32_t row_begin, uint32_t row_end, uint32_t row_step,
+                uint32_t col_begin, uint32_t col_end,
+                double *out, rtwo_stats *stats);
+
+/* One sample, exposed for tests (returns the colour, fills segment counts). */
+void rtwo_trace_sample(const rtwo_camera *cam, const rtwo_scene *sc, uint64_t seed,
+                       uint32_t i, uint32_t j, uint32_t s, double out_rgb[3],
+                       rtwo_stats *stats);
+
+/* scenes::simple (scenes/src/lib.rs:155-233) driven by the build's seeded
+ * RNG; grid a,b in [-n, n) (the reference uses n = 11).  Writes at most
+ * max_* entries; returns 0, or -1 if a capacity is too small.  Counts are
+ * returned through the *_count pointers.  Material ids: 0 = ground plane
+ * material, then one per sphere in insertion order. */
+int rtwo_scene_simple(uint64_t seed, int n,
+                      uint32_t max_spheres, double *spheres, uint32_t *sphere_mat,
+                      uint32_t *n_spheres,
+                      double *planes, uint32_t *plane_mat, uint32_t *n_planes,
+                      uint32_t max_mats, uint32_t *mat_type, double *mat_params,
+                      uint32_t *n_mats,
+                      uint32_t max_lights, double *lights, uint32_t *n_lights);
+
+/* ---- primitive-level entry points for the known-answer tests ---- */
+void rtwo_rng_seed(uint64_t seed, uint64_t pixel_index, uint64_t sample_index, uint64_t st[4]);
+uint64_t rtwo_rng_next(uint64_t st[4]);
+double rtwo_rand_std(uint64_t st[4]);
+double rtwo_rand_open01(uint64_t st[4]);
+double rtwo_rand_uniform_incl(uint64_t st[4], double low, double high);
+uint32_t rtwo_rand_index(uint64_t st[4], uint32_t n);
+void rtwo_sincos_2pi(double r, double *s, double *c);
+/* Sphere::hit (sphere.rs:61-99): returns 1 and t/normal/front on hit. */
+int rtwo_sphere_hit(const double sph[4], const double o[3], const double d[3],
+                    double tmin, double tmax, double *t, double normal[3], int *front);
+/* Plane::hit (plane.rs:61-76). plane = {px,py,pz,nx,ny,nz}. */
+int rtwo_plane_hit(const double pl[6], const double o[3], const double d[3],
+                   double tmin, double tmax, double *t, double normal[3], int *front);
+/* AABBox slab test (hittable.rs:291-339). box = {minx,miny,minz,maxx,maxy,maxz}. */
+int rtwo_aabb_hit(const double box[6], const double o[3], const double d[3],
+                  double tmin, double tmax);
+double rtwo_sphere_pdf_value(const double sph[4], const double o[3], const double d[3]);
+void rtwo_onb(const double n[3], double u[3], double v[3], double w[3]);
+double rtwo_reflectance(double cosine, double ref_idx);
+void rtwo_reflect(const double v[3], const double n[3], double out[3]);
+void rtwo_refract(const double v[3], const double n[3], double eta, double out[3]);
+void rtwo_unit_sphere(uint64_t st[4], double out[3]);
+void rtwo_cosine_hemisphere(uint64_t st[4], double out[3]);
+void rtwo_sphere_random(const double sph[4], const double o[3], uint64_t st[4], double out[3]);
+/* Number of BVH nodes/leaves built for a scene (tests of the BVH restatement). */
+int rtwo_bvh_stats(const rtwo_scene *sc, uint32_t *nodes, uint32_t *leaves, uint32_t *depth);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

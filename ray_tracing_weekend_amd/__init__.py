@@ -1,0 +1,392 @@
+"""ray_tracing_weekend_amd -- MI355X (gfx950) drop-in for the reference's
+per-pixel / per-sample ray_colour loop (N9199/ray_tracing_weekend).
+
+Python mirror of the reference's interface for this path, over the C-ABI in
+include/rtw.h (librtw.so: hand-written HIP kernels + C++ host mirror):
+
+    world, lights, builder = scenes.simple(seed)          # scenes/src/lib.rs:155-233
+    cam = builder.with_image_width(400).with_image_height(225) \
+                 .with_samples_per_pixel(100).with_max_depth(50).build()
+    sums = cam.render(world, lights)                      # shared/src/camera.rs:295-297
+    write_ppm("image.ppm", sums, cam.samples_per_pixel)   # bin/src/main.rs:89-104
+
+`render` returns per-pixel SUMS (not means) as a float64 array [H, W, 3] with
+row j = 0 at the BOTTOM, like render_internal's Vec<Vec<Colour>>.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _capi
+from ._capi import (RTW_ACCEL_AUTO, RTW_ACCEL_BRUTE, RTW_ACCEL_BVH, RTW_DIELECTRIC, RTW_F32,
+                    RTW_F64, RTW_INVISIBLE, RTW_LAMBERTIAN, RTW_METAL)
+
+__all__ = [
+    "Material", "Lambertian", "Metal", "Dialectric", "INVISIBLE", "Sphere", "Plane",
+    "HittableList", "SceneSoA", "flatten", "CameraBuilder", "Camera", "Renderer", "scenes",
+    "encode_rgb8", "write_ppm", "RenderError", "RTW_F32", "RTW_F64",
+]
+
+_lib = _capi.load()   # raises if librtw.so is missing: there is no CPU fallback
+
+
+class RenderError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"{msg} (rtw error {code})")
+        self.code = code
+
+
+# ---------------------------------------------------------------- materials
+@dataclass(frozen=True)
+class Material:
+    type: int
+    albedo: tuple = (0.0, 0.0, 0.0)
+    fuzz: float = 0.0
+    ior: float = 0.0
+
+
+def Lambertian(albedo):                      # material.rs:327-355 (new_with_colour)
+    return Material(RTW_LAMBERTIAN, tuple(map(float, albedo)))
+
+
+def Metal(albedo, fuzz):                     # material.rs:378-406
+    return Material(RTW_METAL, tuple(map(float, albedo)), float(fuzz))
+
+
+def Dialectric(index_of_refraction):         # material.rs:423-455
+    return Material(RTW_DIELECTRIC, (1.0, 1.0, 1.0), 0.0, float(index_of_refraction))
+
+
+INVISIBLE = Material(RTW_INVISIBLE)          # material.rs:321-325
+
+
+@dataclass(frozen=True)
+class Sphere:                                # entities/sphere.rs:24-47
+    center: tuple
+    radius: float
+    mat: Material = INVISIBLE
+
+
+@dataclass(frozen=True)
+class Plane:                                 # entities/plane.rs:20-38 (normal normalized)
+    point: tuple
+    normal: tuple
+    mat: Material = INVISIBLE
+
+    def __post_init__(self):
+        n = [float(v) for v in self.normal]
+        ln = np.sqrt((n[0] * n[0] + n[1] * n[1]) + n[2] * n[2])
+        object.__setattr__(self, "normal", (n[0] / ln, n[1] / ln, n[2] / ln))
+
+
+class HittableList:                          # hittable_collections/hittable_list.rs:247-294
+    def __init__(self, objects=()):
+        self.objects = list(objects)
+
+    def add(self, obj):
+        if not isinstance(obj, (Sphere, Plane)):
+            raise TypeError("only Sphere and Plane are in this build's scope")
+        self.objects.append(obj)
+
+    def __len__(self):
+        return len(self.objects)
+
+
+@dataclass
+class SceneSoA:
+    """Flattened world + lights in the C-ABI's struct-of-arrays layout."""
+    spheres: np.ndarray = field(default_factory=lambda: np.zeros((0, 4)))
+    sphere_mat: np.ndarray = field(default_factory=lambda: np.zeros(0, np.uint32))
+    planes: np.ndarray = field(default_factory=lambda: np.zeros((0, 6)))
+    plane_mat: np.ndarray = field(default_factory=lambda: np.zeros(0, np.uint32))
+    mat_type: np.ndarray = field(default_factory=lambda: np.zeros(0, np.uint32))
+    mat_params: np.ndarray = field(default_factory=lambda: np.zeros((0, 5)))
+    lights: np.ndarray = field(default_factory=lambda: np.zeros((0, 4)))
+
+    def as_c(self):
+        """(rtw_scene, keepalive) -- the struct points into these arrays."""
+        keep = []
+
+        def f(a, cols):
+            a = np.ascontiguousarray(np.asarray(a, np.float64).reshape(-1, cols))
+            keep.append(a)
+            return a.ctypes.data_as(_capi._f64p)
+
+        def u(a):
+            a = np.ascontiguousarray(np.asarray(a, np.uint32).reshape(-1))
+            keep.append(a)
+            return a.ctypes.data_as(_capi._u32p)
+
+        s = _capi.rtw_scene(len(self.sphere_mat), f(self.spheres, 4), u(self.sphere_mat),
+                            len(self.plane_mat), f(self.planes, 6), u(self.plane_mat),
+                            len(self.mat_type), u(self.mat_type), f(self.mat_params, 5),
+                            len(np.asarray(self.lights).reshape(-1, 4)), f(self.lights, 4))
+        return s, keep
+
+    @staticmethod
+    def from_c(s: "_capi.rtw_scene") -> "SceneSoA":
+        def f(ptr, n, cols):
+            return np.ctypeslib.as_array(ptr, shape=(n * cols,)).reshape(n, cols).copy() if n else np.zeros((0, cols))
+
+        def u(ptr, n):
+            return np.ctypeslib.as_array(ptr, shape=(n,)).copy() if n else np.zeros(0, np.uint32)
+
+        return SceneSoA(f(s.spheres, s.n_spheres, 4), u(s.sphere_mat, s.n_spheres),
+                        f(s.planes, s.n_planes, 6), u(s.plane_mat, s.n_planes),
+                        u(s.mat_type, s.n_materials), f(s.mat_params, s.n_materials, 5),
+                        f(s.lights, s.n_lights, 4))
+
+
+def flatten(world, lights) -> SceneSoA:
+    """world: HittableList or SceneSoA; lights: HittableList of Spheres."""
+    if isinstance(world, SceneSoA):
+        return world
+    mats, mtypes, sph, smat, pl, pmat = [], [], [], [], [], []
+
+    def push(m: Material):
+        mtypes.append(m.type)
+        mats.append(list(m.albedo) + [m.fuzz, m.ior])
+        return len(mtypes) - 1
+
+    for o in world.objects:
+        if isinstance(o, Plane):
+            pl.append(list(o.point) + list(o.normal))
+            pmat.append(push(o.mat))
+    for o in world.objects:
+        if isinstance(o, Sphere):
+            sph.append(list(o.center) + [o.radius])
+            smat.append(push(o.mat))
+    li = []
+    for o in lights.objects:
+        if not isinstance(o, Sphere):
+            raise RenderError(_capi.RTW_E_UNSUPPORTED, "only spheres can be lights in this build")
+        li.append(list(o.center) + [o.radius])
+    return SceneSoA(np.array(sph, np.float64).reshape(-1, 4), np.array(smat, np.uint32),
+                    np.array(pl, np.float64).reshape(-1, 6), np.array(pmat, np.uint32),
+                    np.array(mtypes, np.uint32), np.array(mats, np.float64).reshape(-1, 5),
+                    np.array(li, np.float64).reshape(-1, 4))
+
+
+# ---------------------------------------------------------------- camera
+class CameraBuilder:                          # camera.rs:28-112
+    def __init__(self, raw: "_capi.rtw_camera_builder | None" = None):
+        if raw is None:
+            raw = _capi.rtw_camera_builder()
+            _lib.rtw_camera_builder_default(C.byref(raw))
+        self.raw = raw
+
+    def _set3(self, name, v):
+        getattr(self.raw, name)[:] = [float(x) for x in v]
+        return self
+
+    def with_aspect_ratio(self, v):
+        self.raw.has_aspect_ratio, self.raw.aspect_ratio = 1, float(v)
+        return self
+
+    def with_image_width(self, v):
+        self.raw.has_image_width, self.raw.image_width = 1, int(v)
+        return self
+
+    def with_image_height(self, v):
+        self.raw.has_image_height, self.raw.image_height = 1, int(v)
+        return self
+
+    def with_samples_per_pixel(self, v):
+        self.raw.samples_per_pixel = int(v)
+        return self
+
+    def with_max_depth(self, v):
+        self.raw.max_depth = int(v)
+        return self
+
+    def with_background(self, c):
+        return self._set3("background", c)
+
+    def with_vfov(self, v):
+        self.raw.vfov = float(v)
+        return self
+
+    def with_lookfrom(self, p):
+        return self._set3("lookfrom", p)
+
+    def with_lookat(self, p):
+        return self._set3("lookat", p)
+
+    def with_vup(self, v):
+        return self._set3("vup", v)
+
+    def with_defocus_angle(self, v):
+        self.raw.defocus_angle = float(v)
+        return self
+
+    def with_focus_dist(self, v):
+        self.raw.focus_dist = float(v)
+        return self
+
+    def build(self) -> "Camera":              # camera.rs:114-218
+        cam = _capi.rtw_camera()
+        rc = _lib.rtw_camera_build(C.byref(self.raw), C.byref(cam))
+        if rc != 0:
+            raise RenderError(rc, "CameraBuilder::build failed")
+        return Camera(cam)
+
+    def copy(self) -> "CameraBuilder":
+        raw = _capi.rtw_camera_builder()
+        C.pointer(raw)[0] = self.raw
+        return CameraBuilder(raw)
+
+
+class Camera:
+    def __init__(self, raw: "_capi.rtw_camera"):
+        self.raw = raw
+
+    def __getattr__(self, name):
+        raw = self.__dict__["raw"]
+        v = getattr(raw, name)
+        return tuple(v) if isinstance(v, C.Array) else v
+
+    def render(self, world, lights, *, seed: int = 0x5EED0001, precision: int = RTW_F32,
+               device: int = 0, accel: int = RTW_ACCEL_AUTO) -> np.ndarray:
+        """Camera::render (camera.rs:295-297) on the GPU: float64 sums [H, W, 3]."""
+        with Renderer(device=device, precision=precision) as r:
+            r.set_accel(accel)
+            r.set_scene(flatten(world, lights))
+            return r.render(self, seed)
+
+    render_debug = render                     # camera.rs:299-312 (no sequential mode on a GPU)
+
+
+class Renderer:
+    """An rtw_ctx: a device, a precision, a resident scene and work buffers."""
+
+    def __init__(self, device: int = 0, precision: int = RTW_F32):
+        self.ctx = _lib.rtw_create(device, precision)
+        if not self.ctx:
+            raise RenderError(_capi.RTW_E_DEVICE, f"rtw_create(device={device}) failed: no gfx950 "
+                              "device visible (this library has no CPU path)")
+        self.precision = precision
+        self.stats = _capi.rtw_stats()
+
+    def close(self):
+        if self.ctx:
+            _lib.rtw_destroy(self.ctx)
+            self.ctx = None
+
+    __del__ = close
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def _check(self, rc, what):
+        if rc != 0:
+            raise RenderError(rc, f"{what}: {_lib.rtw_last_error(self.ctx).decode()}")
+
+    def set_chunk(self, chunk: int):
+        self._check(_lib.rtw_set_chunk(self.ctx, chunk), "rtw_set_chunk")
+
+    def set_accel(self, accel: int):
+        self._check(_lib.rtw_set_accel(self.ctx, accel), "rtw_set_accel")
+
+    def set_scene(self, scene: SceneSoA):
+        s, keep = scene.as_c()
+        self._check(_lib.rtw_set_scene(self.ctx, C.byref(s)), "rtw_set_scene")
+        del keep
+
+    def render(self, cam: Camera, seed: int) -> np.ndarray:
+        H, W = cam.raw.image_height, cam.raw.image_width
+        out = np.zeros((H, W, 3), np.float64)
+        self._check(_lib.rtw_render(self.ctx, C.byref(cam.raw), None, C.c_uint64(seed),
+                                    out.ctypes.data_as(_capi._f64p), C.byref(self.stats)),
+                    "rtw_render")
+        return out
+
+    def render_device(self, cam: Camera, seed: int, out_ptr: int, out_bytes: int, *,
+                      rank: int = 0, nranks: int = 1, stream: int = 0):
+        """Asynchronous render of this rank's tile rows into device memory."""
+        self._check(_lib.rtw_render_device(self.ctx, C.byref(cam.raw), C.c_uint64(seed), rank,
+                                           nranks, C.c_void_p(out_ptr), out_bytes,
+                                           C.c_void_p(stream) if stream else None),
+                    "rtw_render_device")
+
+    def get_timings(self, n: int = 64):
+        """(render_ms, total_ms) lists for the last n renders (HIP events)."""
+        a, b = (C.c_float * n)(), (C.c_float * n)()
+        got = _lib.rtw_get_timings(self.ctx, a, b, n)
+        if got < 0:
+            self._check(got, "rtw_get_timings")
+        return list(a[:got]), list(b[:got])
+
+    def get_stats(self) -> "_capi.rtw_stats":
+        self._check(_lib.rtw_get_stats(self.ctx, C.byref(self.stats)), "rtw_get_stats")
+        return self.stats
+
+
+def rows_for_rank(height: int, rank: int, nranks: int) -> int:
+    return int(_lib.rtw_rows_for_rank(height, rank, nranks))
+
+
+def tile_rows() -> int:
+    return int(_lib.rtw_tile_rows())
+
+
+# ---------------------------------------------------------------- scenes
+class scenes:                                 # scenes/src/lib.rs
+    @staticmethod
+    def simple_soa(seed: int = 0x5EED0001, n: int = 11):
+        """(SceneSoA, CameraBuilder) straight from the C++ generator."""
+        w = _lib.rtw_scene_simple(C.c_uint64(seed & 0xFFFFFFFFFFFFFFFF), n)
+        if not w:
+            raise RenderError(_capi.RTW_E_INVALID, "rtw_scene_simple failed")
+        try:
+            soa = SceneSoA.from_c(_lib.rtw_world_scene(w).contents)
+            b = _capi.rtw_camera_builder()
+            _lib.rtw_world_camera_builder(w, C.byref(b))
+        finally:
+            _lib.rtw_world_free(w)
+        return soa, CameraBuilder(b)
+
+    @staticmethod
+    def simple(seed: int = 0x5EED0001, n: int = 11):
+        """scenes::simple -> (world, lights, CameraBuilder) as object lists."""
+        soa, builder = scenes.simple_soa(seed, n)
+        world, lights = HittableList(), HittableList()
+        for pl, m in zip(soa.planes, soa.plane_mat):
+            world.add(Plane(tuple(pl[:3]), tuple(pl[3:]), _mat(soa, m)))
+        for sp, m in zip(soa.spheres, soa.sphere_mat):
+            world.add(Sphere(tuple(sp[:3]), float(sp[3]), _mat(soa, m)))
+        for li in soa.lights:
+            lights.add(Sphere(tuple(li[:3]), float(li[3]), INVISIBLE))
+        return world, lights, builder
+
+
+def _mat(soa, m):
+    p = soa.mat_params[m]
+    return Material(int(soa.mat_type[m]), (float(p[0]), float(p[1]), float(p[2])), float(p[3]),
+                    float(p[4]))
+
+
+# ---------------------------------------------------------------- output
+def encode_rgb8(sums: np.ndarray, spp: int) -> np.ndarray:
+    """SampledColour Display (colour.rs:14-36), rows flipped top-first: uint8 [H, W, 3]."""
+    s = np.ascontiguousarray(sums, np.float64)
+    H, W = s.shape[:2]
+    out = np.zeros((H, W, 3), np.uint8)
+    _lib.rtw_encode_rgb8(s.ctypes.data_as(_capi._f64p), W, H, spp,
+                         out.ctypes.data_as(C.POINTER(C.c_uint8)))
+    return out
+
+
+def write_ppm(path: str, sums: np.ndarray, spp: int) -> int:
+    """The reference's P3 image.ppm (bin/src/main.rs:89-104)."""
+    s = np.ascontiguousarray(sums, np.float64)
+    H, W = s.shape[:2]
+    n = _lib.rtw_write_ppm(path.encode(), s.ctypes.data_as(_capi._f64p), W, H, spp)
+    if n < 0:
+        raise RenderError(n, f"cannot write {path}")
+    return n

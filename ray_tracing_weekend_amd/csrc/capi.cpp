@@ -1,0 +1,555 @@
+// capi.cpp -- the C-ABI (include/rtw.h): context, scene upload, CameraBuilder::
+// build, the render entry points, scenes::simple and the PPM encoding.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <new>
+#include <type_traits>
+#include <string>
+#include <vector>
+
+#include "../../include/rtw.h"
+#include "host/rtw_host.hpp"
+#include "rtw_kernels.h"
+
+struct rtw_ctx {
+    int device = 0;
+    int precision = RTW_F32;
+    int accel = RTW_ACCEL_AUTO;
+    uint32_t chunk = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    // ring of per-render event triples: [start, after render kernel, after reduce]
+    static constexpr int kRing = 64;
+    hipEvent_t ring[kRing][3] = {};
+    uint64_t n_renders = 0;
+    // device scene (one allocation holding every array)
+    void* d_scene = nullptr;
+    size_t scene_bytes = 0;
+    rtw::DevScene<float> sc32{};
+    rtw::DevScene<double> sc64{};
+    bool has_scene = false;
+    // work buffers
+    void* d_partial = nullptr;
+    size_t partial_cap = 0;
+    void* d_out = nullptr;
+    size_t out_cap = 0;
+    unsigned long long* d_counters = nullptr;
+    std::vector<unsigned char> h_out;
+    rtw_stats last{};
+    std::string err;
+};
+
+namespace {
+
+constexpr size_t kLdsLimit = 160 * 1024;
+
+int fail(rtw_ctx* c, int code, const std::string& msg) {
+    if (c) c->err = msg;
+    return code;
+}
+int hip_fail(rtw_ctx* c, hipError_t e, const char* what) {
+    return fail(c, RTW_E_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
+}
+#define HIP_TRY(ctx, expr)                                   \
+    do {                                                     \
+        hipError_t e_ = (expr);                              \
+        if (e_ != hipSuccess) return hip_fail(ctx, e_, #expr); \
+    } while (0)
+
+size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+// Convert the caller's f64 SoA into the device layout of precision R, in one
+// host staging blob, and fill the DevScene pointers relative to `base`.
+template <typename R>
+std::vector<unsigned char> stage_scene(const rtw_scene* s, rtw::DevScene<R>* ds, uintptr_t base) {
+    using R4 = rtw::R4<R>;
+    size_t off = 0;
+    auto reserve = [&](size_t bytes) {
+        size_t o = align_up(off, 64);
+        off = o + bytes;
+        return o;
+    };
+    const size_t o_sph = reserve(sizeof(R4) * s->n_spheres);
+    const size_t o_r = reserve(sizeof(R) * s->n_spheres);
+    const size_t o_smat = reserve(sizeof(uint32_t) * s->n_spheres);
+    const size_t o_pl = reserve(sizeof(R) * 6 * s->n_planes);
+    const size_t o_pmat = reserve(sizeof(uint32_t) * s->n_planes);
+    const size_t o_mt = reserve(sizeof(uint32_t) * s->n_materials);
+    const size_t o_mp = reserve(sizeof(R4) * s->n_materials);
+    const size_t o_li = reserve(sizeof(R4) * s->n_lights);
+    std::vector<unsigned char> blob(align_up(off, 64) + 64, 0);
+    unsigned char* b = blob.data();
+    for (uint32_t k = 0; k < s->n_spheres; ++k) {
+        const double* p = s->spheres + 4 * k;
+        R r = (R)p[3];
+        reinterpret_cast<R4*>(b + o_sph)[k] = R4{(R)p[0], (R)p[1], (R)p[2], r * r};
+        reinterpret_cast<R*>(b + o_r)[k] = r;
+        reinterpret_cast<uint32_t*>(b + o_smat)[k] = s->sphere_mat[k];
+    }
+    for (uint32_t k = 0; k < 6 * s->n_planes; ++k) reinterpret_cast<R*>(b + o_pl)[k] = (R)s->planes[k];
+    for (uint32_t k = 0; k < s->n_planes; ++k) reinterpret_cast<uint32_t*>(b + o_pmat)[k] = s->plane_mat[k];
+    for (uint32_t k = 0; k < s->n_materials; ++k) {
+        const double* m = s->mat_params + 5 * k;
+        const uint32_t t = s->mat_type[k];
+        reinterpret_cast<uint32_t*>(b + o_mt)[k] = t;
+        const double w = t == RTW_METAL ? m[3] : (t == RTW_DIELECTRIC ? m[4] : 0.0);
+        reinterpret_cast<R4*>(b + o_mp)[k] = R4{(R)m[0], (R)m[1], (R)m[2], (R)w};
+    }
+    for (uint32_t k = 0; k < s->n_lights; ++k) {
+        const double* p = s->lights + 4 * k;
+        reinterpret_cast<R4*>(b + o_li)[k] = R4{(R)p[0], (R)p[1], (R)p[2], (R)p[3]};
+    }
+    ds->sph = reinterpret_cast<const R4*>(base + o_sph);
+    ds->sph_r = reinterpret_cast<const R*>(base + o_r);
+    ds->sph_mat = reinterpret_cast<const uint32_t*>(base + o_smat);
+    ds->planes = reinterpret_cast<const R*>(base + o_pl);
+    ds->plane_mat = reinterpret_cast<const uint32_t*>(base + o_pmat);
+    ds->mat_type = reinterpret_cast<const uint32_t*>(base + o_mt);
+    ds->mat_p = reinterpret_cast<const R4*>(base + o_mp);
+    ds->lights = reinterpret_cast<const R4*>(base + o_li);
+    ds->bvh = nullptr;
+    ds->n_sph = s->n_spheres;
+    ds->n_planes = s->n_planes;
+    ds->n_mat = s->n_materials;
+    ds->n_lights = s->n_lights;
+    ds->n_nodes = 0;
+    return blob;
+}
+
+int validate_scene(rtw_ctx* c, const rtw_scene* s) {
+    if (!s) return fail(c, RTW_E_INVALID, "scene is NULL");
+    if ((s->n_spheres && (!s->spheres || !s->sphere_mat)) || (s->n_planes && (!s->planes || !s->plane_mat)) ||
+        (s->n_materials && (!s->mat_type || !s->mat_params)) || (s->n_lights && !s->lights))
+        return fail(c, RTW_E_INVALID, "scene array pointer is NULL");
+    bool lambertian = false;
+    for (uint32_t k = 0; k < s->n_materials; ++k) {
+        if (s->mat_type[k] > RTW_INVISIBLE) return fail(c, RTW_E_INVALID, "unknown material type");
+        lambertian |= s->mat_type[k] == RTW_LAMBERTIAN;
+    }
+    for (uint32_t k = 0; k < s->n_spheres; ++k)
+        if (s->sphere_mat[k] >= s->n_materials) return fail(c, RTW_E_INVALID, "sphere material id out of range");
+    for (uint32_t k = 0; k < s->n_planes; ++k)
+        if (s->plane_mat[k] >= s->n_materials) return fail(c, RTW_E_INVALID, "plane material id out of range");
+    if (lambertian && s->n_lights == 0)
+        return fail(c, RTW_E_NO_LIGHTS, "Lambertian material with an empty light list "
+                                        "(the reference panics: HittableList shouldn't be empty)");
+    return RTW_OK;
+}
+
+int ensure(rtw_ctx* c, void** buf, size_t* cap, size_t bytes) {
+    if (*cap >= bytes) return RTW_OK;
+    if (*buf) (void)hipFree(*buf);
+    *buf = nullptr;
+    *cap = 0;
+    HIP_TRY(c, hipMalloc(buf, bytes));
+    *cap = bytes;
+    return RTW_OK;
+}
+
+uint32_t local_tile_rows(uint32_t tiles_y, uint32_t rank, uint32_t nranks) {
+    return rank < tiles_y ? (tiles_y - rank + nranks - 1) / nranks : 0;
+}
+
+template <typename R>
+void fill_camera(rtw::KParams<R>& p, const rtw_camera* cam) {
+    for (int k = 0; k < 3; ++k) {
+        p.center[k] = (R)cam->center[k];
+        p.p00[k] = (R)cam->pixel00_loc[k];
+        p.du[k] = (R)cam->pixel_delta_u[k];
+        p.dv[k] = (R)cam->pixel_delta_v[k];
+        p.disk_u[k] = (R)cam->defocus_disk_u[k];
+        p.disk_v[k] = (R)cam->defocus_disk_v[k];
+        p.bg[k] = (R)cam->background[k];
+    }
+    // Uniform::new_inclusive(-0.5, 0.5) scale (rand 0.8.6)
+    double max_rand = 1.0 - 2.220446049250313080847e-16;
+    double scale = (0.5 - -0.5) / max_rand;
+    while (scale * max_rand + -0.5 > 0.5) scale = nextafter(scale, 0.0);
+    p.u_scale = (R)scale;
+    p.defocus = cam->defocus_angle > 2.220446049250313080847e-16 ? 1u : 0u;
+    p.W = cam->image_width;
+    p.H = cam->image_height;
+    p.spp = cam->samples_per_pixel;
+    p.max_depth = cam->max_depth;
+}
+
+template <typename R>
+int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t rank, uint32_t nranks,
+                    void* d_out, size_t out_bytes, hipStream_t stream) {
+    rtw::KParams<R> p{};
+    p.sc = *reinterpret_cast<const rtw::DevScene<R>*>(
+        std::is_same<R, float>::value ? (const void*)&c->sc32 : (const void*)&c->sc64);
+    fill_camera(p, cam);
+    p.seed = seed;
+    p.rank = rank;
+    p.nranks = nranks;
+    p.tiles_x = (p.W + rtw::kTile - 1) / rtw::kTile;
+    const uint32_t tiles_y = (p.H + rtw::kTile - 1) / rtw::kTile;
+    p.n_local_tiles = local_tile_rows(tiles_y, rank, nranks) * p.tiles_x;
+    const size_t need_out = (size_t)rtw_rows_for_rank(p.H, rank, nranks) * p.W * 3 * sizeof(R);
+    if (out_bytes < need_out) return fail(c, RTW_E_INVALID, "d_out is smaller than rows_for_rank*W*3");
+    // Work items = (tile, chunk of samples).  Enough items to keep the
+    // dispatcher busy to the end; chunks no smaller than 8 samples.
+    uint32_t chunk = c->chunk;
+    if (chunk == 0) {
+        const uint64_t target_items = 1u << 17;
+        uint64_t n_chunks = p.n_local_tiles ? (target_items + p.n_local_tiles - 1) / p.n_local_tiles : 1;
+        n_chunks = std::max<uint64_t>(1, std::min<uint64_t>(n_chunks, (p.spp + 7) / 8));
+        chunk = (uint32_t)((p.spp + n_chunks - 1) / n_chunks);
+    }
+    chunk = std::max<uint32_t>(1, std::min<uint32_t>(chunk, std::max<uint32_t>(p.spp, 1)));
+    p.chunk = chunk;
+    p.n_chunks = p.spp ? (p.spp + chunk - 1) / chunk : 0;
+    p.n_items = p.n_local_tiles * p.n_chunks;
+    const size_t partial_bytes = std::max<size_t>((size_t)p.n_chunks * p.n_local_tiles * 64 * 3 * sizeof(R), 64);
+    int rc = ensure(c, &c->d_partial, &c->partial_cap, partial_bytes);
+    if (rc) return rc;
+    p.partial = reinterpret_cast<R*>(c->d_partial);
+    p.counters = c->d_counters;
+    if (!stream) stream = c->stream;
+    HIP_TRY(c, hipMemsetAsync(c->d_counters, 0, 2 * sizeof(unsigned long long), stream));
+    if (p.spp == 0) {
+        HIP_TRY(c, hipMemsetAsync(d_out, 0, need_out, stream));
+        return RTW_OK;
+    }
+    const size_t lds = (size_t)(p.sc.n_sph + p.sc.n_lights) * sizeof(rtw::R4<R>);
+    int accel = c->accel == RTW_ACCEL_AUTO ? RTW_ACCEL_BRUTE : c->accel;
+    hipEvent_t* ev = c->ring[c->n_renders % rtw_ctx::kRing];
+    HIP_TRY(c, hipEventRecord(c->ev0, stream));
+    HIP_TRY(c, hipEventRecord(ev[0], stream));
+    int lrc;
+    if constexpr (std::is_same<R, float>::value)
+        lrc = rtw::launch_render_f32(p, accel, lds <= kLdsLimit ? lds : 0, reinterpret_cast<float*>(d_out), stream, ev[1]);
+    else
+        lrc = rtw::launch_render_f64(p, accel, lds <= kLdsLimit ? lds : 0, reinterpret_cast<double*>(d_out), stream, ev[1]);
+    if (lrc) return fail(c, RTW_E_DEVICE, std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
+    HIP_TRY(c, hipEventRecord(c->ev1, stream));
+    HIP_TRY(c, hipEventRecord(ev[2], stream));
+    ++c->n_renders;
+    c->last = rtw_stats{};
+    c->last.samples = (uint64_t)rtw_rows_for_rank(p.H, rank, nranks) * p.W * p.spp;
+    c->last.accel = (uint32_t)accel;
+    c->last.chunk = chunk;
+    return RTW_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rtw_abi_version(void) { return RTW_ABI_VERSION; }
+
+rtw_ctx* rtw_create(int device, int precision) {
+    if (precision != RTW_F32 && precision != RTW_F64) return nullptr;
+    rtw_ctx* c = new (std::nothrow) rtw_ctx();
+    if (!c) return nullptr;
+    c->device = device;
+    c->precision = precision;
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&c->d_counters), 4 * sizeof(unsigned long long)) != hipSuccess) {
+        rtw_destroy(c);
+        return nullptr;
+    }
+    for (auto& tri : c->ring)
+        for (auto& e : tri)
+            if (hipEventCreate(&e) != hipSuccess) {
+                rtw_destroy(c);
+                return nullptr;
+            }
+    if (false) {
+        rtw_destroy(c);
+        return nullptr;
+    }
+    return c;
+}
+
+void rtw_destroy(rtw_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->d_scene) (void)hipFree(c->d_scene);
+    if (c->d_partial) (void)hipFree(c->d_partial);
+    if (c->d_out) (void)hipFree(c->d_out);
+    if (c->d_counters) (void)hipFree(c->d_counters);
+    for (auto& tri : c->ring)
+        for (auto& e : tri)
+            if (e) (void)hipEventDestroy(e);
+    if (c->ev0) (void)hipEventDestroy(c->ev0);
+    if (c->ev1) (void)hipEventDestroy(c->ev1);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+const char* rtw_last_error(const rtw_ctx* c) { return c ? c->err.c_str() : "null context"; }
+int rtw_precision(const rtw_ctx* c) { return c ? c->precision : -1; }
+
+int rtw_set_chunk(rtw_ctx* c, uint32_t chunk) {
+    if (!c) return RTW_E_INVALID;
+    c->chunk = chunk;
+    return RTW_OK;
+}
+int rtw_set_accel(rtw_ctx* c, int accel) {
+    if (!c) return RTW_E_INVALID;
+    if (accel < RTW_ACCEL_AUTO || accel > RTW_ACCEL_BRUTE) return fail(c, RTW_E_UNSUPPORTED, "accel not available");
+    c->accel = accel;
+    return RTW_OK;
+}
+
+void rtw_camera_builder_default(rtw_camera_builder* b) {
+    // CameraBuilder::new(), camera.rs:45-60
+    memset(b, 0, sizeof(*b));
+    b->samples_per_pixel = 10;
+    b->max_depth = 10;
+    b->vfov = 90.0;
+    b->lookat[2] = -1.0;
+    b->vup[1] = 1.0;
+    b->defocus_angle = 0.0;
+    b->focus_dist = 10.0;
+}
+
+static uint32_t round_u32(double x) {
+    // f64::round (half away from zero) then `as u32` (saturating, NaN -> 0)
+    double r = round(x);
+    if (!(r > 0.0)) return 0;
+    if (r >= 4294967295.0) return 4294967295u;
+    return (uint32_t)r;
+}
+
+int rtw_camera_build(const rtw_camera_builder* b, rtw_camera* out) {
+    // CameraBuilder::build, camera.rs:114-218
+    if (!b || !out) return RTW_E_INVALID;
+    struct V { double x, y, z; };
+    auto sub = [](V a, V c) { return V{a.x - c.x, a.y - c.y, a.z - c.z}; };
+    auto add = [](V a, V c) { return V{a.x + c.x, a.y + c.y, a.z + c.z}; };
+    auto mul = [](V a, double s) { return V{a.x * s, a.y * s, a.z * s}; };
+    auto dv = [](V a, double s) { return V{a.x / s, a.y / s, a.z / s}; };
+    auto dot = [](V a, V c) { return a.x * c.x + a.y * c.y + a.z * c.z; };
+    auto cross = [](V a, V c) {
+        return V{a.y * c.z - a.z * c.y, a.z * c.x - a.x * c.z, a.x * c.y - a.y * c.x};
+    };
+    auto norm = [&](V a) { return dv(a, sqrt(dot(a, a))); };
+    auto ld = [](const double* p) { return V{p[0], p[1], p[2]}; };
+    auto st = [](double* p, V v) { p[0] = v.x; p[1] = v.y; p[2] = v.z; };
+
+    const bool ha = b->has_aspect_ratio, hh = b->has_image_height, hw = b->has_image_width;
+    double aspect;
+    uint32_t H, W;
+    if (!ha && !hh && !hw) { aspect = 1.0; H = 100; W = 100; }
+    else if (!ha && !hh && hw) { aspect = 1.0; H = b->image_width; W = b->image_width; }
+    else if (!ha && hh && !hw) { aspect = 1.0; H = b->image_height; W = b->image_height; }
+    else if (ha && !hh && !hw) { aspect = b->aspect_ratio; H = round_u32(100.0 / b->aspect_ratio); W = 100; }
+    else if (!ha && hh && hw) { aspect = (double)b->image_width / (double)b->image_height; H = b->image_height; W = b->image_width; }
+    else if (ha && !hh && hw) { aspect = b->aspect_ratio; H = round_u32((double)b->image_width / b->aspect_ratio); W = b->image_width; }
+    else if (ha && hh && !hw) { aspect = b->aspect_ratio; H = b->image_height; W = round_u32((double)b->image_height * b->aspect_ratio); }
+    else { aspect = b->aspect_ratio; H = b->image_height; W = b->image_width; }
+
+    const double kPi = 3.14159265358979323846;
+    V center = ld(b->lookfrom);
+    double theta = b->vfov * (kPi / 180.0);   // f64::to_radians
+    double h = tan(theta / 2.0);
+    double vh = 2.0 * h * b->focus_dist;
+    double vw = vh * aspect;
+    V w = sub(ld(b->lookfrom), ld(b->lookat));
+    V c0 = cross(ld(b->vup), w);
+    if (fabs(c0.x) < 1e-8 && fabs(c0.y) < 1e-8 && fabs(c0.z) < 1e-8) w = add(w, V{0.1, 0.0, 0.0});
+    w = norm(w);
+    V u = norm(cross(ld(b->vup), w));
+    V v = cross(w, u);
+    V vu = mul(u, vw), vv = mul(v, vh);
+    V du = dv(vu, (double)W), dvv = dv(vv, (double)H);
+    V ul = sub(sub(sub(center, mul(w, b->focus_dist)), dv(vu, 2.0)), dv(vv, 2.0));
+    V p00 = add(ul, dv(add(du, dvv), 2.0));
+    double rad = tan(b->defocus_angle / 2.0) * b->focus_dist;
+    memset(out, 0, sizeof(*out));
+    out->image_width = W;
+    out->image_height = H;
+    out->samples_per_pixel = b->samples_per_pixel;
+    out->max_depth = b->max_depth;
+    memcpy(out->background, b->background, sizeof(out->background));
+    out->defocus_angle = b->defocus_angle;
+    st(out->center, center);
+    st(out->pixel00_loc, p00);
+    st(out->pixel_delta_u, du);
+    st(out->pixel_delta_v, dvv);
+    st(out->defocus_disk_u, mul(u, rad));
+    st(out->defocus_disk_v, mul(v, rad));
+    return RTW_OK;
+}
+
+int rtw_set_scene(rtw_ctx* c, const rtw_scene* s) {
+    if (!c) return RTW_E_INVALID;
+    int rc = validate_scene(c, s);
+    if (rc) return rc;
+    HIP_TRY(c, hipSetDevice(c->device));
+    // size the blob first (the pointers are fixed up against the allocation)
+    rtw::DevScene<float> tmp32{};
+    rtw::DevScene<double> tmp64{};
+    std::vector<unsigned char> blob = c->precision == RTW_F32 ? stage_scene<float>(s, &tmp32, 0)
+                                                               : stage_scene<double>(s, &tmp64, 0);
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    if (c->scene_bytes < blob.size()) {
+        if (c->d_scene) (void)hipFree(c->d_scene);
+        c->d_scene = nullptr;
+        c->scene_bytes = 0;
+        HIP_TRY(c, hipMalloc(&c->d_scene, blob.size()));
+        c->scene_bytes = blob.size();
+    }
+    if (c->precision == RTW_F32)
+        blob = stage_scene<float>(s, &c->sc32, reinterpret_cast<uintptr_t>(c->d_scene));
+    else
+        blob = stage_scene<double>(s, &c->sc64, reinterpret_cast<uintptr_t>(c->d_scene));
+    HIP_TRY(c, hipMemcpy(c->d_scene, blob.data(), blob.size(), hipMemcpyHostToDevice));
+    c->has_scene = true;
+    return RTW_OK;
+}
+
+uint32_t rtw_tile_rows(void) { return rtw::kTile; }
+
+uint32_t rtw_rows_for_rank(uint32_t H, uint32_t rank, uint32_t nranks) {
+    if (nranks == 0) return 0;
+    const uint32_t tiles_y = (H + rtw::kTile - 1) / rtw::kTile;
+    uint32_t rows = 0;
+    for (uint32_t t = rank; t < tiles_y; t += nranks) rows += std::min(rtw::kTile, H - t * rtw::kTile);
+    return rows;
+}
+
+int rtw_render_device(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t rank, uint32_t nranks,
+                      void* d_out, size_t out_bytes, void* stream) {
+    if (!c || !cam || !d_out || nranks == 0 || rank >= nranks) return fail(c, RTW_E_INVALID, "bad argument");
+    if (!c->has_scene) return fail(c, RTW_E_NO_SCENE, "rtw_set_scene was not called");
+    HIP_TRY(c, hipSetDevice(c->device));
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    return c->precision == RTW_F32 ? render_device_t<float>(c, cam, seed, rank, nranks, d_out, out_bytes, s)
+                                   : render_device_t<double>(c, cam, seed, rank, nranks, d_out, out_bytes, s);
+}
+
+int rtw_get_stats(rtw_ctx* c, rtw_stats* out) {
+    if (!c || !out) return RTW_E_INVALID;
+    HIP_TRY(c, hipSetDevice(c->device));
+    HIP_TRY(c, hipEventSynchronize(c->ev1));
+    unsigned long long h[2] = {0, 0};
+    HIP_TRY(c, hipMemcpy(h, c->d_counters, sizeof h, hipMemcpyDeviceToHost));
+    float ms = 0.f;
+    HIP_TRY(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
+    c->last.segments = h[0];
+    c->last.lambertian = h[1];
+    c->last.kernel_ms = ms;
+    *out = c->last;
+    return RTW_OK;
+}
+
+int rtw_get_timings(rtw_ctx* c, float* render_ms, float* total_ms, int max) {
+    if (!c || max < 0) return RTW_E_INVALID;
+    HIP_TRY(c, hipSetDevice(c->device));
+    const int n = (int)std::min<uint64_t>({(uint64_t)max, c->n_renders, (uint64_t)rtw_ctx::kRing});
+    for (int k = 0; k < n; ++k) {
+        hipEvent_t* ev = c->ring[(c->n_renders - n + k) % rtw_ctx::kRing];
+        HIP_TRY(c, hipEventSynchronize(ev[2]));
+        float a = 0.f, b = 0.f;
+        HIP_TRY(c, hipEventElapsedTime(&a, ev[0], ev[1]));
+        HIP_TRY(c, hipEventElapsedTime(&b, ev[0], ev[2]));
+        if (render_ms) render_ms[k] = a;
+        if (total_ms) total_ms[k] = b;
+    }
+    return n;
+}
+
+int rtw_render(rtw_ctx* c, const rtw_camera* cam, const rtw_scene* scene, uint64_t seed, double* out_sum,
+               rtw_stats* stats) {
+    if (!c || !cam || !out_sum) return fail(c, RTW_E_INVALID, "bad argument");
+    if (scene) {
+        int rc = rtw_set_scene(c, scene);
+        if (rc) return rc;
+    }
+    if (!c->has_scene) return fail(c, RTW_E_NO_SCENE, "no scene");
+    const size_t esz = c->precision == RTW_F32 ? sizeof(float) : sizeof(double);
+    const size_t n = (size_t)cam->image_width * cam->image_height * 3;
+    int rc = ensure(c, &c->d_out, &c->out_cap, std::max<size_t>(n * esz, 64));
+    if (rc) return rc;
+    rc = rtw_render_device(c, cam, seed, 0, 1, c->d_out, c->out_cap, nullptr);
+    if (rc) return rc;
+    c->h_out.resize(n * esz);
+    if (n) HIP_TRY(c, hipMemcpyAsync(c->h_out.data(), c->d_out, n * esz, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    if (c->precision == RTW_F32) {
+        const float* f = reinterpret_cast<const float*>(c->h_out.data());
+        for (size_t k = 0; k < n; ++k) out_sum[k] = (double)f[k];
+    } else {
+        memcpy(out_sum, c->h_out.data(), n * sizeof(double));
+    }
+    rtw_stats st{};
+    rc = rtw_get_stats(c, &st);
+    if (rc) return rc;
+    if (stats) *stats = st;
+    return RTW_OK;
+}
+
+// ------------------------------------------------------------ scenes::simple
+struct rtw_world {
+    rtw::FlatScene flat;
+    rtw_scene view;
+    rtw_camera_builder cam;
+};
+
+rtw_world* rtw_scene_simple(uint64_t seed, int grid_n) {
+    if (grid_n < 0) return nullptr;
+    try {
+        auto t = rtw::scenes::simple(seed, grid_n);
+        rtw_world* w = new rtw_world();
+        w->flat = rtw::flatten(std::get<0>(t), std::get<1>(t));
+        w->view = w->flat.view();
+        w->cam = std::get<2>(t).raw();
+        return w;
+    } catch (...) {
+        return nullptr;
+    }
+}
+const rtw_scene* rtw_world_scene(const rtw_world* w) { return w ? &w->view : nullptr; }
+void rtw_world_camera_builder(const rtw_world* w, rtw_camera_builder* out) {
+    if (w && out) *out = w->cam;
+}
+void rtw_world_free(rtw_world* w) { delete w; }
+
+// ------------------------------------------------------------ output encoding
+static uint8_t to_u8(double x) {
+    // (256. * x.clamp(0., 1.)) as u8 -- saturating cast, NaN -> 0 (colour.rs:32-34)
+    double c = x != x ? x : (x < 0.0 ? 0.0 : (x > 1.0 ? 1.0 : x));
+    double v = 256.0 * c;
+    if (!(v > 0.0)) return 0;
+    if (v >= 255.0) return 255;
+    return (uint8_t)v;
+}
+
+int rtw_encode_rgb8(const double* sums, uint32_t W, uint32_t H, uint32_t spp, uint8_t* out) {
+    if ((!sums || !out) && W && H) return RTW_E_INVALID;
+    // write_colour, colour.rs:14-36: scale = (spp as f64).recip(); sqrt(c * scale)
+    const double scale = 1.0 / (double)(int32_t)spp;
+    for (uint32_t r = 0; r < H; ++r) {
+        const uint32_t j = H - 1 - r;   // main.rs:97-104 writes rows in reverse
+        for (uint32_t i = 0; i < W; ++i)
+            for (int k = 0; k < 3; ++k)
+                out[((size_t)r * W + i) * 3 + k] = to_u8(sqrt(sums[((size_t)j * W + i) * 3 + k] * scale));
+    }
+    return RTW_OK;
+}
+
+int rtw_write_ppm(const char* path, const double* sums, uint32_t W, uint32_t H, uint32_t spp) {
+    if (!path) return RTW_E_INVALID;
+    std::vector<uint8_t> rgb((size_t)W * H * 3);
+    int rc = rtw_encode_rgb8(sums, W, H, spp, rgb.data());
+    if (rc) return rc;
+    FILE* f = fopen(path, "wb");
+    if (!f) return RTW_E_INVALID;
+    int n = fprintf(f, "P3\n%u %u\n255\n", W, H);
+    for (size_t p = 0; p < (size_t)W * H; ++p)
+        n += fprintf(f, "%u %u %u\n", rgb[3 * p], rgb[3 * p + 1], rgb[3 * p + 2]);
+    fclose(f);
+    return n;
+}
+
+}  // extern "C"

@@ -1,0 +1,177 @@
+// rtw_host.hpp -- C++ host mirror of the reference's interface for the hot
+// path: the types a caller of Camera::render builds (world + lights lists,
+// materials, CameraBuilder) and the scenes::simple generator, flattened to the
+// C-ABI's SoA rtw_scene and rendered by the gfx950 kernels through rtw.h.
+//
+// Mirrors (paths relative to N9199/ray_tracing_weekend):
+//   CameraBuilder / Camera        shared/src/camera.rs:28-261
+//   Camera::render(world, lights) shared/src/camera.rs:295-297
+//   HittableList::add             shared/src/hittable_collections/hittable_list.rs:270-294
+//   Sphere / Plane                shared/src/entities/sphere.rs:24-47, plane.rs:20-38
+//   Lambertian/Metal/Dialectric/Invisible   shared/src/material.rs:321-488
+//   SampledColour (+ Display)     shared/src/colour.rs:14-36, 136-148
+//   scenes::simple                scenes/src/lib.rs:155-233
+#pragma once
+
+#include <stdint.h>
+
+#include <array>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <tuple>
+#include <vector>
+
+#include "../../../include/rtw.h"
+
+namespace rtw {
+
+struct Vec3 {
+    double x = 0, y = 0, z = 0;
+};
+using Point3 = Vec3;
+using Colour = Vec3;
+
+// One material record.  DynMaterial in the reference is a pointer to a trait
+// object; here it is a small value type with the parameters the kernels read.
+struct Material {
+    uint32_t type = RTW_INVISIBLE;
+    Colour albedo{};
+    double fuzz = 0.0;
+    double ior = 0.0;
+
+    static Material lambertian(Colour albedo) { return {RTW_LAMBERTIAN, albedo, 0.0, 0.0}; }
+    static Material metal(Colour albedo, double fuzz) { return {RTW_METAL, albedo, fuzz, 0.0}; }
+    static Material dialectric(double ior) { return {RTW_DIELECTRIC, {1, 1, 1}, 0.0, ior}; }
+    static Material invisible() { return {RTW_INVISIBLE, {0, 0, 0}, 0.0, 0.0}; }
+};
+
+struct Sphere {
+    Point3 center;
+    double radius = 0;
+    Material mat;
+};
+
+struct Plane {
+    Point3 point;
+    Vec3 normal;  // normalized at construction, plane.rs:175
+    Material mat;
+    Plane(Point3 p, Vec3 n, Material m);
+};
+
+// A world or light list.  Only the primitives of the reference's hot path
+// (Sphere, Plane) are representable; Quad/Triangle/Cuboid/Transformed are
+// outside this build's scope.
+class HittableList {
+   public:
+    void add(const Sphere& s) { spheres_.push_back(s); }
+    void add(const Plane& p) { planes_.push_back(p); }
+    size_t len() const { return spheres_.size() + planes_.size(); }
+    bool is_empty() const { return len() == 0; }
+    const std::vector<Sphere>& spheres() const { return spheres_; }
+    const std::vector<Plane>& planes() const { return planes_; }
+
+   private:
+    std::vector<Sphere> spheres_;
+    std::vector<Plane> planes_;
+};
+
+// Flattened (SoA) world + lights; owns the arrays an rtw_scene points into.
+struct FlatScene {
+    std::vector<double> spheres, planes, mat_params, lights;
+    std::vector<uint32_t> sphere_mat, plane_mat, mat_type;
+    rtw_scene view() const;
+};
+// world's spheres/planes with one material record each; lights contribute
+// their sphere geometry only (their material is never consulted on the path).
+FlatScene flatten(const HittableList& world, const HittableList& lights);
+
+// SampledColour(sum, spp) -- colour.rs:136-148
+struct SampledColour {
+    Colour sum;
+    int32_t spp = 1;
+    std::array<uint8_t, 3> rgb8() const;   // write_colour, colour.rs:14-36
+    std::string to_string() const;         // Display: "r g b"
+};
+
+class Camera;
+
+class CameraBuilder {
+   public:
+    CameraBuilder();
+    CameraBuilder& with_aspect_ratio(double v) { b_.has_aspect_ratio = 1; b_.aspect_ratio = v; return *this; }
+    CameraBuilder& with_image_width(uint32_t v) { b_.has_image_width = 1; b_.image_width = v; return *this; }
+    CameraBuilder& with_image_height(uint32_t v) { b_.has_image_height = 1; b_.image_height = v; return *this; }
+    CameraBuilder& with_samples_per_pixel(uint32_t v) { b_.samples_per_pixel = v; return *this; }
+    CameraBuilder& with_max_depth(uint32_t v) { b_.max_depth = v; return *this; }
+    CameraBuilder& with_background(Colour c) { b_.background[0] = c.x; b_.background[1] = c.y; b_.background[2] = c.z; return *this; }
+    CameraBuilder& with_vfov(double v) { b_.vfov = v; return *this; }
+    CameraBuilder& with_lookfrom(Point3 p) { b_.lookfrom[0] = p.x; b_.lookfrom[1] = p.y; b_.lookfrom[2] = p.z; return *this; }
+    CameraBuilder& with_lookat(Point3 p) { b_.lookat[0] = p.x; b_.lookat[1] = p.y; b_.lookat[2] = p.z; return *this; }
+    CameraBuilder& with_vup(Vec3 v) { b_.vup[0] = v.x; b_.vup[1] = v.y; b_.vup[2] = v.z; return *this; }
+    CameraBuilder& with_defocus_angle(double v) { b_.defocus_angle = v; return *this; }
+    CameraBuilder& with_focus_dist(double v) { b_.focus_dist = v; return *this; }
+    Camera build() const;
+    const rtw_camera_builder& raw() const { return b_; }
+    explicit CameraBuilder(const rtw_camera_builder& b) : b_(b) {}
+
+   private:
+    rtw_camera_builder b_;
+};
+
+// Options for the device render that the reference has no equivalent of.
+struct RenderOptions {
+    uint64_t seed = 0x5EED0001ULL;  // the reference seeds from thread_rng (non-deterministic)
+    int device = 0;
+    int precision = RTW_F32;
+    int accel = RTW_ACCEL_AUTO;
+};
+
+class Camera {
+   public:
+    explicit Camera(const rtw_camera& c) : c_(c) {}
+    // Camera::render -- rows indexed [j][i], j = 0 the bottom row.
+    std::vector<std::vector<SampledColour>> render(const HittableList& world,
+                                                   const HittableList& lights,
+                                                   const RenderOptions& opt = {}) const;
+    // render_debug: the reference's sequential debug path; on the GPU it is the
+    // same render (there is no sequential mode to emulate).
+    std::vector<std::vector<SampledColour>> render_debug(const HittableList& world,
+                                                         const HittableList& lights,
+                                                         const RenderOptions& opt = {}) const {
+        return render(world, lights, opt);
+    }
+    const rtw_camera& raw() const { return c_; }
+
+   private:
+    rtw_camera c_;
+};
+
+namespace scenes {
+// scenes::simple restated with the build's seeded RNG; grid a, b in [-n, n).
+std::tuple<HittableList, HittableList, CameraBuilder> simple(uint64_t seed, int n = 11);
+}  // namespace scenes
+
+// host RNG used by the scene generator (the same xoshiro256++/splitmix64 and
+// rand 0.8.6 distributions as the device path)
+class HostRng {
+   public:
+    explicit HostRng(uint64_t seed);  // SmallRng::seed_from_u64
+    uint64_t next();
+    double standard();                               // Standard f64
+    double uniform_incl(double low, double high);    // Uniform::new_inclusive(low, high).sample
+
+   private:
+    uint64_t s_[4];
+};
+
+class Error : public std::runtime_error {
+   public:
+    Error(int code, const std::string& msg) : std::runtime_error(msg), code_(code) {}
+    int code() const { return code_; }
+
+   private:
+    int code_;
+};
+
+}  // namespace rtw

@@ -1,0 +1,16 @@
+// render_f32.hip -- speed-mode (f32) instantiation of the render kernels.
+// Built with -ffp-contract=fast (FMA) and native sqrt/rcp/rsq/sin/cos.
+#include "render_kernel.hpp"
+
+namespace rtw {
+
+int launch_render_f32(const KParams<float>& p, int accel, size_t lds_bytes, float* out,
+                      hipStream_t stream, hipEvent_t mid) {
+    if (lds_bytes > 65536)
+        (void)hipFuncSetAttribute(
+            reinterpret_cast<const void*>(&dev::render_brute_kernel<float, true>),
+            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
+    return launch_render_impl<float>(p, accel, lds_bytes, out, stream, mid);
+}
+
+}  // namespace rtw

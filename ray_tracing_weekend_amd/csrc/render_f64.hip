@@ -1,0 +1,17 @@
+// render_f64.hip -- parity-mode (f64) instantiation of the render kernels.
+// Built with -ffp-contract=off: every a*b+c rounds twice, in the reference's
+// operation order, so the output is bit-comparable with the CPU oracle.
+#include "render_kernel.hpp"
+
+namespace rtw {
+
+int launch_render_f64(const KParams<double>& p, int accel, size_t lds_bytes, double* out,
+                      hipStream_t stream, hipEvent_t mid) {
+    if (lds_bytes > 65536)
+        (void)hipFuncSetAttribute(
+            reinterpret_cast<const void*>(&dev::render_brute_kernel<double, true>),
+            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
+    return launch_render_impl<double>(p, accel, lds_bytes, out, stream, mid);
+}
+
+}  // namespace rtw

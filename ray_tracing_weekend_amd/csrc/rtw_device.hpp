@@ -1,0 +1,344 @@
+// rtw_device.hpp -- device-side math, RNG and sampling for the gfx950 render
+// kernels.  Templated on the arithmetic type R (float = speed mode, double =
+// parity mode).  Reference functions restated here are cited as
+// path:line relative to N9199/ray_tracing_weekend.
+//
+// Parity mode (R = double) is compiled with -ffp-contract=off and keeps the
+// reference's operation order exactly, so its results can be compared bit
+// for bit with the CPU oracle.  Speed mode (R = float) keeps the same
+// algorithm and RNG draw order but uses FMA contraction and the native
+// v_sqrt/v_rcp/v_rsq/v_sin/v_cos instructions.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace rtw {
+namespace dev {
+
+template <typename R>
+struct V3 {
+    R x, y, z;
+};
+
+template <typename R>
+__device__ __forceinline__ V3<R> mk(R x, R y, R z) { return V3<R>{x, y, z}; }
+template <typename R>
+__device__ __forceinline__ V3<R> operator+(V3<R> a, V3<R> b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+template <typename R>
+__device__ __forceinline__ V3<R> operator-(V3<R> a, V3<R> b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+template <typename R>
+__device__ __forceinline__ V3<R> operator-(V3<R> a) { return {-a.x, -a.y, -a.z}; }
+template <typename R>
+__device__ __forceinline__ V3<R> operator*(V3<R> a, R s) { return {a.x * s, a.y * s, a.z * s}; }
+template <typename R>
+__device__ __forceinline__ V3<R> operator*(V3<R> a, V3<R> b) { return {a.x * b.x, a.y * b.y, a.z * b.z}; }
+// vec.rs:70-72: (x*x' + y*y') + z*z'
+template <typename R>
+__device__ __forceinline__ R dot(V3<R> a, V3<R> b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+// vec.rs:76-82
+template <typename R>
+__device__ __forceinline__ V3<R> cross(V3<R> a, V3<R> b) {
+    return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
+}
+
+// ---------------------------------------------------------------------------
+// Precision-specific primitives
+// ---------------------------------------------------------------------------
+template <typename R>
+struct P;
+
+template <>
+struct P<double> {
+    static constexpr double kPi = 3.14159265358979323846;
+    static constexpr double kTau = 2.0 * 3.14159265358979323846;
+    static constexpr double kEps = 2.220446049250313080847e-16;  // f64::EPSILON
+    __device__ static __forceinline__ double sqrt_(double x) { return __builtin_sqrt(x); }
+    __device__ static __forceinline__ double div_(double a, double b) { return a / b; }
+    __device__ static __forceinline__ double over_pi(double a) { return a / kPi; }
+    __device__ static __forceinline__ double min_(double a, double b) { return __builtin_fmin(a, b); }
+    __device__ static __forceinline__ double max_(double a, double b) { return __builtin_fmax(a, b); }
+    // vec.rs:86-94: self / self.length()
+    __device__ static __forceinline__ V3<double> normalize(V3<double> a) {
+        double l = sqrt_(dot(a, a));
+        return {a.x / l, a.y / l, a.z / l};
+    }
+    __device__ static __forceinline__ V3<double> divs(V3<double> a, double s) {
+        return {a.x / s, a.y / s, a.z / s};
+    }
+    // rand 0.8.6 Standard for f64: (v >> 11) * 2^-53
+    __device__ static __forceinline__ double u_std(uint64_t v) {
+        return (1.0 / 9007199254740992.0) * (double)(v >> 11);
+    }
+    __device__ static __forceinline__ double unit12(uint64_t v) {
+        return __longlong_as_double((long long)((v >> 12) | 0x3FF0000000000000ULL));
+    }
+    // rand 0.8.6 Open01 for f64
+    __device__ static __forceinline__ double u_open01(uint64_t v) {
+        return unit12(v) - (1.0 - kEps / 2.0);
+    }
+    // rand 0.8.6 UniformFloat::sample: value0_1 * scale + low
+    __device__ static __forceinline__ double u_incl(uint64_t v, double low, double scale) {
+        double v01 = unit12(v) - 1.0;
+        return v01 * scale + low;
+    }
+    // fdlibm __kernel_sin / __kernel_cos after an exact quadrant reduction of r
+    // (identical arithmetic to the oracle's rtwo_sincos_2pi)
+    __device__ static __forceinline__ double k_sin(double x) {
+        const double S1 = -1.66666666666666324348e-01, S2 = 8.33333333332248946124e-03,
+                     S3 = -1.98412698298579493134e-04, S4 = 2.75573137070700676789e-06,
+                     S5 = -2.50507602534068634195e-08, S6 = 1.58969099521155010221e-10;
+        double z = x * x;
+        double v = z * x;
+        double r = S2 + z * (S3 + z * (S4 + z * (S5 + z * S6)));
+        return x + v * (S1 + z * r);
+    }
+    __device__ static __forceinline__ double k_cos(double x) {
+        const double C1 = 4.16666666666666019037e-02, C2 = -1.38888888888741095749e-03,
+                     C3 = 2.48015872894767294178e-05, C4 = -2.75573143513906633035e-07,
+                     C5 = 2.08757232129817482790e-09, C6 = -1.13596475577881948265e-11;
+        double z = x * x;
+        double r = z * (C1 + z * (C2 + z * (C3 + z * (C4 + z * (C5 + z * C6)))));
+        double ax = __builtin_fabs(x);
+        if (ax < 0.3) return 1.0 - (0.5 * z - (z * r));
+        double qx;
+        if (ax > 0.78125) {
+            qx = 0.28125;
+        } else {
+            unsigned long long b = (unsigned long long)__double_as_longlong(ax);
+            b = (b - 0x0020000000000000ULL) & 0xFFFFFFFF00000000ULL;
+            qx = __longlong_as_double((long long)b);
+        }
+        double hz = 0.5 * z - qx;
+        double a = 1.0 - qx;
+        return a - (hz - z * r);
+    }
+    __device__ static __forceinline__ void sincos_2pi(double r, double* s, double* c) {
+        double q = __builtin_rint(r * 4.0);
+        double f = r - q * 0.25;
+        double x = f * kTau;
+        double ks = k_sin(x), kc = k_cos(x);
+        switch (((long long)q) & 3) {
+            case 0: *s = ks; *c = kc; break;
+            case 1: *s = kc; *c = -ks; break;
+            case 2: *s = -ks; *c = -kc; break;
+            default: *s = -kc; *c = ks; break;
+        }
+    }
+};
+
+template <>
+struct P<float> {
+    static constexpr float kPi = 3.14159265358979323846f;
+    static constexpr float kInvPi = 0.318309886183790671538f;
+    static constexpr float kEps = 2.220446049250313080847e-16f;  // same t_min as f64 (2^-52)
+    __device__ static __forceinline__ float sqrt_(float x) { return __builtin_amdgcn_sqrtf(x); }
+    __device__ static __forceinline__ float div_(float a, float b) { return a * __builtin_amdgcn_rcpf(b); }
+    __device__ static __forceinline__ float over_pi(float a) { return a * kInvPi; }
+    __device__ static __forceinline__ float min_(float a, float b) { return __builtin_fminf(a, b); }
+    __device__ static __forceinline__ float max_(float a, float b) { return __builtin_fmaxf(a, b); }
+    __device__ static __forceinline__ V3<float> normalize(V3<float> a) {
+        float k = __builtin_amdgcn_rsqf(dot(a, a));
+        return {a.x * k, a.y * k, a.z * k};
+    }
+    __device__ static __forceinline__ V3<float> divs(V3<float> a, float s) {
+        float k = __builtin_amdgcn_rcpf(s);
+        return {a.x * k, a.y * k, a.z * k};
+    }
+    // The f32 draws are the top bits of the SAME 64-bit words the f64 path
+    // uses, so both precisions follow the same sample paths until rounding
+    // separates them.
+    __device__ static __forceinline__ float u_std(uint64_t v) {
+        return (float)(uint32_t)(v >> 40) * 5.9604644775390625e-08f;  // 2^-24
+    }
+    __device__ static __forceinline__ float u_open01(uint64_t v) {
+        return (float)(uint32_t)(v >> 41) * 1.1920928955078125e-07f + 5.9604644775390625e-08f;
+    }
+    __device__ static __forceinline__ float u_incl(uint64_t v, float low, float /*scale*/) {
+        return (float)(uint32_t)(v >> 40) * 5.9604644775390625e-08f + low;
+    }
+    // v_sin_f32 / v_cos_f32 take their argument in revolutions: sin(2*pi*r)
+    __device__ static __forceinline__ void sincos_2pi(float r, float* s, float* c) {
+        *s = __builtin_amdgcn_sinf(r);
+        *c = __builtin_amdgcn_cosf(r);
+    }
+};
+
+// ---------------------------------------------------------------------------
+// RNG: xoshiro256++ (rand 0.8.6 SmallRng) seeded per (pixel, sample) through
+// splitmix64 -- identical to the oracle's rtwo_rng_seed / rtwo_rng_next.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+__device__ __forceinline__ uint64_t rotl(uint64_t x, int k) { return (x << k) | (x >> (64 - k)); }
+
+struct Rng {
+    uint64_t s0, s1, s2, s3;
+    __device__ __forceinline__ void seed(uint64_t seed, uint64_t pixel, uint64_t sample) {
+        uint64_t k = mix64(seed + 0x9E3779B97F4A7C15ULL * (pixel + 1));
+        k = mix64(k ^ (0xD1B54A32D192ED03ULL * (sample + 1)));
+        k += 0x9E3779B97F4A7C15ULL; s0 = mix64(k);
+        k += 0x9E3779B97F4A7C15ULL; s1 = mix64(k);
+        k += 0x9E3779B97F4A7C15ULL; s2 = mix64(k);
+        k += 0x9E3779B97F4A7C15ULL; s3 = mix64(k);
+    }
+    __device__ __forceinline__ uint64_t next() {
+        uint64_t result = rotl(s0 + s3, 23) + s0;
+        uint64_t t = s1 << 17;
+        s2 ^= s0;
+        s3 ^= s1;
+        s1 ^= s2;
+        s0 ^= s3;
+        s2 ^= t;
+        s3 = rotl(s3, 45);
+        return result;
+    }
+    // gen_range(0..n) for u32 (rand 0.8.6 sample_single_inclusive), next_u32 = next >> 32
+    __device__ __forceinline__ uint32_t index(uint32_t n) {
+        uint32_t zone = (n << __builtin_clz(n)) - 1u;
+        for (;;) {
+            uint32_t v = (uint32_t)(next() >> 32);
+            uint64_t m = (uint64_t)v * (uint64_t)n;
+            if ((uint32_t)m <= zone) return (uint32_t)(m >> 32);
+        }
+    }
+};
+
+// ---------------------------------------------------------------------------
+// Geometry helpers
+// ---------------------------------------------------------------------------
+template <typename R>
+__device__ __forceinline__ V3<R> reflect(V3<R> v, V3<R> n) {   // vec.rs:105-107
+    R d = dot(v, n);
+    V3<R> n2 = n * (R)2;
+    return v - n2 * d;
+}
+template <typename R>
+__device__ __forceinline__ V3<R> refract(V3<R> v, V3<R> n, R eta) {   // vec.rs:111-116
+    R cos_theta = P<R>::min_(dot(v, -n), (R)1);
+    V3<R> perp = (v + n * cos_theta) * eta;
+    V3<R> par = n * (-(P<R>::sqrt_((R)1 - dot(perp, perp))));
+    return perp + par;
+}
+
+template <typename R>
+struct Onb {   // geometry/src/onb.rs:8-35
+    V3<R> u, v, w;
+    __device__ __forceinline__ explicit Onb(V3<R> n) {
+        w = P<R>::normalize(n);
+        V3<R> a = __builtin_fabs((double)w.x) > 0.9 ? mk<R>(0, 1, 0) : mk<R>(1, 0, 0);
+        v = P<R>::normalize(cross(w, a));
+        u = cross(w, v);
+    }
+    // (0..3).map(|i| e[i] * x[i]).sum() folds from Vec3::default()
+    __device__ __forceinline__ V3<R> transform(V3<R> x) const {
+        V3<R> acc = mk<R>(0, 0, 0);
+        acc = acc + u * x.x;
+        acc = acc + v * x.y;
+        acc = acc + w * x.z;
+        return acc;
+    }
+};
+
+// utils.rs:99-122 (UnitSphere, rejection + the 3-element shuffle)
+template <typename R>
+__device__ __forceinline__ V3<R> unit_sphere(Rng& g) {
+    for (;;) {
+        R in0 = (R)2 * P<R>::u_std(g.next()) - (R)1;
+        R in1 = (R)2 * P<R>::u_std(g.next()) - (R)1;
+        R in2 = (R)2 * P<R>::u_std(g.next()) - (R)1;
+        // SliceRandom::shuffle: i = 2 then i = 1, swap(i, gen_index(i + 1))
+        uint32_t j = g.index(3);
+        R t;
+        if (j == 0) { t = in2; in2 = in0; in0 = t; }
+        else if (j == 1) { t = in2; in2 = in1; in1 = t; }
+        j = g.index(2);
+        if (j == 0) { t = in1; in1 = in0; in0 = t; }
+        V3<R> out = mk(in0, in1, in2);
+        if (dot(out, out) < (R)1) return out;
+    }
+}
+// utils.rs:124-144
+template <typename R>
+__device__ __forceinline__ V3<R> unit_disk(Rng& g) {
+    for (;;) {
+        R x = (R)2 * P<R>::u_std(g.next()) - (R)1;
+        R z = (R)2 * P<R>::u_std(g.next()) - (R)1;
+        V3<R> out = mk<R>(x, 0, z);
+        if (dot(out, out) < (R)1) return out;
+    }
+}
+// utils.rs:146-161
+template <typename R>
+__device__ __forceinline__ V3<R> cosine_hemisphere(Rng& g) {
+    R r1 = P<R>::u_std(g.next());
+    R r2 = P<R>::u_std(g.next());
+    R s, c;
+    P<R>::sincos_2pi(r1, &s, &c);
+    R sq = P<R>::sqrt_(r2);
+    return mk(c * sq, s * sq, P<R>::sqrt_((R)1 - r2));
+}
+
+// Sphere::hit root selection, sphere.rs:61-80.  r2 = radius * radius.
+template <typename R>
+__device__ __forceinline__ bool sphere_t(V3<R> c, R r2, V3<R> o, V3<R> d, R tmin, R& t) {
+    V3<R> oc = o - c;
+    R a = dot(d, d);
+    R half_b = dot(d, oc);
+    R cc = dot(oc, oc) - r2;
+    R disc = half_b * half_b - a * cc;
+    if (!(disc > (R)0)) return false;
+    R sq = P<R>::sqrt_(disc);
+    R root = P<R>::div_(-half_b - sq, a);
+    if (!(tmin <= root && root <= (R)INFINITY)) {
+        root = P<R>::div_(-half_b + sq, a);
+        if (!(tmin <= root && root <= (R)INFINITY)) return false;
+    }
+    t = root;
+    return true;
+}
+
+// Sphere::pdf_value, sphere.rs:101-111
+template <typename R>
+__device__ __forceinline__ R sphere_pdf_value(V3<R> c, R radius, V3<R> o, V3<R> d) {
+    R t;
+    if (!sphere_t(c, radius * radius, o, d, (R)0, t)) return (R)0;
+    V3<R> co = c - o;
+    R dist2 = dot(co, co);
+    R cos_theta_max = P<R>::sqrt_((R)1 - P<R>::div_(radius * radius, dist2));
+    R solid_angle = ((R)2 * P<R>::kPi) * ((R)1 - cos_theta_max);
+    return P<R>::div_((R)1, solid_angle);
+}
+
+// Sphere::random, sphere.rs:114-127
+template <typename R>
+__device__ __forceinline__ V3<R> sphere_random(V3<R> c, R radius, V3<R> o, Rng& g) {
+    V3<R> direction = c - o;
+    R distance = P<R>::sqrt_(dot(direction, direction));
+    Onb<R> uvw(direction);
+    R r1 = P<R>::u_std(g.next());
+    R r2 = P<R>::u_std(g.next());
+    R z = (R)1 + r1 * (P<R>::sqrt_((R)1 - P<R>::div_(radius * radius, distance * distance)) - (R)1);
+    R s, cph;
+    P<R>::sincos_2pi(r2, &s, &cph);
+    R x = cph * P<R>::sqrt_((R)1 - z * z);
+    R y = s * P<R>::sqrt_((R)1 - z * z);
+    return uvw.transform(mk(x, y, z));
+}
+
+// Dialectric::reflectance, material.rs:450-454; powi(5) = x * ((x*x)*(x*x))
+template <typename R>
+__device__ __forceinline__ R reflectance(R cosine, R ref_idx) {
+    R r0 = P<R>::div_((R)1 - ref_idx, (R)1 + ref_idx);
+    r0 = r0 * r0;
+    R x = (R)1 - cosine;
+    R x2 = x * x;
+    R p5 = x * (x2 * x2);
+    return r0 + ((R)1 - r0) * p5;
+}
+
+}  // namespace dev
+}  // namespace rtw

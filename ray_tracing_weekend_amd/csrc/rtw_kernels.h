@@ -1,0 +1,81 @@
+// rtw_kernels.h -- host-visible description of the device scene layout and the
+// launch entry points of the gfx950 render kernels (render_f32.hip /
+// render_f64.hip).  Included by the C-ABI (capi.cpp) and by the kernels.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace rtw {
+
+constexpr uint32_t kTile = 8;          // 8 x 8 pixel tile = one wavefront of 64 lanes
+constexpr uint32_t kWavesPerBlock = 4; // 256-thread workgroups, one tile item per wave
+constexpr uint32_t kBlock = 64 * kWavesPerBlock;
+
+template <typename R>
+struct alignas(4 * sizeof(R)) R4 {
+    R x, y, z, w;
+};
+
+// Device-resident scene, precision R.  HBM layout (all arrays tightly packed):
+//   sph      : n_sph   x R4 {cx, cy, cz, r*r}   -- staged into LDS by the brute kernel
+//   sph_r    : n_sph   x R  radius              -- read once per hit (normal)
+//   sph_mat  : n_sph   x u32 material id
+//   planes   : n_pl    x 6 R {px, py, pz, nx, ny, nz}
+//   plane_mat: n_pl    x u32
+//   mat_type : n_mat   x u32
+//   mat_p    : n_mat   x R4 {albedo r, g, b, fuzz | ior}
+//   lights   : n_li    x R4 {cx, cy, cz, r}     -- staged into LDS
+//   bvh      : n_nodes x BvhNode<R> (RTW_ACCEL_BVH only)
+template <typename R>
+struct BvhNode {
+    // two child boxes per node (children tested together, the classic
+    // "both children in one fetch" layout); a child index c >= 0 is an inner
+    // node, c < 0 encodes a leaf: spheres [first, first + count) of the
+    // BVH-ordered sphere arrays, first = (~c) >> 4, count = (~c) & 15.
+    R lo_x[2], lo_y[2], lo_z[2], hi_x[2], hi_y[2], hi_z[2];
+    int32_t child[2];
+    int32_t pad[2];
+};
+
+template <typename R>
+struct DevScene {
+    const R4<R>* sph;
+    const R* sph_r;
+    const uint32_t* sph_mat;
+    const R* planes;
+    const uint32_t* plane_mat;
+    const uint32_t* mat_type;
+    const R4<R>* mat_p;
+    const R4<R>* lights;
+    const BvhNode<R>* bvh;
+    uint32_t n_sph, n_planes, n_mat, n_lights, n_nodes;
+};
+
+template <typename R>
+struct KParams {
+    DevScene<R> sc;
+    R* partial;                       // [n_chunks][n_local_tiles][64][3] chunk sums
+    unsigned long long* counters;     // [0] segments, [1] lambertian
+    R center[3], p00[3], du[3], dv[3], disk_u[3], disk_v[3], bg[3];
+    R u_scale;                        // Uniform::new_inclusive(-0.5, 0.5) scale
+    uint64_t seed;
+    uint32_t defocus;                 // defocus_angle > f64::EPSILON
+    uint32_t W, H, spp, max_depth;
+    uint32_t chunk, n_chunks;
+    uint32_t tiles_x, n_local_tiles, rank, nranks;
+    uint32_t n_items;                 // n_local_tiles * n_chunks
+};
+
+// Host-side launch helpers (defined in render_f32.hip / render_f64.hip).
+// accel: 1 = brute force (LDS-staged sphere list when it fits), 2 = BVH.
+// `lds_bytes` = 0 selects the global-memory sphere loop.
+// `mid` (may be null) is recorded on `stream` between the render kernel and
+// the chunk reduction, so the render kernel can be timed on its own.
+int launch_render_f32(const KParams<float>& p, int accel, size_t lds_bytes, float* out,
+                      hipStream_t stream, hipEvent_t mid);
+int launch_render_f64(const KParams<double>& p, int accel, size_t lds_bytes, double* out,
+                      hipStream_t stream, hipEvent_t mid);
+
+}  // namespace rtw

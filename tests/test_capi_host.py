@@ -1,0 +1,161 @@
+"""CPU-side tests of the product: the C-ABI library loads and exports every
+symbol include/rtw.h declares; the C++ host mirror (CameraBuilder::build,
+scenes::simple, output encoding) agrees with the oracle restatement; nothing
+here launches a kernel."""
+import ctypes as C
+import os
+import re
+
+import numpy as np
+import pytest
+
+import ray_tracing_weekend_amd as rtw
+from ray_tracing_weekend_amd import _capi
+from oracle import oracle as O
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared_symbols():
+    text = open(os.path.join(ROOT, "include", "rtw.h")).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(rtw_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_library_exports_every_declared_symbol():
+    lib = C.CDLL(_capi.LIB_PATH)
+    names = _declared_symbols()
+    assert len(names) >= 20
+    for n in names:
+        assert hasattr(lib, n), n
+    assert {p[0] for p in _capi.PROTOTYPES} == set(names)
+
+
+def test_abi_version():
+    assert rtw._lib.rtw_abi_version() == 1
+
+
+def test_camera_builder_defaults_match_reference():
+    b = rtw.CameraBuilder().raw           # camera.rs:45-60
+    assert (b.samples_per_pixel, b.max_depth, b.vfov, b.focus_dist, b.defocus_angle) == (10, 10, 90.0, 10.0, 0.0)
+    assert list(b.lookat) == [0.0, 0.0, -1.0] and list(b.vup) == [0.0, 1.0, 0.0]
+    assert not (b.has_aspect_ratio or b.has_image_width or b.has_image_height)
+
+
+@pytest.mark.parametrize("kw", [
+    {},                                                    # (None, None, None) -> 100x100
+    {"image_width": 64},
+    {"image_height": 50},
+    {"aspect_ratio": 16 / 9},
+    {"image_width": 400, "image_height": 225},
+    {"aspect_ratio": 1.5, "image_width": 301},
+    {"aspect_ratio": 1.5, "image_height": 99},
+    {"aspect_ratio": 2.0, "image_width": 10, "image_height": 3},
+    {"lookfrom": (0, 5, 0), "lookat": (0, 0, 0)},         # vup x w ~ 0: the +0.1x nudge
+    {"defocus_angle": 0.6, "focus_dist": 3.4, "vfov": 20.0},
+])
+def test_camera_build_matches_oracle(kw):
+    b = rtw.CameraBuilder()
+    for k, v in kw.items():
+        getattr(b, "with_" + k)(v)
+    cam = b.build()
+    ocam = O.camera_build(**kw)
+    for name, _ in O.Camera._fields_:
+        a, c = getattr(cam.raw, name), getattr(ocam, name)
+        a = list(a) if isinstance(a, C.Array) else a
+        c = list(c) if isinstance(c, C.Array) else c
+        assert a == c, name
+
+
+def test_camera_known_answer_simple():
+    """Analytic pixel00 for scenes::simple's camera (camera.rs:161-188)."""
+    _, b = rtw.scenes.simple_soa()
+    cam = b.with_image_width(400).with_image_height(225).build()
+    lookfrom = np.array([10.0, 5.0, 10.0])
+    f = np.linalg.norm(lookfrom)
+    w = lookfrom / f
+    u = np.cross([0, 1, 0], w)
+    u /= np.linalg.norm(u)
+    v = np.cross(w, u)
+    vh = 2 * np.tan(np.radians(40) / 2) * f
+    vw = vh * 400 / 225
+    p00 = lookfrom - w * f - u * vw / 2 - v * vh / 2 + (u * vw / 400 + v * vh / 225) / 2
+    np.testing.assert_allclose(cam.pixel00_loc, p00, rtol=0, atol=1e-12)
+    np.testing.assert_allclose(cam.pixel_delta_u, u * vw / 400, atol=1e-14)
+    np.testing.assert_allclose(cam.pixel_delta_v, v * vh / 225, atol=1e-14)
+    assert cam.pixel_delta_v[1] > 0       # j = 0 is the bottom row
+
+
+@pytest.mark.parametrize("seed,n", [(0x5EED0001, 11), (1, 11), (42, 3), (7, 0), (0xFFFFFFFFFFFFFFFF, 2)])
+def test_scene_simple_matches_oracle(seed, n):
+    soa, _ = rtw.scenes.simple_soa(seed, n)
+    osc = O.scene_simple(seed, n)
+    for f in ("spheres", "sphere_mat", "planes", "plane_mat", "mat_type", "mat_params", "lights"):
+        np.testing.assert_array_equal(getattr(soa, f), getattr(osc, f), err_msg=f)
+
+
+def test_scene_simple_structure():
+    """scenes/src/lib.rs:155-233: 1 ground plane, <= 484 small + 3 big spheres,
+    one light per glass sphere, materials drawn from the stated ranges."""
+    soa, b = rtw.scenes.simple_soa(0x5EED0001)
+    assert len(soa.plane_mat) == 1 and list(soa.planes[0]) == [0, 0, 0, 0, 1, 0]
+    small = soa.spheres[:-3]
+    assert np.all(small[:, 1] == 0.2) and np.all(small[:, 3] == 0.2)
+    assert np.all(np.linalg.norm(small[:, :3] - [4, 0.2, 0], axis=1) > 0.9)
+    np.testing.assert_array_equal(soa.spheres[-3:], [[0, 1, 0, 1], [-4, 1, 0, 1], [4, 1, 0, 1]])
+    glass = soa.mat_type[soa.sphere_mat] == rtw.RTW_DIELECTRIC
+    assert glass.sum() == len(soa.lights)
+    mt, mp = soa.mat_type, soa.mat_params
+    metal = mp[mt == rtw.RTW_METAL]
+    assert np.all((metal[:, :3] >= 0.5) & (metal[:, :3] <= 1.0)) and np.all((metal[:, 3] >= 0) & (metal[:, 3] <= 0.5))
+    lamb = mp[mt == rtw.RTW_LAMBERTIAN]
+    assert np.all((lamb[:, :3] >= 0) & (lamb[:, :3] < 1))
+    assert b.raw.vfov == 40.0 and list(b.raw.background) == [1, 1, 1]
+    assert b.raw.focus_dist == pytest.approx(np.sqrt(225.0), abs=0)
+
+
+def test_python_flatten_matches_cpp_flatten():
+    world, lights, _ = rtw.scenes.simple(0x5EED0001)
+    soa, _ = rtw.scenes.simple_soa(0x5EED0001)
+    flat = rtw.flatten(world, lights)
+    for f in ("spheres", "sphere_mat", "planes", "plane_mat", "mat_type", "mat_params", "lights"):
+        np.testing.assert_array_equal(getattr(flat, f), getattr(soa, f), err_msg=f)
+
+
+def test_encode_rgb8_matches_write_colour():
+    """colour.rs:14-36: sqrt(sum/spp), clamp, (256 x) as u8 saturating, NaN -> 0;
+    main.rs:97-104 writes the rows top (j = H-1) first."""
+    sums = np.array([[[0.0, 1.0, 4.0], [np.nan, -1.0, 1e9]],
+                     [[0.999 * 4, 0.25 * 4, np.inf]]] * 1, dtype=object)
+    sums = np.array([[[0.0, 1.0, 4.0], [np.nan, -1.0, 1e9]],
+                     [[3.996, 1.0, np.inf], [2.0, 0.04, 0.0]]], np.float64)
+    out = rtw.encode_rgb8(sums, 4)
+
+    def ref(x):
+        v = np.sqrt(x / 4) if x >= 0 else np.nan
+        if np.isnan(v):
+            return 0
+        return min(255, int(256 * min(max(v, 0.0), 1.0)))
+
+    for r in range(2):
+        j = 1 - r
+        for i in range(2):
+            assert list(out[r, i]) == [ref(x) for x in sums[j, i]]
+
+
+def test_write_ppm_layout(tmp_path):
+    sums = np.zeros((2, 3, 3))
+    sums[0, :, 0] = 4.0          # bottom row red
+    p = tmp_path / "image.ppm"
+    rtw.write_ppm(str(p), sums, 4)
+    lines = p.read_text().splitlines()
+    assert lines[:3] == ["P3", "3 2", "255"]
+    assert lines[3:6] == ["0 0 0"] * 3 and lines[6:9] == ["255 0 0"] * 3
+
+
+def test_renderer_without_gpu_fails_loudly():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(rtw.RenderError):
+        rtw.Renderer()
