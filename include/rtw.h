@@ -121,6 +121,10 @@ int rtw_precision(const rtw_ctx *ctx);
 /* knobs: samples per work item (0 = auto), acceleration (RTW_ACCEL_*) */
 int rtw_set_chunk(rtw_ctx *ctx, uint32_t chunk);
 int rtw_set_accel(rtw_ctx *ctx, int accel);
+/* scheduling knobs (benchmarking): "chunk" (samples per item, 0 = auto),
+ * "auto_chunk", "group" (chunks per wave task, 0 = auto), "target_tasks",
+ * "lds" (1 = stage the sphere list in LDS when it fits, 0 = read it from HBM) */
+int rtw_set_tuning(rtw_ctx *ctx, const char *key, int64_t value);
 
 /* ---- CameraBuilder::build (camera.rs:114-218) ------------------------- */
 int rtw_camera_build(const rtw_camera_builder *builder, rtw_camera *out);

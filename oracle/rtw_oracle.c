@@ -682,14 +682,24 @@ static int world_hit(const ctx_t *cx, v3 o, v3 d, hitrec *rec) {
     int best = -1;
     double bt = INFINITY;
     if (cx->accel == RTWO_ACCEL_BRUTE) {
+        /* Every object is reached through bounded_hit (hittable.rs:190-196,
+         * utils.rs:172-179): its own AABB test comes first.  That matters for
+         * a plane, whose AABB pins the normal axis at coordinate 0 wherever
+         * the plane lies (plane.rs:218-242), and for a negative-radius sphere,
+         * whose AABB is inverted and never hit (sphere.rs:42-45).  For a
+         * positive-radius sphere the box contains the sphere, so the test is
+         * skipped (it can only disagree on rounding at the silhouette). */
         for (uint32_t k = 0; k < sc->n_planes; ++k) {
             double t;
-            if (plane_t(ld(sc->planes + 6 * k), ld(sc->planes + 6 * k + 3), o, d, tmin, tmax, &t) &&
+            aabb pb = object_box(sc, (int)k);
+            if (aabb_hit(&pb, o, d, tmin, tmax) &&
+                plane_t(ld(sc->planes + 6 * k), ld(sc->planes + 6 * k + 3), o, d, tmin, tmax, &t) &&
                 (best < 0 || t < bt)) { bt = t; best = (int)k; }
         }
         for (uint32_t k = 0; k < sc->n_spheres; ++k) {
             const double *s = sc->spheres + 4 * k;
             double t;
+            if (s[3] < 0.0) continue;
             if (sphere_t(ld(s), s[3], o, d, tmin, tmax, &t) && (best < 0 || t < bt)) {
                 bt = t; best = (int)(sc->n_planes + k);
             }

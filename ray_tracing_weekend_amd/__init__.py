@@ -290,6 +290,9 @@ class Renderer:
     def set_chunk(self, chunk: int):
         self._check(_lib.rtw_set_chunk(self.ctx, chunk), "rtw_set_chunk")
 
+    def set_tuning(self, key: str, value: int):
+        self._check(_lib.rtw_set_tuning(self.ctx, key.encode(), int(value)), "rtw_set_tuning")
+
     def set_accel(self, accel: int):
         self._check(_lib.rtw_set_accel(self.ctx, accel), "rtw_set_accel")
 

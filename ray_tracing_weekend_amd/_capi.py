@@ -71,6 +71,7 @@ PROTOTYPES = [
     ("rtw_precision", C.c_int, [C.c_void_p]),
     ("rtw_set_chunk", C.c_int, [C.c_void_p, C.c_uint32]),
     ("rtw_set_accel", C.c_int, [C.c_void_p, C.c_int]),
+    ("rtw_set_tuning", C.c_int, [C.c_void_p, C.c_char_p, C.c_int64]),
     ("rtw_camera_build", C.c_int, [C.POINTER(rtw_camera_builder), C.POINTER(rtw_camera)]),
     ("rtw_camera_builder_default", None, [C.POINTER(rtw_camera_builder)]),
     ("rtw_set_scene", C.c_int, [C.c_void_p, C.POINTER(rtw_scene)]),

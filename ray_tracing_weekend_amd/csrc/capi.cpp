@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "../../include/rtw.h"
+#include "host/bvh.hpp"
 #include "host/rtw_host.hpp"
 #include "rtw_kernels.h"
 
@@ -19,7 +20,12 @@ struct rtw_ctx {
     int device = 0;
     int precision = RTW_F32;
     int accel = RTW_ACCEL_AUTO;
-    uint32_t chunk = 0;
+    uint32_t chunk = 0;           // samples per item (0 = auto_chunk)
+    uint32_t auto_chunk = 8;
+    uint32_t group = 0;           // chunks per wave task (0 = from target_tasks)
+    uint64_t target_tasks = 1u << 17;
+    int world_pref = 1;           // 1: LDS-staged sphere list when it fits, 0: global
+    int auto_accel = RTW_ACCEL_BRUTE;   // what RTW_ACCEL_AUTO resolves to
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     // ring of per-render event triples: [start, after render kernel, after reduce]
@@ -76,21 +82,42 @@ std::vector<unsigned char> stage_scene(const rtw_scene* s, rtw::DevScene<R>* ds,
     const size_t o_sph = reserve(sizeof(R4) * s->n_spheres);
     const size_t o_r = reserve(sizeof(R) * s->n_spheres);
     const size_t o_smat = reserve(sizeof(uint32_t) * s->n_spheres);
-    const size_t o_pl = reserve(sizeof(R) * 6 * s->n_planes);
+    const size_t o_pl = reserve(sizeof(R) * 12 * s->n_planes);
     const size_t o_pmat = reserve(sizeof(uint32_t) * s->n_planes);
     const size_t o_mt = reserve(sizeof(uint32_t) * s->n_materials);
     const size_t o_mp = reserve(sizeof(R4) * s->n_materials);
     const size_t o_li = reserve(sizeof(R4) * s->n_lights);
+    // BVH over the spheres; boxes padded outward by a margin that absorbs the
+    // rounding of the slab test in precision R (it only ever culls)
+    const rtw::BvhBuild bb = rtw::build_bvh(s->spheres, s->n_spheres,
+                                            std::is_same<R, float>::value ? 1e-5 : 1e-12);
+    const size_t o_nodes = reserve(sizeof(rtw::BvhNode<R>) * bb.nodes.size());
+    const size_t o_bsph = reserve(sizeof(R4) * s->n_spheres);
+    const size_t o_bid = reserve(sizeof(uint32_t) * s->n_spheres);
     std::vector<unsigned char> blob(align_up(off, 64) + 64, 0);
     unsigned char* b = blob.data();
     for (uint32_t k = 0; k < s->n_spheres; ++k) {
         const double* p = s->spheres + 4 * k;
         R r = (R)p[3];
-        reinterpret_cast<R4*>(b + o_sph)[k] = R4{(R)p[0], (R)p[1], (R)p[2], r * r};
+        // a negative radius inverts the sphere's AABB, which bounded_hit never
+        // passes (sphere.rs:42-45): r^2 = -inf makes the discriminant -inf
+        reinterpret_cast<R4*>(b + o_sph)[k] = R4{(R)p[0], (R)p[1], (R)p[2], p[3] < 0 ? (R)-INFINITY : r * r};
         reinterpret_cast<R*>(b + o_r)[k] = r;
         reinterpret_cast<uint32_t*>(b + o_smat)[k] = s->sphere_mat[k];
     }
-    for (uint32_t k = 0; k < 6 * s->n_planes; ++k) reinterpret_cast<R*>(b + o_pl)[k] = (R)s->planes[k];
+    for (uint32_t k = 0; k < s->n_planes; ++k) {
+        // {point, normal, AABB lo, AABB hi}: Plane::get_aabbox (plane.rs:218-242)
+        // pins the normal axis at 0 and leaves the others infinite
+        const double* pl = s->planes + 6 * k;
+        const double e = 2.220446049250313080847e-16;
+        const bool fx = fabs(pl[5]) < e && fabs(pl[4]) < e, fy = fabs(pl[3]) < e && fabs(pl[5]) < e,
+                   fz = fabs(pl[3]) < e && fabs(pl[4]) < e;
+        const double box[6] = {fx ? 0.0 : -INFINITY, fy ? 0.0 : -INFINITY, fz ? 0.0 : -INFINITY,
+                               fx ? 0.0 : INFINITY, fy ? 0.0 : INFINITY, fz ? 0.0 : INFINITY};
+        R* dst = reinterpret_cast<R*>(b + o_pl) + 12 * k;
+        for (int q = 0; q < 6; ++q) dst[q] = (R)pl[q];
+        for (int q = 0; q < 6; ++q) dst[6 + q] = (R)box[q];
+    }
     for (uint32_t k = 0; k < s->n_planes; ++k) reinterpret_cast<uint32_t*>(b + o_pmat)[k] = s->plane_mat[k];
     for (uint32_t k = 0; k < s->n_materials; ++k) {
         const double* m = s->mat_params + 5 * k;
@@ -111,12 +138,43 @@ std::vector<unsigned char> stage_scene(const rtw_scene* s, rtw::DevScene<R>* ds,
     ds->mat_type = reinterpret_cast<const uint32_t*>(base + o_mt);
     ds->mat_p = reinterpret_cast<const R4*>(base + o_mp);
     ds->lights = reinterpret_cast<const R4*>(base + o_li);
-    ds->bvh = nullptr;
+    // round box bounds outward into precision R
+    auto down = [](double x) {
+        R r = (R)x;
+        return (double)r > x ? std::nextafter(r, (R)-INFINITY) : r;
+    };
+    auto up = [](double x) {
+        R r = (R)x;
+        return (double)r < x ? std::nextafter(r, (R)INFINITY) : r;
+    };
+    for (size_t k = 0; k < bb.nodes.size(); ++k) {
+        const rtw::BvhBuild::Node& n = bb.nodes[k];
+        rtw::BvhNode<R> d{};
+        for (int c = 0; c < 2; ++c) {
+            d.lo_x[c] = down(n.lo[c][0]);
+            d.lo_y[c] = down(n.lo[c][1]);
+            d.lo_z[c] = down(n.lo[c][2]);
+            d.hi_x[c] = up(n.hi[c][0]);
+            d.hi_y[c] = up(n.hi[c][1]);
+            d.hi_z[c] = up(n.hi[c][2]);
+            d.child[c] = n.child[c];
+        }
+        reinterpret_cast<rtw::BvhNode<R>*>(b + o_nodes)[k] = d;
+    }
+    for (uint32_t k = 0; k < s->n_spheres; ++k) {
+        const uint32_t id = bb.order[k];
+        reinterpret_cast<R4*>(b + o_bsph)[k] = reinterpret_cast<const R4*>(b + o_sph)[id];
+        reinterpret_cast<uint32_t*>(b + o_bid)[k] = id;
+    }
+    ds->bvh = reinterpret_cast<const rtw::BvhNode<R>*>(base + o_nodes);
+    ds->bsph = reinterpret_cast<const R4*>(base + o_bsph);
+    ds->bid = reinterpret_cast<const uint32_t*>(base + o_bid);
     ds->n_sph = s->n_spheres;
     ds->n_planes = s->n_planes;
     ds->n_mat = s->n_materials;
     ds->n_lights = s->n_lights;
-    ds->n_nodes = 0;
+    ds->n_nodes = (uint32_t)bb.nodes.size();
+    ds->bvh_depth = bb.depth;
     return blob;
 }
 
@@ -192,19 +250,22 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
     p.n_local_tiles = local_tile_rows(tiles_y, rank, nranks) * p.tiles_x;
     const size_t need_out = (size_t)rtw_rows_for_rank(p.H, rank, nranks) * p.W * 3 * sizeof(R);
     if (out_bytes < need_out) return fail(c, RTW_E_INVALID, "d_out is smaller than rows_for_rank*W*3");
-    // Work items = (tile, chunk of samples).  Enough items to keep the
-    // dispatcher busy to the end; chunks no smaller than 8 samples.
-    uint32_t chunk = c->chunk;
-    if (chunk == 0) {
-        const uint64_t target_items = 1u << 17;
-        uint64_t n_chunks = p.n_local_tiles ? (target_items + p.n_local_tiles - 1) / p.n_local_tiles : 1;
-        n_chunks = std::max<uint64_t>(1, std::min<uint64_t>(n_chunks, (p.spp + 7) / 8));
-        chunk = (uint32_t)((p.spp + n_chunks - 1) / n_chunks);
-    }
+    // Work decomposition: ITEM = (pixel, chunk of `chunk` samples) -- the unit
+    // a lane folds in sample order; TASK = (8x8 tile, group of chunks) -- one
+    // wavefront's dynamic item pool.  Small chunks balance the lanes of a
+    // wave; enough tasks keep the dispatcher fed to the end of the launch.
+    uint32_t chunk = c->chunk ? c->chunk : c->auto_chunk;
     chunk = std::max<uint32_t>(1, std::min<uint32_t>(chunk, std::max<uint32_t>(p.spp, 1)));
     p.chunk = chunk;
     p.n_chunks = p.spp ? (p.spp + chunk - 1) / chunk : 0;
-    p.n_items = p.n_local_tiles * p.n_chunks;
+    uint32_t group = c->group;
+    if (group == 0) {
+        const uint64_t n_groups = p.n_local_tiles ? (c->target_tasks + p.n_local_tiles - 1) / p.n_local_tiles : 1;
+        group = (uint32_t)((p.n_chunks + n_groups - 1) / std::max<uint64_t>(n_groups, 1));
+    }
+    p.group = std::max<uint32_t>(1, std::min<uint32_t>(group, std::max<uint32_t>(p.n_chunks, 1)));
+    p.n_groups = p.n_chunks ? (p.n_chunks + p.group - 1) / p.group : 0;
+    p.n_tasks = p.n_local_tiles * p.n_groups;
     const size_t partial_bytes = std::max<size_t>((size_t)p.n_chunks * p.n_local_tiles * 64 * 3 * sizeof(R), 64);
     int rc = ensure(c, &c->d_partial, &c->partial_cap, partial_bytes);
     if (rc) return rc;
@@ -212,20 +273,27 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
     p.counters = c->d_counters;
     if (!stream) stream = c->stream;
     HIP_TRY(c, hipMemsetAsync(c->d_counters, 0, 2 * sizeof(unsigned long long), stream));
-    if (p.spp == 0) {
-        HIP_TRY(c, hipMemsetAsync(d_out, 0, need_out, stream));
-        return RTW_OK;
-    }
     const size_t lds = (size_t)(p.sc.n_sph + p.sc.n_lights) * sizeof(rtw::R4<R>);
-    int accel = c->accel == RTW_ACCEL_AUTO ? RTW_ACCEL_BRUTE : c->accel;
+    const int accel = c->accel == RTW_ACCEL_AUTO ? c->auto_accel : c->accel;
+    int world = (c->world_pref == 0 || lds > kLdsLimit) ? rtw::kWorldGlobal : rtw::kWorldLds;
+    if (accel == RTW_ACCEL_BVH) {
+        if (p.sc.bvh_depth > rtw::kBvhStack)
+            return fail(c, RTW_E_UNSUPPORTED, "BVH deeper than the kernel's traversal stack");
+        world = rtw::kWorldBvh;
+    }
     hipEvent_t* ev = c->ring[c->n_renders % rtw_ctx::kRing];
     HIP_TRY(c, hipEventRecord(c->ev0, stream));
     HIP_TRY(c, hipEventRecord(ev[0], stream));
-    int lrc;
-    if constexpr (std::is_same<R, float>::value)
-        lrc = rtw::launch_render_f32(p, accel, lds <= kLdsLimit ? lds : 0, reinterpret_cast<float*>(d_out), stream, ev[1]);
-    else
-        lrc = rtw::launch_render_f64(p, accel, lds <= kLdsLimit ? lds : 0, reinterpret_cast<double*>(d_out), stream, ev[1]);
+    int lrc = 0;
+    if (p.spp == 0 || p.max_depth == 0) {
+        // depth == 0: every sample is Colour::default() + res = 0 (camera.rs:470-472)
+        HIP_TRY(c, hipMemsetAsync(d_out, 0, need_out, stream));
+        HIP_TRY(c, hipEventRecord(ev[1], stream));
+    } else if constexpr (std::is_same<R, float>::value) {
+        lrc = rtw::launch_render_f32(p, world, lds, reinterpret_cast<float*>(d_out), stream, ev[1]);
+    } else {
+        lrc = rtw::launch_render_f64(p, world, lds, reinterpret_cast<double*>(d_out), stream, ev[1]);
+    }
     if (lrc) return fail(c, RTW_E_DEVICE, std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
     HIP_TRY(c, hipEventRecord(c->ev1, stream));
     HIP_TRY(c, hipEventRecord(ev[2], stream));
@@ -293,9 +361,23 @@ int rtw_set_chunk(rtw_ctx* c, uint32_t chunk) {
     c->chunk = chunk;
     return RTW_OK;
 }
+int rtw_set_tuning(rtw_ctx* c, const char* key, int64_t value) {
+    if (!c || !key) return RTW_E_INVALID;
+    const std::string k = key;
+    if (value < 0) return fail(c, RTW_E_INVALID, "negative tuning value");
+    if (k == "chunk") c->chunk = (uint32_t)value;
+    else if (k == "auto_chunk") c->auto_chunk = std::max<uint32_t>(1, (uint32_t)value);
+    else if (k == "group") c->group = (uint32_t)value;
+    else if (k == "target_tasks") c->target_tasks = std::max<uint64_t>(1, (uint64_t)value);
+    else if (k == "lds") c->world_pref = value ? 1 : 0;
+    else if (k == "auto_accel") c->auto_accel = value == RTW_ACCEL_BVH ? RTW_ACCEL_BVH : RTW_ACCEL_BRUTE;
+    else return fail(c, RTW_E_INVALID, "unknown tuning key " + k);
+    return RTW_OK;
+}
+
 int rtw_set_accel(rtw_ctx* c, int accel) {
     if (!c) return RTW_E_INVALID;
-    if (accel < RTW_ACCEL_AUTO || accel > RTW_ACCEL_BRUTE) return fail(c, RTW_E_UNSUPPORTED, "accel not available");
+    if (accel < RTW_ACCEL_AUTO || accel > RTW_ACCEL_BVH) return fail(c, RTW_E_UNSUPPORTED, "accel not available");
     c->accel = accel;
     return RTW_OK;
 }
@@ -386,7 +468,7 @@ int rtw_set_scene(rtw_ctx* c, const rtw_scene* s) {
     int rc = validate_scene(c, s);
     if (rc) return rc;
     HIP_TRY(c, hipSetDevice(c->device));
-    // size the blob first (the pointers are fixed up against the allocation)
+    // stage once against base 0, then rebase the device pointers
     rtw::DevScene<float> tmp32{};
     rtw::DevScene<double> tmp64{};
     std::vector<unsigned char> blob = c->precision == RTW_F32 ? stage_scene<float>(s, &tmp32, 0)
@@ -399,10 +481,22 @@ int rtw_set_scene(rtw_ctx* c, const rtw_scene* s) {
         HIP_TRY(c, hipMalloc(&c->d_scene, blob.size()));
         c->scene_bytes = blob.size();
     }
-    if (c->precision == RTW_F32)
-        blob = stage_scene<float>(s, &c->sc32, reinterpret_cast<uintptr_t>(c->d_scene));
-    else
-        blob = stage_scene<double>(s, &c->sc64, reinterpret_cast<uintptr_t>(c->d_scene));
+    const uintptr_t base = reinterpret_cast<uintptr_t>(c->d_scene);
+    auto rebase = [base](auto& ds) {
+        auto fix = [base](auto*& ptr) {
+            using T = std::remove_reference_t<decltype(ptr)>;
+            ptr = reinterpret_cast<T>(reinterpret_cast<uintptr_t>(ptr) + base);
+        };
+        fix(ds.sph); fix(ds.sph_r); fix(ds.sph_mat); fix(ds.planes); fix(ds.plane_mat);
+        fix(ds.mat_type); fix(ds.mat_p); fix(ds.lights); fix(ds.bvh); fix(ds.bsph); fix(ds.bid);
+    };
+    if (c->precision == RTW_F32) {
+        rebase(tmp32);
+        c->sc32 = tmp32;
+    } else {
+        rebase(tmp64);
+        c->sc64 = tmp64;
+    }
     HIP_TRY(c, hipMemcpy(c->d_scene, blob.data(), blob.size(), hipMemcpyHostToDevice));
     c->has_scene = true;
     return RTW_OK;

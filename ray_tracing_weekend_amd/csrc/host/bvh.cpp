@@ -1,0 +1,184 @@
+// bvh.cpp -- binned-SAH BVH build over spheres (see bvh.hpp).
+#include "bvh.hpp"
+
+#include <math.h>
+
+#include <algorithm>
+#include <numeric>
+
+namespace rtw {
+namespace {
+
+struct Box {
+    double lo[3] = {INFINITY, INFINITY, INFINITY};
+    double hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    void grow(const Box& b) {
+        for (int k = 0; k < 3; ++k) {
+            lo[k] = std::min(lo[k], b.lo[k]);
+            hi[k] = std::max(hi[k], b.hi[k]);
+        }
+    }
+    void grow_pt(const double* p) {
+        for (int k = 0; k < 3; ++k) {
+            lo[k] = std::min(lo[k], p[k]);
+            hi[k] = std::max(hi[k], p[k]);
+        }
+    }
+    double area() const {
+        double dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
+        if (!(dx >= 0) || !(dy >= 0) || !(dz >= 0)) return 0.0;
+        return 2.0 * (dx * dy + dx * dz + dy * dz);
+    }
+};
+
+struct Prim {
+    Box box;
+    double c[3];
+    uint32_t id;
+};
+
+struct Builder {
+    std::vector<Prim> prims;
+    BvhBuild* out;
+    double pad;
+
+    Box padded(Box b) const {
+        for (int k = 0; k < 3; ++k) {
+            b.lo[k] -= pad;
+            b.hi[k] += pad;
+        }
+        return b;
+    }
+
+    // returns the child code for prims [b, e) and fills its box
+    int32_t build(uint32_t b, uint32_t e, uint32_t level, Box* box_out) {
+        Box box;
+        for (uint32_t k = b; k < e; ++k) box.grow(prims[k].box);
+        *box_out = padded(box);
+        const uint32_t n = e - b;
+        if (n <= kLeafMax) {
+            std::sort(prims.begin() + b, prims.begin() + e,
+                      [](const Prim& x, const Prim& y) { return x.id < y.id; });
+            const uint32_t first = (uint32_t)out->order.size();
+            for (uint32_t k = b; k < e; ++k) out->order.push_back(prims[k].id);
+            out->leaves++;
+            out->depth = std::max(out->depth, level);
+            return leaf_code(first, n);
+        }
+        Box cb;
+        for (uint32_t k = b; k < e; ++k) cb.grow_pt(prims[k].c);
+        constexpr int kBins = 16;
+        double best_cost = INFINITY;
+        int best_axis = -1, best_split = 0;
+        for (int axis = 0; axis < 3; ++axis) {
+            const double ext = cb.hi[axis] - cb.lo[axis];
+            if (!(ext > 0)) continue;
+            Box bins[kBins];
+            uint32_t cnt[kBins] = {};
+            const double scale = kBins / ext;
+            for (uint32_t k = b; k < e; ++k) {
+                int bi = std::min(kBins - 1, (int)((prims[k].c[axis] - cb.lo[axis]) * scale));
+                cnt[bi]++;
+                bins[bi].grow(prims[k].box);
+            }
+            double right_area[kBins];
+            uint32_t right_cnt[kBins];
+            Box acc;
+            uint32_t c = 0;
+            for (int s = kBins - 1; s > 0; --s) {
+                acc.grow(bins[s]);
+                c += cnt[s];
+                right_area[s] = acc.area();
+                right_cnt[s] = c;
+            }
+            Box lacc;
+            uint32_t lc = 0;
+            for (int s = 1; s < kBins; ++s) {
+                lacc.grow(bins[s - 1]);
+                lc += cnt[s - 1];
+                if (lc == 0 || right_cnt[s] == 0) continue;
+                const double cost = lacc.area() * lc + right_area[s] * right_cnt[s];
+                if (cost < best_cost) {
+                    best_cost = cost;
+                    best_axis = axis;
+                    best_split = s;
+                }
+            }
+        }
+        uint32_t mid;
+        if (best_axis < 0) {
+            mid = b + n / 2;   // coincident centroids: split by index
+        } else {
+            const double ext = cb.hi[best_axis] - cb.lo[best_axis];
+            const double scale = kBins / ext;
+            auto it = std::partition(prims.begin() + b, prims.begin() + e, [&](const Prim& p) {
+                int bi = std::min(kBins - 1, (int)((p.c[best_axis] - cb.lo[best_axis]) * scale));
+                return bi < best_split;
+            });
+            mid = (uint32_t)(it - prims.begin());
+            if (mid == b || mid == e) mid = b + n / 2;
+        }
+        const int32_t node = (int32_t)out->nodes.size();
+        out->nodes.emplace_back();
+        Box lb, rb;
+        const int32_t l = build(b, mid, level + 1, &lb);
+        const int32_t r = build(mid, e, level + 1, &rb);
+        BvhBuild::Node& nd = out->nodes[node];
+        for (int k = 0; k < 3; ++k) {
+            nd.lo[0][k] = lb.lo[k];
+            nd.hi[0][k] = lb.hi[k];
+            nd.lo[1][k] = rb.lo[k];
+            nd.hi[1][k] = rb.hi[k];
+        }
+        nd.child[0] = l;
+        nd.child[1] = r;
+        return node;
+    }
+};
+
+}  // namespace
+
+BvhBuild build_bvh(const double* spheres, uint32_t n, double pad_rel) {
+    BvhBuild out;
+    Builder bld;
+    bld.out = &out;
+    bld.prims.resize(n);
+    double scale = 0.0;
+    for (uint32_t k = 0; k < n; ++k) {
+        const double* s = spheres + 4 * k;
+        Prim& p = bld.prims[k];
+        const double r = fabs(s[3]);
+        for (int a = 0; a < 3; ++a) {
+            p.box.lo[a] = s[a] - r;
+            p.box.hi[a] = s[a] + r;
+            p.c[a] = s[a];
+            scale = std::max(scale, fabs(s[a]) + r);
+        }
+        p.id = k;
+    }
+    bld.pad = pad_rel * (scale + 1.0);
+    out.order.reserve(n);
+    out.nodes.reserve(n ? 2 * (n / kLeafMax + 1) : 1);
+    // the root is always an inner node (an empty right child when n <= kLeafMax)
+    if (n <= kLeafMax) {
+        out.nodes.emplace_back();
+        Box lb;
+        int32_t l = n ? bld.build(0, n, 1, &lb) : leaf_code(0, 0);
+        BvhBuild::Node& nd = out.nodes[0];
+        for (int k = 0; k < 3; ++k) {
+            nd.lo[0][k] = n ? lb.lo[k] : INFINITY;
+            nd.hi[0][k] = n ? lb.hi[k] : -INFINITY;
+            nd.lo[1][k] = INFINITY;
+            nd.hi[1][k] = -INFINITY;
+        }
+        nd.child[0] = l;
+        nd.child[1] = leaf_code(0, 0);
+        out.depth = 1;
+    } else {
+        Box root;
+        bld.build(0, n, 0, &root);
+    }
+    return out;
+}
+
+}  // namespace rtw

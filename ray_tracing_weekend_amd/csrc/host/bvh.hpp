@@ -1,0 +1,41 @@
+// bvh.hpp -- host-side BVH over the world's spheres for the RTW_ACCEL_BVH
+// render kernel.
+//
+// The reference builds a median-split binary BVH with <= 5 objects per leaf
+// and visits BOTH children of every node it enters (bvh.rs:106-188); only its
+// closest-hit semantics are part of the contract.  This
+// build is a binned-SAH binary tree with <= kLeafMax spheres per leaf, stored
+// "children in the parent" (one node = both child boxes + both child links),
+// traversed near-child-first with t-culling.  Box tests only cull: every
+// sphere that survives is tested with exactly the brute-force arithmetic, and
+// boxes are padded outward so that rounding can never cull the true closest
+// sphere.
+#pragma once
+
+#include <stdint.h>
+
+#include <vector>
+
+namespace rtw {
+
+struct BvhBuild {
+    struct Node {
+        double lo[2][3], hi[2][3];   // child boxes (padded)
+        int32_t child[2];            // >= 0 inner node; < 0 leaf, see leaf_code()
+    };
+    std::vector<Node> nodes;         // nodes[0] is the root
+    std::vector<uint32_t> order;     // BVH position -> original sphere index
+    uint32_t depth = 0;              // inner-node levels on the deepest path
+    uint32_t leaves = 0;
+};
+
+constexpr uint32_t kLeafMax = 4;
+
+// leaf code: ~((first << 4) | count), count in [0, 15]
+inline int32_t leaf_code(uint32_t first, uint32_t count) { return ~(int32_t)((first << 4) | count); }
+
+// spheres: n x {cx, cy, cz, r}.  pad_rel: relative outward padding of every
+// box (absorbs the rounding of the device slab test in the kernel precision).
+BvhBuild build_bvh(const double* spheres, uint32_t n, double pad_rel);
+
+}  // namespace rtw

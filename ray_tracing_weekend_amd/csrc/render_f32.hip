@@ -4,13 +4,13 @@
 
 namespace rtw {
 
-int launch_render_f32(const KParams<float>& p, int accel, size_t lds_bytes, float* out,
+int launch_render_f32(const KParams<float>& p, int world, size_t lds_bytes, float* out,
                       hipStream_t stream, hipEvent_t mid) {
-    if (lds_bytes > 65536)
+    if (world == kWorldLds && lds_bytes > 65536)
         (void)hipFuncSetAttribute(
-            reinterpret_cast<const void*>(&dev::render_brute_kernel<float, true>),
+            reinterpret_cast<const void*>(&dev::render_kernel<float, kWorldLds>),
             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
-    return launch_render_impl<float>(p, accel, lds_bytes, out, stream, mid);
+    return launch_render_impl<float>(p, world, lds_bytes, out, stream, mid);
 }
 
 }  // namespace rtw

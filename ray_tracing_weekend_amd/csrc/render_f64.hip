@@ -5,13 +5,13 @@
 
 namespace rtw {
 
-int launch_render_f64(const KParams<double>& p, int accel, size_t lds_bytes, double* out,
+int launch_render_f64(const KParams<double>& p, int world, size_t lds_bytes, double* out,
                       hipStream_t stream, hipEvent_t mid) {
-    if (lds_bytes > 65536)
+    if (world == kWorldLds && lds_bytes > 65536)
         (void)hipFuncSetAttribute(
-            reinterpret_cast<const void*>(&dev::render_brute_kernel<double, true>),
+            reinterpret_cast<const void*>(&dev::render_kernel<double, kWorldLds>),
             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
-    return launch_render_impl<double>(p, accel, lds_bytes, out, stream, mid);
+    return launch_render_impl<double>(p, world, lds_bytes, out, stream, mid);
 }
 
 }  // namespace rtw

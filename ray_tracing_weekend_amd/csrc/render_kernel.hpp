@@ -1,25 +1,32 @@
-// render_kernel.hpp -- the gfx950 render kernels, templated on precision R.
+// render_kernel.hpp -- the gfx950 render kernels, templated on precision R
+// and on the world query (brute force over an LDS-staged or a global sphere
+// list; BVH).
 //
 // Restates the reference's per-pixel / per-sample loop:
 //   render_internal / render_lambda   shared/src/camera.rs:315-388
 //   Camera::get_ray                   shared/src/camera.rs:274-293
 //   ray_colour_tail_call              shared/src/camera.rs:459-522
-// as ONE iterative loop per lane ("path regeneration"): a lane owns a pixel
-// of its wave's 8x8 tile and walks that pixel's samples [s_begin, s_end) of
-// the work item's chunk; every loop trip traces one segment (one world.hit)
-// and, when the path ends, deposits the sample into the lane's running sum
-// and immediately starts the next sample.  All 64 lanes therefore share each
-// trip's closest-hit sweep, whatever the lengths of their individual paths.
+// as ONE iterative loop per lane.  Work is cut into ITEMS = (pixel, chunk of
+// `chunk` consecutive samples); a wavefront owns a TASK = one 8x8 tile x a
+// group of chunks, i.e. a pool of 64 * group items.  Every lane takes an item,
+// traces its samples one segment (one world.hit) per loop trip, folds them in
+// sample order into the item's partial sum, and when the item is done takes
+// the next free item of the pool (ballot + mbcnt: no atomics).  All lanes thus
+// share every trip's closest-hit sweep even though the reference's path
+// lengths range from 1 to max_depth segments (its t_min = f64::EPSILON makes
+// self-intersecting, depth-long paths common).
 //
-// The sample sum of a chunk is folded in sample order exactly like
-// `(0..spp).map(..).fold(Colour::default(), +)` (camera.rs:323-335); chunk
-// sums are folded in chunk order by reduce_chunks_kernel.
+// Chunk sums land in partial[chunk][tile][pixel]; reduce_chunks_kernel folds
+// them in chunk order.  Inside a chunk the samples are folded exactly like
+// `(0..spp).map(..).fold(Colour::default(), +)` (camera.rs:323-335), so with
+// chunk >= spp the f64 result is the reference's fold order bit for bit.
 #pragma once
 
 #include "rtw_device.hpp"
 #include "rtw_kernels.h"
 
 namespace rtw {
+
 namespace dev {
 
 template <typename R>
@@ -38,54 +45,251 @@ __device__ __forceinline__ bool plane_t(const R* pl, V3<R> o, V3<R> d, R tmin, R
     return true;
 }
 
-template <typename R, bool kLds>
-__global__ void __launch_bounds__(kBlock) render_brute_kernel(const KParams<R> p) {
+// AABBox::hit, hittable.rs:291-339, over [rs, +inf]: the slab test the
+// reference runs before every object's own hit (bounded_hit).  Rust's f64
+// max/min ignore a NaN operand like fmax/fmin.
+template <typename R>
+__device__ __forceinline__ bool aabb_hit_ref(const R* lo, const R* hi, V3<R> o, V3<R> d, R rs) {
+    R t0 = P<R>::div_(lo[0] - o.x, d.x), t1 = P<R>::div_(hi[0] - o.x, d.x);
+    if (__builtin_signbit(d.x)) { R q = t0; t0 = t1; t1 = q; }
+    R tmin = t0, tmax = t1;
+    R a0 = P<R>::div_(lo[1] - o.y, d.y), a1 = P<R>::div_(hi[1] - o.y, d.y);
+    if (__builtin_signbit(d.y)) { R q = a0; a0 = a1; a1 = q; }
+    if (tmax < a0 || tmin > a1) return false;
+    tmin = P<R>::max_(tmin, a0);
+    tmax = P<R>::min_(tmax, a1);
+    a0 = P<R>::div_(lo[2] - o.z, d.z);
+    a1 = P<R>::div_(hi[2] - o.z, d.z);
+    if (__builtin_signbit(d.z)) { R q = a0; a0 = a1; a1 = q; }
+    if (tmax < a0 || tmin > a1) return false;
+    tmin = P<R>::max_(tmin, a0);
+    tmax = P<R>::min_(tmax, a1);
+    return P<R>::max_(rs, tmin) <= P<R>::min_((R)INFINITY, tmax);
+}
+
+// Closest sphere of a contiguous list [0, n), ids base + k.  Semantics of the
+// reference's closest hit: t = near root if it lies in [tmin, inf], else the
+// far root (sphere.rs:71-80); the smallest t wins, the lowest id on ties.
+//
+// f64 (parity mode): the reference's exact arithmetic, divisions included.
+__device__ __forceinline__ void sweep_spheres(const R4<double>* __restrict__ sph, uint32_t n,
+                                              int32_t base, V3<double> o, V3<double> d, double tmin,
+                                              double& tb, int32_t& best) {
+#pragma unroll 2
+    for (uint32_t k = 0; k < n; ++k) {
+        const R4<double> s = sph[k];
+        double t;
+        if (sphere_t(mk(s.x, s.y, s.z), s.w, o, d, tmin, t) && (best < 0 || t < tb)) {
+            tb = t;
+            best = base + (int32_t)k;
+        }
+    }
+}
+// f32 (speed mode): branch-free body so that the compiler keeps a batch of
+// sphere loads in flight.  Both roots come from one reciprocal of a = d.d.
+// The range test "t in [tmin, tb)" is ONE unsigned compare on
+// u = bits(t) - bits(tmin): for t >= 0 float bits are monotonic, while every
+// t < tmin (negative, or in [0, tmin)) and NaN maps above bits(+inf) -
+// bits(tmin) >= any live bound.  Since t0 <= t1, min_u32(u0, u1) is the
+// near root when it is >= tmin, else the far root (sphere.rs:71-80).  A
+// negative discriminant gives sqrt = NaN and so no hit; disc == 0 exactly (a
+// tangent ray) counts as a hit here, where the reference needs disc > 0.
+__device__ __forceinline__ void sweep_spheres(const R4<float>* __restrict__ sph, uint32_t n,
+                                              int32_t base, V3<float> o, V3<float> d, float tmin,
+                                              float& tb, int32_t& best) {
+    const float a = dot(d, d);
+    const float ia = __builtin_amdgcn_rcpf(a);
+    const uint32_t tminb = __float_as_uint(tmin);
+    uint32_t ub = __float_as_uint(tb) - tminb;
+#pragma unroll 8
+    for (uint32_t k = 0; k < n; ++k) {
+        const R4<float> s = sph[k];
+        const float ocx = o.x - s.x, ocy = o.y - s.y, ocz = o.z - s.z;
+        const float hb = d.x * ocx + d.y * ocy + d.z * ocz;
+        const float c = ocx * ocx + (ocy * ocy + (ocz * ocz - s.w));
+        const float disc = hb * hb - a * c;
+        const float sq = __builtin_amdgcn_sqrtf(disc);   // NaN when disc < 0
+        const float nb = -hb * ia;
+        const float t0 = nb - sq * ia, t1 = nb + sq * ia;
+        const uint32_t u = min(__float_as_uint(t0) - tminb, __float_as_uint(t1) - tminb);
+        const bool h = u < ub;
+        ub = h ? u : ub;
+        best = h ? base + (int32_t)k : best;
+    }
+    tb = __uint_as_float(ub + tminb);
+}
+
+// ---------------------------------------------------------------------------
+// BVH closest hit (RTW_ACCEL_BVH).  Box tests only cull; every surviving
+// sphere goes through the same per-sphere arithmetic as the brute-force
+// sweep, and the lowest id wins ties, so the result is the brute-force result.
+// ---------------------------------------------------------------------------
+template <typename R>
+struct SphereTester;
+
+template <>
+struct SphereTester<double> {   // exact reference arithmetic (sphere.rs:61-80)
+    V3<double> o, d;
+    double tmin, tb;
+    int32_t best;
+    __device__ __forceinline__ double bound() const { return tb; }
+    __device__ __forceinline__ void test(const R4<double>& s, int32_t id) {
+        double t;
+        if (sphere_t(mk(s.x, s.y, s.z), s.w, o, d, tmin, t) &&
+            (best < 0 || t < tb || (t == tb && id < best))) {
+            tb = t;
+            best = id;
+        }
+    }
+};
+
+template <>
+struct SphereTester<float> {    // the f32 sweep's arithmetic (see sweep_spheres)
+    V3<float> o, d;
+    float a, ia;
+    uint32_t tminb, ub;
+    int32_t best;
+    __device__ __forceinline__ float bound() const { return __uint_as_float(ub + tminb); }
+    __device__ __forceinline__ void test(const R4<float>& s, int32_t id) {
+        const float ocx = o.x - s.x, ocy = o.y - s.y, ocz = o.z - s.z;
+        const float hb = d.x * ocx + d.y * ocy + d.z * ocz;
+        const float c = ocx * ocx + (ocy * ocy + (ocz * ocz - s.w));
+        const float disc = hb * hb - a * c;
+        const float sq = __builtin_amdgcn_sqrtf(disc);
+        const float nb = -hb * ia;
+        const float t0 = nb - sq * ia, t1 = nb + sq * ia;
+        const uint32_t u = min(__float_as_uint(t0) - tminb, __float_as_uint(t1) - tminb);
+        if (u < ub || (u == ub && id < best)) {
+            ub = u;
+            best = id;
+        }
+    }
+};
+
+__device__ __forceinline__ double inv_(double x) { return 1.0 / x; }
+__device__ __forceinline__ float inv_(float x) { return __builtin_amdgcn_rcpf(x); }
+
+// Near-child-first traversal with a per-lane stack in LDS (stk[entry * 64]).
+// Slab test on padded child boxes against [0, tb].
+template <typename R>
+__device__ __forceinline__ void bvh_traverse(const DevScene<R>& sc, int32_t base, V3<R> o, V3<R> d,
+                                             SphereTester<R>& T, int32_t* __restrict__ stk) {
+    const R ix = inv_(d.x), iy = inv_(d.y), iz = inv_(d.z);
+    const R oix = o.x * ix, oiy = o.y * iy, oiz = o.z * iz;
+    const BvhNode<R>* __restrict__ nodes = sc.bvh;
+    int32_t sp = 0;
+    int32_t node = 0;
+    for (;;) {
+        if (node >= 0) {
+            const BvhNode<R>& nd = nodes[node];
+            const R tb = T.bound();
+            R tn[2], tf[2];
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                const R x0 = nd.lo_x[c] * ix - oix, x1 = nd.hi_x[c] * ix - oix;
+                const R y0 = nd.lo_y[c] * iy - oiy, y1 = nd.hi_y[c] * iy - oiy;
+                const R z0 = nd.lo_z[c] * iz - oiz, z1 = nd.hi_z[c] * iz - oiz;
+                tn[c] = fmax(fmax(fmin(x0, x1), fmin(y0, y1)), fmax(fmin(z0, z1), (R)0));
+                tf[c] = fmin(fmin(fmax(x0, x1), fmax(y0, y1)), fmin(fmax(z0, z1), tb));
+            }
+            const bool h0 = tn[0] <= tf[0], h1 = tn[1] <= tf[1];
+            const int32_t c0 = nd.child[0], c1 = nd.child[1];
+            if (h0 && h1) {
+                const bool first0 = tn[0] <= tn[1];
+                stk[sp * 64] = first0 ? c1 : c0;
+                ++sp;
+                node = first0 ? c0 : c1;
+            } else if (h0) {
+                node = c0;
+            } else if (h1) {
+                node = c1;
+            } else {
+                if (sp == 0) break;
+                --sp;
+                node = stk[sp * 64];
+            }
+        } else {
+            const uint32_t code = (uint32_t)~node;
+            const uint32_t first = code >> 4, cnt = code & 15u;
+            for (uint32_t k = 0; k < cnt; ++k)
+                T.test(sc.bsph[first + k], base + (int32_t)sc.bid[first + k]);
+            if (sp == 0) break;
+            --sp;
+            node = stk[sp * 64];
+        }
+    }
+}
+
+__device__ __forceinline__ void bvh_closest(const DevScene<double>& sc, int32_t base, V3<double> o,
+                                            V3<double> d, double tmin, double& tb, int32_t& best,
+                                            int32_t* stk) {
+    SphereTester<double> T{o, d, tmin, tb, best};
+    bvh_traverse(sc, base, o, d, T, stk);
+    tb = T.tb;
+    best = T.best;
+}
+__device__ __forceinline__ void bvh_closest(const DevScene<float>& sc, int32_t base, V3<float> o,
+                                            V3<float> d, float tmin, float& tb, int32_t& best,
+                                            int32_t* stk) {
+    SphereTester<float> T;
+    T.o = o;
+    T.d = d;
+    T.a = dot(d, d);
+    T.ia = __builtin_amdgcn_rcpf(T.a);
+    T.tminb = __float_as_uint(tmin);
+    T.ub = __float_as_uint(tb) - T.tminb;
+    T.best = best;
+    bvh_traverse(sc, base, o, d, T, stk);
+    tb = T.bound();
+    best = T.best;
+}
+
+template <typename R, int kWorld>
+__global__ void __launch_bounds__(kBlock) render_kernel(const KParams<R> p) {
     using PR = P<R>;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     R4<R>* s_sph = reinterpret_cast<R4<R>*>(smem);
     R4<R>* s_li = s_sph + p.sc.n_sph;
-    if constexpr (kLds) {
+    if constexpr (kWorld == kWorldLds) {
         // Stage the sphere list {c, r^2} and the light list into LDS once per
-        // workgroup: every lane of every wave then reads sphere k with the
-        // same LDS address (a broadcast read) in its closest-hit sweep.
+        // workgroup: every lane of every wave then reads sphere k at the same
+        // LDS address (a broadcast read) during its closest-hit sweep.
         for (uint32_t k = threadIdx.x; k < p.sc.n_sph; k += kBlock) s_sph[k] = p.sc.sph[k];
         for (uint32_t k = threadIdx.x; k < p.sc.n_lights; k += kBlock) s_li[k] = p.sc.lights[k];
         __syncthreads();
     }
-    const R4<R>* __restrict__ sph = kLds ? s_sph : p.sc.sph;
-    const R4<R>* __restrict__ li = kLds ? s_li : p.sc.lights;
+    const R4<R>* __restrict__ sph = kWorld == kWorldLds ? s_sph : p.sc.sph;
+    const R4<R>* __restrict__ li = kWorld == kWorldLds ? s_li : p.sc.lights;
 
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const uint32_t item = blockIdx.x * kWavesPerBlock + wave;
-    if (item >= p.n_items) return;
-    const uint32_t lt = item / p.n_chunks;
-    const uint32_t ch = item - lt * p.n_chunks;
+    const uint32_t task = blockIdx.x * kWavesPerBlock + wave;
+    if (task >= p.n_tasks) return;
+    const uint32_t lt = task / p.n_groups;
+    const uint32_t cg = task - lt * p.n_groups;
     const uint32_t tr = lt / p.tiles_x;
     const uint32_t tx = lt - tr * p.tiles_x;
     const uint32_t ty = tr * p.nranks + p.rank;
-    const uint32_t i = tx * kTile + (lane & 7);
-    const uint32_t j = ty * kTile + (lane >> 3);
-    const bool valid = i < p.W && j < p.H;
-    uint32_t s = ch * p.chunk;
-    const uint32_t s_end = min(s + p.chunk, p.spp);
-    const uint64_t pix = (uint64_t)j * p.W + i;
+    const uint32_t c_begin = cg * p.group;
+    const uint32_t c_end = min(c_begin + p.group, p.n_chunks);
+    const uint32_t n_items = 64u * (c_end - c_begin);
 
     const V3<R> center = v3of(p.center), p00 = v3of(p.p00), du = v3of(p.du), dv = v3of(p.dv);
     const V3<R> bg = v3of(p.bg);
     const V3<R> zero = mk<R>(0, 0, 0);
     const R tmin = PR::kEps;
+    const int32_t nplanes = (int32_t)p.sc.n_planes;
 
-    V3<R> part = zero;             // fold(Colour::default(), +) of this chunk
-    uint32_t segs = 0, lambs = 0;
+    // per-lane item state
+    uint32_t q = lane;            // item index in the task's pool
+    uint32_t next_q = 64;         // wave-uniform: first unassigned item
+    uint32_t px = 0, i = 0, j = 0, c = 0, s = 0, s_end = 0;
+    uint64_t pix = 0;
+    V3<R> part = zero;            // fold(Colour::default(), +) of the item's samples
     Rng g;
     V3<R> o = zero, d = zero, mult = zero, res = zero;
     uint32_t depth = 0;
-    bool alive = valid && s < s_end;
-    if (alive && p.max_depth == 0) {
-        // depth == 0 on entry: every sample is Colour::default() + res = 0
-        for (; s < s_end; ++s) part = part + (zero + zero);
-        alive = false;
-    }
+    uint32_t segs = 0, lambs = 0;
+    bool active = false, need = true;
 
     auto start_sample = [&]() {
         // Camera::get_ray, camera.rs:274-293 + ray_colour_call, camera.rs:439-457
@@ -95,8 +299,8 @@ __global__ void __launch_bounds__(kBlock) render_brute_kernel(const KParams<R> p
         V3<R> ps = (p00 + du * ((R)i + ox)) + dv * ((R)j + oy);
         V3<R> origin = center;
         if (p.defocus) {
-            V3<R> q = unit_disk<R>(g);
-            origin = (center + v3of(p.disk_u) * q.x) + v3of(p.disk_v) * q.z;
+            V3<R> qd = unit_disk<R>(g);
+            origin = (center + v3of(p.disk_u) * qd.x) + v3of(p.disk_v) * qd.z;
         }
         o = origin;
         d = ps - origin;
@@ -104,149 +308,197 @@ __global__ void __launch_bounds__(kBlock) render_brute_kernel(const KParams<R> p
         res = zero;
         depth = p.max_depth;
     };
-    if (alive) start_sample();
-
-    while (alive) {
-        // ---- world.hit(&r, EPSILON..=INFINITY): closest over all primitives
-        R tb = (R)INFINITY;
-        int32_t best = -1;
-        for (uint32_t k = 0; k < p.sc.n_planes; ++k) {
-            R t;
-            if (plane_t(p.sc.planes + 6 * k, o, d, tmin, t) && (best < 0 || t < tb)) {
-                tb = t;
-                best = (int32_t)k;
-            }
-        }
-        const int32_t nplanes = (int32_t)p.sc.n_planes;
-#pragma unroll 4
-        for (uint32_t k = 0; k < p.sc.n_sph; ++k) {
-            const R4<R> sk = sph[k];
-            R t;
-            if (sphere_t(mk(sk.x, sk.y, sk.z), sk.w, o, d, tmin, t) && (best < 0 || t < tb)) {
-                tb = t;
-                best = nplanes + (int32_t)k;
-            }
-        }
-        ++segs;
-
-        bool done = false;
-        V3<R> c = zero;
-        if (best < 0) {
-            c = mult * bg + res;                                   // camera.rs:473-475
-            done = true;
-        } else {
-            // HitRecord::new, hittable.rs:101-129
-            V3<R> pnt = o + d * tb;
-            V3<R> outward;
-            uint32_t m;
-            if (best < nplanes) {
-                const R* pl = p.sc.planes + 6 * best;
-                outward = mk(pl[3], pl[4], pl[5]);
-                m = p.sc.plane_mat[best];
-            } else {
-                const uint32_t k = (uint32_t)(best - nplanes);
-                const R4<R> sk = sph[k];
-                outward = PR::divs(pnt - mk(sk.x, sk.y, sk.z), p.sc.sph_r[k]);   // sphere.rs:82-83
-                m = p.sc.sph_mat[k];
-            }
-            const bool front = dot(d, outward) < (R)0;
-            const V3<R> nrm = front ? outward : -outward;
-            const uint32_t mtype = p.sc.mat_type[m];
-            const R4<R> mp = p.sc.mat_p[m];
-            const V3<R> emitted = zero;                            // material.rs:42-44
-            if (mtype == 1) {
-                // Metal::scatter, material.rs:407-421
-                V3<R> refl = reflect(PR::normalize(d), nrm);
-                V3<R> dir = refl + unit_sphere<R>(g) * mp.w;
-                if (!(dot(dir, nrm) > (R)0)) {
-                    c = mult * emitted + res;
-                    done = true;
+    // Give every lane that needs one a valid item (or none: pool drained).
+    auto acquire = [&]() {
+        for (;;) {
+            const uint64_t want = __ballot(need);
+            if (want == 0) break;
+            if (need) {
+                const uint32_t below = __builtin_amdgcn_mbcnt_hi(
+                    (uint32_t)(want >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)want, 0u));
+                q = next_q + below;
+                if (q < n_items) {
+                    px = q & 63u;
+                    c = c_begin + (q >> 6);
+                    i = tx * kTile + (px & 7u);
+                    j = ty * kTile + (px >> 3);
+                    if (i < p.W && j < p.H) {
+                        pix = (uint64_t)j * p.W + i;
+                        s = c * p.chunk;
+                        s_end = min(s + p.chunk, p.spp);
+                        part = zero;
+                        active = true;
+                        need = false;
+                        start_sample();
+                    }
                 } else {
-                    mult = mult * mk(mp.x, mp.y, mp.z);
+                    need = false;
+                }
+            }
+            next_q += (uint32_t)__popcll(want);
+        }
+    };
+    // the first 64 items go to lanes 0..63 in order
+    need = false;
+    px = lane;
+    c = c_begin;
+    i = tx * kTile + (px & 7u);
+    j = ty * kTile + (px >> 3);
+    if (i < p.W && j < p.H) {
+        pix = (uint64_t)j * p.W + i;
+        s = c * p.chunk;
+        s_end = min(s + p.chunk, p.spp);
+        active = true;
+        start_sample();
+    } else {
+        need = true;
+    }
+    acquire();
+
+    while (__ballot(active) != 0) {
+        if (active) {
+            // ---- world.hit(&r, EPSILON..=INFINITY): closest over all primitives
+            R tb = (R)INFINITY;
+            int32_t best = -1;
+            for (int32_t k = 0; k < nplanes; ++k) {
+                R t;
+                const R* pl = p.sc.planes + 12 * k;
+                if (aabb_hit_ref(pl + 6, pl + 9, o, d, tmin) && plane_t(pl, o, d, tmin, t) &&
+                    (best < 0 || t < tb)) {
+                    tb = t;
+                    best = k;
+                }
+            }
+            if constexpr (kWorld == kWorldBvh) {
+                bvh_closest(p.sc, nplanes, o, d, tmin, tb, best,
+                            reinterpret_cast<int32_t*>(smem) + wave * kBvhStack * 64 + lane);
+            } else {
+                sweep_spheres(sph, p.sc.n_sph, nplanes, o, d, tmin, tb, best);
+            }
+            ++segs;
+
+            bool done = false;
+            V3<R> col = zero;
+            if (best < 0) {
+                col = mult * bg + res;                                 // camera.rs:473-475
+                done = true;
+            } else {
+                // HitRecord::new, hittable.rs:101-129
+                V3<R> pnt = o + d * tb;
+                V3<R> outward;
+                uint32_t m;
+                if (best < nplanes) {
+                    const R* pl = p.sc.planes + 12 * best;
+                    outward = mk(pl[3], pl[4], pl[5]);
+                    m = p.sc.plane_mat[best];
+                } else {
+                    const uint32_t k = (uint32_t)(best - nplanes);
+                    const R4<R> sk = p.sc.sph[k];
+                    outward = PR::divs(pnt - mk(sk.x, sk.y, sk.z), p.sc.sph_r[k]);  // sphere.rs:82-83
+                    m = p.sc.sph_mat[k];
+                }
+                const bool front = dot(d, outward) < (R)0;
+                const V3<R> nrm = front ? outward : -outward;
+                const uint32_t mtype = p.sc.mat_type[m];
+                const R4<R> mp = p.sc.mat_p[m];
+                const V3<R> emitted = zero;                            // material.rs:42-44
+                if (mtype == kMatMetal) {
+                    // Metal::scatter, material.rs:407-421
+                    V3<R> refl = reflect(PR::normalize(d), nrm);
+                    V3<R> dir = refl + unit_sphere<R>(g) * mp.w;
+                    if (!(dot(dir, nrm) > (R)0)) {
+                        col = mult * emitted + res;
+                        done = true;
+                    } else {
+                        mult = mult * mk(mp.x, mp.y, mp.z);            // Reflect, camera.rs:488-500
+                        o = pnt;
+                        d = dir;
+                    }
+                } else if (mtype == kMatDielectric) {
+                    // Dialectric::scatter, material.rs:458-487
+                    R ratio = front ? PR::div_((R)1, mp.w) : mp.w;
+                    V3<R> unit = PR::normalize(d);
+                    R cos_t = PR::min_(dot(unit, -nrm), (R)1);
+                    R sin_t = PR::sqrt_((R)1 - cos_t * cos_t);
+                    bool cannot = ratio * sin_t > (R)1;
+                    V3<R> dir;
+                    if (cannot || reflectance(cos_t, ratio) > PR::u_open01(g.next()))
+                        dir = reflect(unit, nrm);
+                    else
+                        dir = refract(unit, nrm, ratio);
+                    // mult * Colour(1, 1, 1) is the identity on every value
                     o = pnt;
                     d = dir;
-                }
-            } else if (mtype == 2) {
-                // Dialectric::scatter, material.rs:458-487
-                R ratio = front ? PR::div_((R)1, mp.w) : mp.w;
-                V3<R> unit = PR::normalize(d);
-                R cos_t = PR::min_(dot(unit, -nrm), (R)1);
-                R sin_t = PR::sqrt_((R)1 - cos_t * cos_t);
-                bool cannot = ratio * sin_t > (R)1;
-                V3<R> dir;
-                if (cannot || reflectance(cos_t, ratio) > PR::u_open01(g.next()))
-                    dir = reflect(unit, nrm);
-                else
-                    dir = refract(unit, nrm, ratio);
-                // mult * Colour(1, 1, 1) is the identity on every value
-                o = pnt;
-                d = dir;
-            } else if (mtype == 0) {
-                // Lambertian + MixturePdf(HittablePdf(lights), CosinePdf):
-                // material.rs:357-376, pdf.rs:33-101, camera.rs:504-521
-                ++lambs;
-                const V3<R> att = mk(mp.x, mp.y, mp.z);
-                const Onb<R> uvw(nrm);
-                V3<R> dir;
-                if (PR::u_std(g.next()) < (R)0.5) {
-                    // HittableList::random (hittable_list.rs:414-419): choose()
-                    const uint32_t nl = p.sc.n_lights;
-                    uint32_t pick = 0;
-                    (void)g.index(1);
-                    if (nl == 2) {
-                        if (g.index(2) == 0) pick = 1;
-                    } else if (nl >= 3) {
-                        uint32_t ix = g.index(nl);
-                        pick = ix < nl - 1 ? ix + 1 : 0;
+                } else if (mtype == kMatLambertian) {
+                    // Lambertian + MixturePdf(HittablePdf(lights), CosinePdf):
+                    // material.rs:357-376, pdf.rs:33-101, camera.rs:504-521
+                    ++lambs;
+                    const V3<R> att = mk(mp.x, mp.y, mp.z);
+                    const Onb<R> uvw(nrm);
+                    V3<R> dir;
+                    if (PR::u_std(g.next()) < (R)0.5) {
+                        // HittableList::random (hittable_list.rs:414-419): choose()
+                        const uint32_t nl = p.sc.n_lights;
+                        uint32_t pick = 0;
+                        (void)g.index(1);
+                        if (nl == 2) {
+                            if (g.index(2) == 0) pick = 1;
+                        } else if (nl >= 3) {
+                            uint32_t ix = g.index(nl);
+                            pick = ix < nl - 1 ? ix + 1 : 0;
+                        }
+                        const R4<R> L = li[pick];
+                        dir = sphere_random(mk(L.x, L.y, L.z), L.w, pnt, g);
+                    } else {
+                        dir = uvw.transform(cosine_hemisphere<R>(g));
                     }
-                    const R4<R> L = li[pick];
-                    dir = sphere_random(mk(L.x, L.y, L.z), L.w, pnt, g);
+                    const V3<R> ndir = PR::normalize(dir);
+                    const R cos_w = PR::over_pi(dot(ndir, uvw.w));
+                    R acc = (R)0;                                      // hittable_list.rs:408-412
+                    for (uint32_t k = 0; k < p.sc.n_lights; ++k) {
+                        const R4<R> L = li[k];
+                        acc = acc + sphere_pdf_value(mk(L.x, L.y, L.z), L.w, pnt, dir);
+                    }
+                    const R lpdf = PR::div_(acc, (R)p.sc.n_lights);
+                    const R pdf = lpdf * (R)0.5 + PR::max_(cos_w, (R)0) * (R)0.5;
+                    const R spdf = PR::max_(PR::over_pi(dot(nrm, ndir)), (R)0);
+                    const V3<R> w = PR::divs(att * spdf, pdf);
+                    const V3<R> new_mult = mult * w;
+                    res = res + mult * emitted;
+                    mult = new_mult;
+                    o = pnt;
+                    d = dir;
                 } else {
-                    dir = uvw.transform(cosine_hemisphere<R>(g));
-                }
-                const V3<R> ndir = PR::normalize(dir);
-                const R cos_w = PR::over_pi(dot(ndir, uvw.w));
-                R acc = (R)0;                                       // hittable_list.rs:408-412
-                for (uint32_t k = 0; k < p.sc.n_lights; ++k) {
-                    const R4<R> L = li[k];
-                    acc = acc + sphere_pdf_value(mk(L.x, L.y, L.z), L.w, pnt, dir);
-                }
-                const R lpdf = PR::div_(acc, (R)p.sc.n_lights);
-                const R pdf = lpdf * (R)0.5 + PR::max_(cos_w, (R)0) * (R)0.5;
-                const R spdf = PR::max_(PR::over_pi(dot(nrm, ndir)), (R)0);
-                const V3<R> w = PR::divs(att * spdf, pdf);
-                const V3<R> new_mult = mult * w;
-                res = res + mult * emitted;
-                mult = new_mult;
-                o = pnt;
-                d = dir;
-            } else {
-                // Invisible (material.rs:321-325): scatter() == None
-                c = mult * emitted + res;
-                done = true;
-            }
-            if (!done) {
-                depth -= 1;
-                if (depth == 0) {                                    // camera.rs:470-472
-                    c = zero + res;
+                    // Invisible (material.rs:321-325): scatter() == None
+                    col = mult * emitted + res;
                     done = true;
                 }
+                if (!done) {
+                    depth -= 1;
+                    if (depth == 0) {                                  // camera.rs:470-472
+                        col = zero + res;
+                        done = true;
+                    }
+                }
+            }
+            if (done) {
+                part = part + col;
+                ++s;
+                if (s < s_end) {
+                    start_sample();
+                } else {
+                    R* dst = p.partial + (((size_t)c * p.n_local_tiles + lt) * 64 + px) * 3;
+                    dst[0] = part.x;
+                    dst[1] = part.y;
+                    dst[2] = part.z;
+                    active = false;
+                    need = true;
+                }
             }
         }
-        if (done) {
-            part = part + c;
-            ++s;
-            if (s < s_end) start_sample();
-            else alive = false;
-        }
+        acquire();
     }
 
-    if (valid) {
-        R* dst = p.partial + (((size_t)ch * p.n_local_tiles + lt) * 64 + lane) * 3;
-        dst[0] = part.x;
-        dst[1] = part.y;
-        dst[2] = part.z;
-    }
     // wave-reduce the counters, one atomic per wave
     for (int off = 32; off > 0; off >>= 1) {
         segs += __shfl_xor(segs, off);
@@ -287,16 +539,18 @@ __global__ void __launch_bounds__(256) reduce_chunks_kernel(const KParams<R> p, 
 }  // namespace dev
 
 template <typename R>
-inline int launch_render_impl(const KParams<R>& p, int accel, size_t lds_bytes, R* out,
+inline int launch_render_impl(const KParams<R>& p, int world, size_t lds_bytes, R* out,
                               hipStream_t stream, hipEvent_t mid) {
-    (void)accel;
-    const uint32_t blocks = (p.n_items + kWavesPerBlock - 1) / kWavesPerBlock;
+    const uint32_t blocks = (p.n_tasks + kWavesPerBlock - 1) / kWavesPerBlock;
     if (blocks) {
-        if (lds_bytes) {
-            hipLaunchKernelGGL((dev::render_brute_kernel<R, true>), dim3(blocks), dim3(kBlock),
+        if (world == kWorldLds) {
+            hipLaunchKernelGGL((dev::render_kernel<R, kWorldLds>), dim3(blocks), dim3(kBlock),
                                lds_bytes, stream, p);
+        } else if (world == kWorldBvh) {
+            hipLaunchKernelGGL((dev::render_kernel<R, kWorldBvh>), dim3(blocks), dim3(kBlock),
+                               (size_t)kWavesPerBlock * kBvhStack * 64 * sizeof(int32_t), stream, p);
         } else {
-            hipLaunchKernelGGL((dev::render_brute_kernel<R, false>), dim3(blocks), dim3(kBlock), 0,
+            hipLaunchKernelGGL((dev::render_kernel<R, kWorldGlobal>), dim3(blocks), dim3(kBlock), 0,
                                stream, p);
         }
         if (hipGetLastError() != hipSuccess) return -1;

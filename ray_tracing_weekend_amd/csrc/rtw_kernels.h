@@ -13,6 +13,12 @@ constexpr uint32_t kTile = 8;          // 8 x 8 pixel tile = one wavefront of 64
 constexpr uint32_t kWavesPerBlock = 4; // 256-thread workgroups, one tile item per wave
 constexpr uint32_t kBlock = 64 * kWavesPerBlock;
 
+// world query of the render kernel
+enum WorldMode : int { kWorldGlobal = 0, kWorldLds = 1, kWorldBvh = 2 };
+
+// material kinds (same codes as RTW_LAMBERTIAN.. in include/rtw.h)
+enum : uint32_t { kMatLambertian = 0, kMatMetal = 1, kMatDielectric = 2, kMatInvisible = 3 };
+
 template <typename R>
 struct alignas(4 * sizeof(R)) R4 {
     R x, y, z, w;
@@ -22,12 +28,14 @@ struct alignas(4 * sizeof(R)) R4 {
 //   sph      : n_sph   x R4 {cx, cy, cz, r*r}   -- staged into LDS by the brute kernel
 //   sph_r    : n_sph   x R  radius              -- read once per hit (normal)
 //   sph_mat  : n_sph   x u32 material id
-//   planes   : n_pl    x 6 R {px, py, pz, nx, ny, nz}
+//   planes   : n_pl    x 12 R {px, py, pz, nx, ny, nz, aabb lo xyz, aabb hi xyz}
 //   plane_mat: n_pl    x u32
 //   mat_type : n_mat   x u32
 //   mat_p    : n_mat   x R4 {albedo r, g, b, fuzz | ior}
 //   lights   : n_li    x R4 {cx, cy, cz, r}     -- staged into LDS
-//   bvh      : n_nodes x BvhNode<R> (RTW_ACCEL_BVH only)
+//   bvh      : n_nodes x BvhNode<R>            -- RTW_ACCEL_BVH
+//   bsph     : n_sph   x R4 {cx, cy, cz, r*r} in BVH leaf order
+//   bid      : n_sph   x u32 original sphere index of bsph[k]
 template <typename R>
 struct BvhNode {
     // two child boxes per node (children tested together, the classic
@@ -50,32 +58,36 @@ struct DevScene {
     const R4<R>* mat_p;
     const R4<R>* lights;
     const BvhNode<R>* bvh;
-    uint32_t n_sph, n_planes, n_mat, n_lights, n_nodes;
+    const R4<R>* bsph;
+    const uint32_t* bid;
+    uint32_t n_sph, n_planes, n_mat, n_lights, n_nodes, bvh_depth;
 };
+
+constexpr uint32_t kBvhStack = 32;    // per-lane traversal stack entries (LDS)
 
 template <typename R>
 struct KParams {
     DevScene<R> sc;
-    R* partial;                       // [n_chunks][n_local_tiles][64][3] chunk sums
+    R* partial;                       // [n_chunks][n_local_tiles][64][3] item (chunk) sums
     unsigned long long* counters;     // [0] segments, [1] lambertian
     R center[3], p00[3], du[3], dv[3], disk_u[3], disk_v[3], bg[3];
     R u_scale;                        // Uniform::new_inclusive(-0.5, 0.5) scale
     uint64_t seed;
     uint32_t defocus;                 // defocus_angle > f64::EPSILON
     uint32_t W, H, spp, max_depth;
-    uint32_t chunk, n_chunks;
+    uint32_t chunk, n_chunks;         // samples per item, items per pixel
+    uint32_t group, n_groups;         // chunks per wave task, tasks per tile
     uint32_t tiles_x, n_local_tiles, rank, nranks;
-    uint32_t n_items;                 // n_local_tiles * n_chunks
+    uint32_t n_tasks;                 // n_local_tiles * n_groups
 };
 
 // Host-side launch helpers (defined in render_f32.hip / render_f64.hip).
-// accel: 1 = brute force (LDS-staged sphere list when it fits), 2 = BVH.
-// `lds_bytes` = 0 selects the global-memory sphere loop.
+// world: a WorldMode; lds_bytes: dynamic LDS of the kWorldLds variant.
 // `mid` (may be null) is recorded on `stream` between the render kernel and
 // the chunk reduction, so the render kernel can be timed on its own.
-int launch_render_f32(const KParams<float>& p, int accel, size_t lds_bytes, float* out,
+int launch_render_f32(const KParams<float>& p, int world, size_t lds_bytes, float* out,
                       hipStream_t stream, hipEvent_t mid);
-int launch_render_f64(const KParams<double>& p, int accel, size_t lds_bytes, double* out,
+int launch_render_f64(const KParams<double>& p, int world, size_t lds_bytes, double* out,
                       hipStream_t stream, hipEvent_t mid);
 
 }  // namespace rtw

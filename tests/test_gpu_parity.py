@@ -185,3 +185,40 @@ def test_public_render_api_roundtrip(tmp_path):
     n = rtw.write_ppm(str(tmp_path / "image.ppm"), sums, 2)
     text = (tmp_path / "image.ppm").read_text().splitlines()
     assert text[:3] == ["P3", "20 12", "255"] and len(text) == 3 + 240 and n > 0
+
+
+def _same(a, b):
+    return np.array_equal(np.nan_to_num(a, nan=-7.0), np.nan_to_num(b, nan=-7.0))
+
+
+@pytest.mark.parametrize("prec", [rtw.RTW_F32, rtw.RTW_F64])
+@pytest.mark.parametrize("n", [11, 30])
+def test_bvh_equals_brute_force(prec, n):
+    """RTW_ACCEL_BVH only culls: the closest hit, hence every pixel, must be
+    bit-identical to the brute-force sweep (same per-sphere arithmetic)."""
+    soa, b = _scene(n)
+    cam = b.with_image_width(64).with_image_height(40).with_samples_per_pixel(6).with_max_depth(50).build()
+    brute, _, cb = _render_gpu(soa, cam, 13, prec, accel=rtw.RTW_ACCEL_BRUTE)
+    bvh, _, cv = _render_gpu(soa, cam, 13, prec, accel=rtw.RTW_ACCEL_BVH)
+    assert _same(brute, bvh)
+    assert cb == cv
+
+
+def test_bvh_f64_matches_oracle_custom_scene():
+    world = rtw.HittableList()
+    rng = np.random.default_rng(3)
+    for k in range(200):
+        c = rng.uniform(-3, 3, 3)
+        kind = k % 3
+        mat = [rtw.Lambertian(rng.uniform(0, 1, 3)), rtw.Metal(rng.uniform(0.5, 1, 3), rng.uniform(0, 0.5)),
+               rtw.Dialectric(1.5)][kind]
+        world.add(rtw.Sphere(tuple(c), float(rng.uniform(0.05, 0.6)), mat))
+    lights = rtw.HittableList([rtw.Sphere((0, 4, 0), 1.0), rtw.Sphere((2, 2, 2), 0.3)])
+    soa = rtw.flatten(world, lights)
+    cam = rtw.CameraBuilder().with_image_width(32).with_image_height(24).with_samples_per_pixel(4) \
+        .with_max_depth(30).with_lookfrom((0, 1, 9)).with_lookat((0, 0, 0)).with_vfov(50) \
+        .with_background((0.6, 0.7, 1.0)).build()
+    gpu, chunk, _ = _render_gpu(soa, cam, 17, rtw.RTW_F64, accel=rtw.RTW_ACCEL_BVH)
+    ref, _ = _render_oracle(soa, cam, 17, chunk)
+    mae, exact = _compare_f64(gpu, ref, 4)
+    assert mae < F64_MAE_TOL and exact > 0.999
