@@ -32,11 +32,15 @@ SCENE_SEED = 0x5EED0001
 W, H, SPP, DEPTH = 1200, 800, 500, 50
 PEAK_FP32_TFLOPS = 157.3     # MI355X vector FP32 (MI355X_MICROARCH.md, chip table)
 PEAK_FP64_TFLOPS = 78.6      # MI355X vector FP64
-# Algorithmic flops of the brute-force closest-hit:
+# Algorithmic flops of one segment's work, priced from
+# the kernel's own counters (segments, Lambertian bounces, BVH node visits,
+# ray-sphere tests):
 FLOP_SPHERE = 17             # oc (3) + half_b (5) + c = oc.oc - r^2 (6) + disc (3)
+FLOP_BOX = 20                # one child slab test: 6 x (lo*inv - o*inv) + 6 min/max + 2 clamps
 FLOP_PLANE = 6               # d.n (5) + compare
 FLOP_LAMBERT_BASE = 40       # mixture sample + ONB + cosine pdf, per Lambertian bounce
 FLOP_LIGHT = 17              # one light's Sphere::hit discriminant in HittablePdf::value
+ACCEL_NAMES = {1: "brute_lds", 2: "bvh"}
 
 
 def parse():
@@ -48,6 +52,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="target CPU time of the cpu_baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--accel", choices=["auto", "brute", "bvh"], default="auto")
     return ap.parse_args()
 
 
@@ -108,6 +113,7 @@ def main():
     cam = builder.with_image_width(W).with_image_height(H).with_samples_per_pixel(SPP) \
                  .with_max_depth(DEPTH).build()
     r = rtw.Renderer(device=dev.index, precision=prec)
+    r.set_accel({"auto": rtw.RTW_ACCEL_AUTO, "brute": rtw.RTW_ACCEL_BRUTE, "bvh": rtw.RTW_ACCEL_BVH}[a.accel])
     r.set_scene(scene)
     t_rows = rtw.tile_rows()
     my_rows = rtw.rows_for_rank(H, rank, world_size)
@@ -166,11 +172,12 @@ def main():
         if dist is not None:
             dist.destroy_process_group()
         return
-    # roofline of the dominant kernel (render_brute_kernel): algorithmic flops
-    # of this rank's last launch / its average launch duration
+    # roofline of the dominant kernel (render_kernel): algorithmic flops of
+    # this rank's last launch / its average launch duration
     n_sph, n_pl, n_li = len(scene.sphere_mat), len(scene.plane_mat), len(scene.lights)
-    flops = st.segments * (FLOP_SPHERE * n_sph + FLOP_PLANE * n_pl) + \
-        st.lambertian * (FLOP_LIGHT * n_li + FLOP_LAMBERT_BASE)
+    flops = st.node_visits * 2 * FLOP_BOX + st.sphere_tests * FLOP_SPHERE + \
+        st.segments * FLOP_PLANE * n_pl + st.lambertian * (FLOP_LIGHT * n_li + FLOP_LAMBERT_BASE)
+    accel = ACCEL_NAMES.get(int(st.accel), str(st.accel))
     avg_ms = float(np.mean(render_ms)) if render_ms else float("nan")
     achieved = flops / (avg_ms * 1e-3) / 1e12
     peak = PEAK_FP32_TFLOPS if prec == rtw.RTW_F32 else PEAK_FP64_TFLOPS
@@ -191,12 +198,15 @@ def main():
         "config": {"workload": f"book1_simple_{W}x{H}_{SPP}spp_depth{DEPTH}", "width": W,
                    "height": H, "spp": SPP, "max_depth": DEPTH, "spheres": n_sph,
                    "lights": n_li, "parallelism": f"rowtile{world_size}",
-                   "accel": "brute_lds", "chunk": int(st.chunk)},
+                   "accel": accel, "chunk": int(st.chunk)},
         "roofline": {"bound": "valu", "achieved": round(achieved, 3), "peak": peak,
                      "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": None,
-                     "kernel": "render_brute_kernel", "kernel_ms_avg": round(avg_ms, 3),
+                     "kernel": f"render_kernel<{a.precision}, {accel}>",
+                     "kernel_ms_avg": round(avg_ms, 3),
                      "flops_per_launch": int(flops),
                      "segments_per_sample": round(st.segments / max(st.samples, 1), 4),
+                     "node_visits_per_segment": round(st.node_visits / max(st.segments, 1), 3),
+                     "sphere_tests_per_segment": round(st.sphere_tests / max(st.segments, 1), 3),
                      "lambertian_per_sample": round(st.lambertian / max(st.samples, 1), 4)},
     }
     if world_size == 1 and not a.no_cpu_baseline:

@@ -108,6 +108,8 @@ typedef struct rtw_stats {
     double kernel_ms;             /* device time of the last render (HIP events) */
     uint32_t accel;               /* RTW_ACCEL_* actually used */
     uint32_t chunk;               /* samples per work item */
+    uint64_t node_visits;         /* BVH inner nodes entered (RTW_ACCEL_BVH) */
+    uint64_t sphere_tests;        /* ray-sphere discriminant evaluations */
 } rtw_stats;
 
 typedef struct rtw_ctx rtw_ctx;

@@ -14,8 +14,10 @@
  *    algorithm on 64-bit targets) seeded through splitmix64 from
  *    (seed, pixel, sample).  The distributions on top of it restate rand
  *    0.8.6's published algorithms (Standard, Open01, Uniform::new_inclusive,
- *    gen_range's widening multiply, SliceRandom::shuffle,
- *    IteratorRandom::choose) and keep the reference's draw ORDER.
+ *    gen_range's widening multiply) in the reference's draw order, except
+ *    for two draws that cannot change any sampled law: the light pick is one
+ *    gen_index(n) (choose()'s reservoir step adds a gen_index(1)), and
+ *    UnitSphere does not shuffle its three i.i.d. coordinates.
  *  - cos/sin of 2*pi*r are evaluated by rtwo_sincos_2pi (fdlibm kernel
  *    polynomials after an exact quadrant reduction of r) instead of libm's
  *    cos(2*PI*r); both are within ~1 ulp of the true value.  The GPU f64 path
@@ -218,15 +220,14 @@ uint32_t rtwo_rand_index(uint64_t st[4], uint32_t n) {
 /* ------------------------------------------------------------------------ */
 /* Random utilities (shared/src/utils.rs:93-161)                            */
 /* ------------------------------------------------------------------------ */
-static v3 unit_sphere(uint64_t st[4]) {                                       /* utils.rs:99-122 */
+/* UnitSphere, utils.rs:99-122: rejection sampling in the cube [-1, 1)^3.  The
+ * reference shuffles the three i.i.d. coordinates before the test
+ * (utils.rs:116, two gen_index draws); a permutation of i.i.d. coordinates
+ * does not change their joint law, so the build draws no shuffle indices. */
+static v3 unit_sphere(uint64_t st[4]) {
     for (;;) {
         double in[3];
         for (int k = 0; k < 3; ++k) in[k] = 2.0 * rtwo_rand_std(st) - 1.0;
-        /* SliceRandom::shuffle: for i in (1..len).rev() swap(i, gen_index(i+1)) */
-        for (uint32_t i = 2; i >= 1; --i) {
-            uint32_t j = rtwo_rand_index(st, i + 1);
-            double tmp = in[i]; in[i] = in[j]; in[j] = tmp;
-        }
         v3 out = mk(in[0], in[1], in[2]);
         if (dot(out, out) < 1.0) return out;
     }
@@ -730,18 +731,12 @@ static double lights_pdf_value(const rtwo_scene *sc, v3 o, v3 d) {
     return acc / (double)sc->n_lights;
 }
 /* HittableList::random, hittable_list.rs:414-419: iter_hittable().choose(rng)
- * (rand 0.8.6 IteratorRandom::choose over a flat_map whose size_hint becomes
- * exact after the first element), then Sphere::random */
+ * picks a light uniformly, then Sphere::random.  rand 0.8.6's
+ * IteratorRandom::choose reaches that uniform pick through a reservoir step
+ * over the flat_map (an extra gen_index(1) draw, then gen_index(n)); the build
+ * draws the uniform index directly with one gen_index(n). */
 static v3 lights_random(const rtwo_scene *sc, v3 o, uint64_t st[4]) {
-    uint32_t n = sc->n_lights;
-    uint32_t pick = 0;
-    (void)rtwo_rand_index(st, 1);            /* first element, consumed = 1 */
-    if (n == 2) {
-        if (rtwo_rand_index(st, 2) == 0) pick = 1;
-    } else if (n >= 3) {
-        uint32_t ix = rtwo_rand_index(st, n);  /* gen_index(lower + consumed) */
-        pick = ix < n - 1 ? ix + 1 : 0;
-    }
+    const uint32_t pick = rtwo_rand_index(st, sc->n_lights);
     const double *s = sc->lights + 4 * pick;
     return sphere_random(ld(s), s[3], o, st);
 }

@@ -59,6 +59,7 @@ class rtw_stats(C.Structure):
     _fields_ = [
         ("samples", C.c_uint64), ("segments", C.c_uint64), ("lambertian", C.c_uint64),
         ("kernel_ms", C.c_double), ("accel", C.c_uint32), ("chunk", C.c_uint32),
+        ("node_visits", C.c_uint64), ("sphere_tests", C.c_uint64),
     ]
 
 

@@ -21,11 +21,12 @@ struct rtw_ctx {
     int precision = RTW_F32;
     int accel = RTW_ACCEL_AUTO;
     uint32_t chunk = 0;           // samples per item (0 = auto_chunk)
-    uint32_t auto_chunk = 8;
+    uint32_t auto_chunk = 2;
     uint32_t group = 0;           // chunks per wave task (0 = from target_tasks)
-    uint64_t target_tasks = 1u << 17;
+    uint64_t target_tasks = 1u << 18;
     int world_pref = 1;           // 1: LDS-staged sphere list when it fits, 0: global
-    int auto_accel = RTW_ACCEL_BRUTE;   // what RTW_ACCEL_AUTO resolves to
+    int auto_accel = RTW_ACCEL_AUTO;    // RTW_ACCEL_AUTO resolves to this (AUTO: by scene size)
+    int bvh_ww = 1;               // BVH traversal: 1 = while-while + leaf postponing, 0 = one loop
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     // ring of per-render event triples: [start, after render kernel, after reduce]
@@ -46,6 +47,7 @@ struct rtw_ctx {
     unsigned long long* d_counters = nullptr;
     std::vector<unsigned char> h_out;
     rtw_stats last{};
+    uint32_t last_n_sph = 0;
     std::string err;
 };
 
@@ -272,14 +274,15 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
     p.partial = reinterpret_cast<R*>(c->d_partial);
     p.counters = c->d_counters;
     if (!stream) stream = c->stream;
-    HIP_TRY(c, hipMemsetAsync(c->d_counters, 0, 2 * sizeof(unsigned long long), stream));
+    HIP_TRY(c, hipMemsetAsync(c->d_counters, 0, 4 * sizeof(unsigned long long), stream));
     const size_t lds = (size_t)(p.sc.n_sph + p.sc.n_lights) * sizeof(rtw::R4<R>);
-    const int accel = c->accel == RTW_ACCEL_AUTO ? c->auto_accel : c->accel;
+    int accel = c->accel == RTW_ACCEL_AUTO ? c->auto_accel : c->accel;
+    if (accel == RTW_ACCEL_AUTO) accel = p.sc.n_sph >= 64 ? RTW_ACCEL_BVH : RTW_ACCEL_BRUTE;
     int world = (c->world_pref == 0 || lds > kLdsLimit) ? rtw::kWorldGlobal : rtw::kWorldLds;
     if (accel == RTW_ACCEL_BVH) {
         if (p.sc.bvh_depth > rtw::kBvhStack)
             return fail(c, RTW_E_UNSUPPORTED, "BVH deeper than the kernel's traversal stack");
-        world = rtw::kWorldBvh;
+        world = c->bvh_ww ? rtw::kWorldBvhWW : rtw::kWorldBvh;
     }
     hipEvent_t* ev = c->ring[c->n_renders % rtw_ctx::kRing];
     HIP_TRY(c, hipEventRecord(c->ev0, stream));
@@ -301,6 +304,7 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
     c->last = rtw_stats{};
     c->last.samples = (uint64_t)rtw_rows_for_rank(p.H, rank, nranks) * p.W * p.spp;
     c->last.accel = (uint32_t)accel;
+    c->last_n_sph = p.sc.n_sph;
     c->last.chunk = chunk;
     return RTW_OK;
 }
@@ -370,7 +374,8 @@ int rtw_set_tuning(rtw_ctx* c, const char* key, int64_t value) {
     else if (k == "group") c->group = (uint32_t)value;
     else if (k == "target_tasks") c->target_tasks = std::max<uint64_t>(1, (uint64_t)value);
     else if (k == "lds") c->world_pref = value ? 1 : 0;
-    else if (k == "auto_accel") c->auto_accel = value == RTW_ACCEL_BVH ? RTW_ACCEL_BVH : RTW_ACCEL_BRUTE;
+    else if (k == "bvh_ww") c->bvh_ww = value ? 1 : 0;
+    else if (k == "auto_accel") c->auto_accel = (int)std::min<int64_t>(value, RTW_ACCEL_BVH);
     else return fail(c, RTW_E_INVALID, "unknown tuning key " + k);
     return RTW_OK;
 }
@@ -526,12 +531,15 @@ int rtw_get_stats(rtw_ctx* c, rtw_stats* out) {
     if (!c || !out) return RTW_E_INVALID;
     HIP_TRY(c, hipSetDevice(c->device));
     HIP_TRY(c, hipEventSynchronize(c->ev1));
-    unsigned long long h[2] = {0, 0};
+    unsigned long long h[4] = {0, 0, 0, 0};
     HIP_TRY(c, hipMemcpy(h, c->d_counters, sizeof h, hipMemcpyDeviceToHost));
     float ms = 0.f;
     HIP_TRY(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
     c->last.segments = h[0];
     c->last.lambertian = h[1];
+    c->last.node_visits = h[2];
+    // the brute-force sweep tests every sphere on every segment
+    c->last.sphere_tests = c->last.accel == RTW_ACCEL_BVH ? h[3] : h[0] * (uint64_t)c->last_n_sph;
     c->last.kernel_ms = ms;
     *out = c->last;
     return RTW_OK;

@@ -119,6 +119,52 @@ __device__ __forceinline__ void sweep_spheres(const R4<float>* __restrict__ sph,
     tb = __uint_as_float(ub + tminb);
 }
 
+// Sum of Sphere::pdf_value over the light list in list order
+// (HittableList::pdf_value, hittable_list.rs:408-412; sphere.rs:101-111).
+// f64: the reference's arithmetic, light by light.
+__device__ __forceinline__ double lights_pdf_sum(const R4<double>* __restrict__ li, uint32_t n,
+                                                 V3<double> o, V3<double> d) {
+    double acc = 0.0;
+    for (uint32_t k = 0; k < n; ++k) {
+        const R4<double> L = li[k];
+        acc = acc + sphere_pdf_value(mk(L.x, L.y, L.z), L.w, o, d);
+    }
+    return acc;
+}
+// f32: pass 1 finds the lights the ray hits without a square root -- with
+// disc > 0 the far root (-hb + sqrt(disc)) / a is >= 0 exactly when hb <= 0
+// or c <= 0 -- into a bit mask; pass 2 adds the hit lights' solid-angle pdfs
+// in list order.  Most rays hit zero or one light.
+__device__ __forceinline__ float lights_pdf_sum(const R4<float>* __restrict__ li, uint32_t n,
+                                                V3<float> o, V3<float> d) {
+    const float a = dot(d, d);
+    float acc = 0.f;
+    for (uint32_t base = 0; base < n; base += 32) {
+        const uint32_t m = min(32u, n - base);
+        uint32_t mask = 0;
+#pragma unroll 4
+        for (uint32_t k = 0; k < m; ++k) {
+            const R4<float> L = li[base + k];
+            const float ocx = o.x - L.x, ocy = o.y - L.y, ocz = o.z - L.z;
+            const float hb = d.x * ocx + d.y * ocy + d.z * ocz;
+            const float c = ocx * ocx + (ocy * ocy + (ocz * ocz - L.w * L.w));
+            const float disc = hb * hb - a * c;
+            const bool hit = (disc > 0.f) & ((hb <= 0.f) | (c <= 0.f));
+            mask |= (hit ? 1u : 0u) << k;
+        }
+        while (mask) {
+            const uint32_t k = (uint32_t)__builtin_ctz(mask);
+            mask &= mask - 1u;
+            const R4<float> L = li[base + k];
+            const float cx = L.x - o.x, cy = L.y - o.y, cz = L.z - o.z;
+            const float dist2 = cx * cx + cy * cy + cz * cz;
+            const float cos_max = __builtin_amdgcn_sqrtf(1.f - L.w * L.w * __builtin_amdgcn_rcpf(dist2));
+            acc += __builtin_amdgcn_rcpf(6.283185307179586f * (1.f - cos_max));
+        }
+    }
+    return acc;
+}
+
 // ---------------------------------------------------------------------------
 // BVH closest hit (RTW_ACCEL_BVH).  Box tests only cull; every surviving
 // sphere goes through the same per-sphere arithmetic as the brute-force
@@ -173,7 +219,8 @@ __device__ __forceinline__ float inv_(float x) { return __builtin_amdgcn_rcpf(x)
 // Slab test on padded child boxes against [0, tb].
 template <typename R>
 __device__ __forceinline__ void bvh_traverse(const DevScene<R>& sc, int32_t base, V3<R> o, V3<R> d,
-                                             SphereTester<R>& T, int32_t* __restrict__ stk) {
+                                             SphereTester<R>& T, int32_t* __restrict__ stk,
+                                             uint32_t& nvis, uint32_t& ntest) {
     const R ix = inv_(d.x), iy = inv_(d.y), iz = inv_(d.z);
     const R oix = o.x * ix, oiy = o.y * iy, oiz = o.z * iz;
     const BvhNode<R>* __restrict__ nodes = sc.bvh;
@@ -181,6 +228,7 @@ __device__ __forceinline__ void bvh_traverse(const DevScene<R>& sc, int32_t base
     int32_t node = 0;
     for (;;) {
         if (node >= 0) {
+            ++nvis;
             const BvhNode<R>& nd = nodes[node];
             const R tb = T.bound();
             R tn[2], tf[2];
@@ -213,6 +261,7 @@ __device__ __forceinline__ void bvh_traverse(const DevScene<R>& sc, int32_t base
             const uint32_t first = code >> 4, cnt = code & 15u;
             for (uint32_t k = 0; k < cnt; ++k)
                 T.test(sc.bsph[first + k], base + (int32_t)sc.bid[first + k]);
+            ntest += cnt;
             if (sp == 0) break;
             --sp;
             node = stk[sp * 64];
@@ -220,17 +269,84 @@ __device__ __forceinline__ void bvh_traverse(const DevScene<R>& sc, int32_t base
     }
 }
 
+// "While-while" traversal with leaf postponing (Aila & Laine 2009): inner
+// nodes and leaves are processed in separate wave-uniform phases, so the
+// SIMD never runs the box-test and the sphere-test code under one divergent
+// branch.  A lane that reaches a leaf parks it and keeps descending until it
+// holds a second leaf; the inner phase ends when every lane holds a leaf (or
+// is done), then all parked leaves are tested together.
+template <typename R>
+__device__ __forceinline__ void bvh_traverse_ww(const DevScene<R>& sc, int32_t base, V3<R> o, V3<R> d,
+                                                SphereTester<R>& T, int32_t* __restrict__ stk,
+                                                uint32_t& nvis, uint32_t& ntest) {
+    constexpr int32_t kDone = 0x7fffffff;
+    const R ix = inv_(d.x), iy = inv_(d.y), iz = inv_(d.z);
+    const R oix = o.x * ix, oiy = o.y * iy, oiz = o.z * iz;
+    const BvhNode<R>* __restrict__ nodes = sc.bvh;
+    int32_t sp = 0;
+    int32_t node = 0;   // inner node index, leaf code (< 0) or kDone
+    int32_t leaf = 0;   // parked leaf code, 0 = none
+    for (;;) {
+        for (;;) {
+            if (node < 0 && leaf == 0) {   // park the leaf, continue with the stack
+                leaf = node;
+                node = sp ? stk[--sp * 64] : kDone;
+            }
+            const bool inner = node >= 0 && node != kDone;
+            if (!__any(inner) || __all(leaf != 0 || node == kDone)) break;
+            if (inner) {
+                ++nvis;
+                const BvhNode<R>& nd = nodes[node];
+                const R tb = T.bound();
+                R tn[2], tf[2];
+#pragma unroll
+                for (int c = 0; c < 2; ++c) {
+                    const R x0 = nd.lo_x[c] * ix - oix, x1 = nd.hi_x[c] * ix - oix;
+                    const R y0 = nd.lo_y[c] * iy - oiy, y1 = nd.hi_y[c] * iy - oiy;
+                    const R z0 = nd.lo_z[c] * iz - oiz, z1 = nd.hi_z[c] * iz - oiz;
+                    tn[c] = fmax(fmax(fmin(x0, x1), fmin(y0, y1)), fmax(fmin(z0, z1), (R)0));
+                    tf[c] = fmin(fmin(fmax(x0, x1), fmax(y0, y1)), fmin(fmax(z0, z1), tb));
+                }
+                const bool h0 = tn[0] <= tf[0], h1 = tn[1] <= tf[1];
+                const int32_t c0 = nd.child[0], c1 = nd.child[1];
+                if (h0 && h1) {
+                    const bool first0 = tn[0] <= tn[1];
+                    stk[sp * 64] = first0 ? c1 : c0;
+                    ++sp;
+                    node = first0 ? c0 : c1;
+                } else if (h0 | h1) {
+                    node = h0 ? c0 : c1;
+                } else {
+                    node = sp ? stk[--sp * 64] : kDone;
+                }
+            }
+        }
+        if (!__any(leaf != 0)) break;   // no parked leaves: every lane is done
+        if (leaf != 0) {
+            const uint32_t code = (uint32_t)~leaf;
+            const uint32_t first = code >> 4, cnt = code & 15u;
+            for (uint32_t k = 0; k < cnt; ++k)
+                T.test(sc.bsph[first + k], base + (int32_t)sc.bid[first + k]);
+            ntest += cnt;
+            leaf = 0;
+        }
+    }
+}
+
+template <bool kWW>
 __device__ __forceinline__ void bvh_closest(const DevScene<double>& sc, int32_t base, V3<double> o,
                                             V3<double> d, double tmin, double& tb, int32_t& best,
-                                            int32_t* stk) {
+                                            int32_t* stk, uint32_t& nvis, uint32_t& ntest) {
     SphereTester<double> T{o, d, tmin, tb, best};
-    bvh_traverse(sc, base, o, d, T, stk);
+    if constexpr (kWW) bvh_traverse_ww(sc, base, o, d, T, stk, nvis, ntest);
+    else bvh_traverse(sc, base, o, d, T, stk, nvis, ntest);
     tb = T.tb;
     best = T.best;
 }
+template <bool kWW>
 __device__ __forceinline__ void bvh_closest(const DevScene<float>& sc, int32_t base, V3<float> o,
                                             V3<float> d, float tmin, float& tb, int32_t& best,
-                                            int32_t* stk) {
+                                            int32_t* stk, uint32_t& nvis, uint32_t& ntest) {
     SphereTester<float> T;
     T.o = o;
     T.d = d;
@@ -239,13 +355,16 @@ __device__ __forceinline__ void bvh_closest(const DevScene<float>& sc, int32_t b
     T.tminb = __float_as_uint(tmin);
     T.ub = __float_as_uint(tb) - T.tminb;
     T.best = best;
-    bvh_traverse(sc, base, o, d, T, stk);
+    if constexpr (kWW) bvh_traverse_ww(sc, base, o, d, T, stk, nvis, ntest);
+    else bvh_traverse(sc, base, o, d, T, stk, nvis, ntest);
     tb = T.bound();
     best = T.best;
 }
 
 template <typename R, int kWorld>
-__global__ void __launch_bounds__(kBlock) render_kernel(const KParams<R> p) {
+// f32: ask for 5 waves per SIMD (<= 96 VGPRs; the kernel fits without
+// spilling); f64 keeps the compiler's choice.
+__global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? 5 : 1) render_kernel(const KParams<R> p) {
     using PR = P<R>;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     R4<R>* s_sph = reinterpret_cast<R4<R>*>(smem);
@@ -288,7 +407,7 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams<R> p) {
     Rng g;
     V3<R> o = zero, d = zero, mult = zero, res = zero;
     uint32_t depth = 0;
-    uint32_t segs = 0, lambs = 0;
+    uint32_t segs = 0, lambs = 0, nvis = 0, ntest = 0;
     bool active = false, need = true;
 
     auto start_sample = [&]() {
@@ -369,9 +488,10 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams<R> p) {
                     best = k;
                 }
             }
-            if constexpr (kWorld == kWorldBvh) {
-                bvh_closest(p.sc, nplanes, o, d, tmin, tb, best,
-                            reinterpret_cast<int32_t*>(smem) + wave * kBvhStack * 64 + lane);
+            if constexpr (kWorld == kWorldBvh || kWorld == kWorldBvhWW) {
+                bvh_closest<kWorld == kWorldBvhWW>(p.sc, nplanes, o, d, tmin, tb, best,
+                            reinterpret_cast<int32_t*>(smem) + wave * kBvhStack * 64 + lane, nvis,
+                            ntest);
             } else {
                 sweep_spheres(sph, p.sc.n_sph, nplanes, o, d, tmin, tb, best);
             }
@@ -437,28 +557,16 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams<R> p) {
                     const Onb<R> uvw(nrm);
                     V3<R> dir;
                     if (PR::u_std(g.next()) < (R)0.5) {
-                        // HittableList::random (hittable_list.rs:414-419): choose()
-                        const uint32_t nl = p.sc.n_lights;
-                        uint32_t pick = 0;
-                        (void)g.index(1);
-                        if (nl == 2) {
-                            if (g.index(2) == 0) pick = 1;
-                        } else if (nl >= 3) {
-                            uint32_t ix = g.index(nl);
-                            pick = ix < nl - 1 ? ix + 1 : 0;
-                        }
-                        const R4<R> L = li[pick];
+                        // HittableList::random (hittable_list.rs:414-419): a
+                        // uniform light (one gen_index draw), then Sphere::random
+                        const R4<R> L = li[g.index(p.sc.n_lights)];
                         dir = sphere_random(mk(L.x, L.y, L.z), L.w, pnt, g);
                     } else {
                         dir = uvw.transform(cosine_hemisphere<R>(g));
                     }
                     const V3<R> ndir = PR::normalize(dir);
                     const R cos_w = PR::over_pi(dot(ndir, uvw.w));
-                    R acc = (R)0;                                      // hittable_list.rs:408-412
-                    for (uint32_t k = 0; k < p.sc.n_lights; ++k) {
-                        const R4<R> L = li[k];
-                        acc = acc + sphere_pdf_value(mk(L.x, L.y, L.z), L.w, pnt, dir);
-                    }
+                    const R acc = lights_pdf_sum(li, p.sc.n_lights, pnt, dir);   // hittable_list.rs:408-412
                     const R lpdf = PR::div_(acc, (R)p.sc.n_lights);
                     const R pdf = lpdf * (R)0.5 + PR::max_(cos_w, (R)0) * (R)0.5;
                     const R spdf = PR::max_(PR::over_pi(dot(nrm, ndir)), (R)0);
@@ -502,11 +610,15 @@ __global__ void __launch_bounds__(kBlock) render_kernel(const KParams<R> p) {
     // wave-reduce the counters, one atomic per wave
     for (int off = 32; off > 0; off >>= 1) {
         segs += __shfl_xor(segs, off);
+        nvis += __shfl_xor(nvis, off);
+        ntest += __shfl_xor(ntest, off);
         lambs += __shfl_xor(lambs, off);
     }
     if (lane == 0 && p.counters) {
         atomicAdd(p.counters + 0, (unsigned long long)segs);
         atomicAdd(p.counters + 1, (unsigned long long)lambs);
+        if (nvis) atomicAdd(p.counters + 2, (unsigned long long)nvis);
+        if (ntest) atomicAdd(p.counters + 3, (unsigned long long)ntest);
     }
 }
 
@@ -546,6 +658,9 @@ inline int launch_render_impl(const KParams<R>& p, int world, size_t lds_bytes, 
         if (world == kWorldLds) {
             hipLaunchKernelGGL((dev::render_kernel<R, kWorldLds>), dim3(blocks), dim3(kBlock),
                                lds_bytes, stream, p);
+        } else if (world == kWorldBvhWW) {
+            hipLaunchKernelGGL((dev::render_kernel<R, kWorldBvhWW>), dim3(blocks), dim3(kBlock),
+                               (size_t)kWavesPerBlock * kBvhStack * 64 * sizeof(int32_t), stream, p);
         } else if (world == kWorldBvh) {
             hipLaunchKernelGGL((dev::render_kernel<R, kWorldBvh>), dim3(blocks), dim3(kBlock),
                                (size_t)kWavesPerBlock * kBvhStack * 64 * sizeof(int32_t), stream, p);

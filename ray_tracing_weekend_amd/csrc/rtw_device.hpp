@@ -243,20 +243,15 @@ struct Onb {   // geometry/src/onb.rs:8-35
     }
 };
 
-// utils.rs:99-122 (UnitSphere, rejection + the 3-element shuffle)
+// utils.rs:99-122 (UnitSphere): rejection sampling in [-1, 1)^3.  The
+// reference's shuffle of the three i.i.d. coordinates (utils.rs:116) leaves
+// their law unchanged and is not drawn (as in the oracle).
 template <typename R>
 __device__ __forceinline__ V3<R> unit_sphere(Rng& g) {
     for (;;) {
         R in0 = (R)2 * P<R>::u_std(g.next()) - (R)1;
         R in1 = (R)2 * P<R>::u_std(g.next()) - (R)1;
         R in2 = (R)2 * P<R>::u_std(g.next()) - (R)1;
-        // SliceRandom::shuffle: i = 2 then i = 1, swap(i, gen_index(i + 1))
-        uint32_t j = g.index(3);
-        R t;
-        if (j == 0) { t = in2; in2 = in0; in0 = t; }
-        else if (j == 1) { t = in2; in2 = in1; in1 = t; }
-        j = g.index(2);
-        if (j == 0) { t = in1; in1 = in0; in0 = t; }
         V3<R> out = mk(in0, in1, in2);
         if (dot(out, out) < (R)1) return out;
     }

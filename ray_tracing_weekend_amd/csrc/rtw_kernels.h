@@ -14,7 +14,7 @@ constexpr uint32_t kWavesPerBlock = 4; // 256-thread workgroups, one tile item p
 constexpr uint32_t kBlock = 64 * kWavesPerBlock;
 
 // world query of the render kernel
-enum WorldMode : int { kWorldGlobal = 0, kWorldLds = 1, kWorldBvh = 2 };
+enum WorldMode : int { kWorldGlobal = 0, kWorldLds = 1, kWorldBvh = 2, kWorldBvhWW = 3 };
 
 // material kinds (same codes as RTW_LAMBERTIAN.. in include/rtw.h)
 enum : uint32_t { kMatLambertian = 0, kMatMetal = 1, kMatDielectric = 2, kMatInvisible = 3 };

@@ -1,0 +1,26 @@
+#!/bin/bash
+# rocprofv3 on the bench workload: kernel-trace stats + separate PMC passes
+# (never combined with sys/runtime traces).  Usage: profile.sh TAG [bench args]
+set -u
+ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
+OUT="$ROOT/gpurun_out"; mkdir -p "$OUT"
+TAG="$1"; shift
+ARGS="${*:---steps 2 --warmup 1 --no-cpu-baseline}"
+export TMPDIR=/tmp
+cd /tmp
+bad() { case "$1" in 124|134|137|139) return 0;; *) return 1;; esac; }
+if [ ! -f "$OUT/rocprof_counters.txt" ]; then
+  timeout -k 10 120 rocprofv3 -L > "$OUT/rocprof_counters.txt" 2>&1; echo "list rc=$?"
+fi
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$TAG" -o trace --output-format csv \
+  -- python3 "$ROOT/bench.py" $ARGS > "$OUT/prof_${TAG}_trace.log" 2>&1
+rc=$?; echo "trace rc=$rc"; if bad $rc; then exit $rc; fi
+i=0
+for set in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES" \
+           "SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE" ${EXTRA_PMC:-}; do
+  i=$((i+1))
+  timeout -k 10 600 rocprofv3 --pmc $set -d "$OUT/prof_$TAG/pmc$i" -o pmc --output-format csv \
+    -- python3 "$ROOT/bench.py" $ARGS > "$OUT/prof_${TAG}_pmc$i.log" 2>&1
+  rc=$?; echo "pmc$i ($set) rc=$rc"; if bad $rc; then exit $rc; fi
+done
+exit 0
