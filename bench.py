@@ -27,6 +27,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 import ray_tracing_weekend_amd as rtw  # noqa: E402
+from ray_tracing_weekend_amd import sharding  # noqa: E402
 
 SCENE_SEED = 0x5EED0001
 W, H, SPP, DEPTH = 1200, 800, 500, 50
@@ -115,7 +116,7 @@ def main():
     r = rtw.Renderer(device=dev.index, precision=prec)
     r.set_accel({"auto": rtw.RTW_ACCEL_AUTO, "brute": rtw.RTW_ACCEL_BRUTE, "bvh": rtw.RTW_ACCEL_BVH}[a.accel])
     r.set_scene(scene)
-    t_rows = rtw.tile_rows()
+    assert rtw.tile_rows() == sharding.TILE_ROWS
     my_rows = rtw.rows_for_rank(H, rank, world_size)
     max_rows = max(rtw.rows_for_rank(H, k, world_size) for k in range(world_size))
     buf = torch.zeros((max_rows, W, 3), dtype=tdtype, device=dev)
@@ -123,22 +124,13 @@ def main():
     image = torch.empty((H, W, 3), dtype=tdtype, device=dev) if rank == 0 else None
     stream = torch.cuda.current_stream(dev)
 
-    def assemble():
-        # rank k's packed rows are tile rows t = k, k + N, ...
-        for k in range(world_size):
-            pos = 0
-            for ty in range(k, (H + t_rows - 1) // t_rows, world_size):
-                n = min(t_rows, H - ty * t_rows)
-                image[ty * t_rows: ty * t_rows + n] = gathered[k][pos: pos + n]
-                pos += n
-
     def step(seed):
         r.render_device(cam, seed, buf.data_ptr(), buf.numel() * buf.element_size(),
                         rank=rank, nranks=world_size, stream=stream.cuda_stream)
         if dist is not None:
             dist.gather(buf, gathered, dst=0)
             if rank == 0:
-                assemble()
+                sharding.assemble(image, gathered, H)
         elif image is not None:
             image.copy_(buf[:H])
 

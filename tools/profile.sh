@@ -15,9 +15,11 @@ fi
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$TAG" -o trace --output-format csv \
   -- python3 "$ROOT/bench.py" $ARGS > "$OUT/prof_${TAG}_trace.log" 2>&1
 rc=$?; echo "trace rc=$rc"; if bad $rc; then exit $rc; fi
+# counter sets separated by ';' (PMC_SETS overrides the default list)
+SETS="${PMC_SETS:-FETCH_SIZE;WRITE_SIZE;SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES;SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE}"
 i=0
-for set in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES" \
-           "SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE" ${EXTRA_PMC:-}; do
+IFS=';' read -ra SETLIST <<< "$SETS"
+for set in "${SETLIST[@]}"; do
   i=$((i+1))
   timeout -k 10 600 rocprofv3 --pmc $set -d "$OUT/prof_$TAG/pmc$i" -o pmc --output-format csv \
     -- python3 "$ROOT/bench.py" $ARGS > "$OUT/prof_${TAG}_pmc$i.log" 2>&1
