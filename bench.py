@@ -54,6 +54,7 @@ def parse():
                     help="target CPU time of the cpu_baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--accel", choices=["auto", "brute", "bvh"], default="auto")
+    ap.add_argument("--tuning", default="", help="rtw_set_tuning overrides, e.g. bvh_kind=1,auto_chunk=4")
     return ap.parse_args()
 
 
@@ -115,6 +116,9 @@ def main():
                  .with_max_depth(DEPTH).build()
     r = rtw.Renderer(device=dev.index, precision=prec)
     r.set_accel({"auto": rtw.RTW_ACCEL_AUTO, "brute": rtw.RTW_ACCEL_BRUTE, "bvh": rtw.RTW_ACCEL_BVH}[a.accel])
+    for kv in filter(None, a.tuning.split(",")):
+        k, v = kv.split("=")
+        r.set_tuning(k, int(v))
     r.set_scene(scene)
     assert rtw.tile_rows() == sharding.TILE_ROWS
     my_rows = rtw.rows_for_rank(H, rank, world_size)
@@ -167,7 +171,7 @@ def main():
     # roofline of the dominant kernel (render_kernel): algorithmic flops of
     # this rank's last launch / its average launch duration
     n_sph, n_pl, n_li = len(scene.sphere_mat), len(scene.plane_mat), len(scene.lights)
-    flops = st.node_visits * 2 * FLOP_BOX + st.sphere_tests * FLOP_SPHERE + \
+    flops = st.node_visits * int(st.bvh_width) * FLOP_BOX + st.sphere_tests * FLOP_SPHERE + \
         st.segments * FLOP_PLANE * n_pl + st.lambertian * (FLOP_LIGHT * n_li + FLOP_LAMBERT_BASE)
     accel = ACCEL_NAMES.get(int(st.accel), str(st.accel))
     avg_ms = float(np.mean(render_ms)) if render_ms else float("nan")
@@ -190,13 +194,15 @@ def main():
         "config": {"workload": f"book1_simple_{W}x{H}_{SPP}spp_depth{DEPTH}", "width": W,
                    "height": H, "spp": SPP, "max_depth": DEPTH, "spheres": n_sph,
                    "lights": n_li, "parallelism": f"rowtile{world_size}",
-                   "accel": accel, "chunk": int(st.chunk)},
+                   "accel": accel if accel != "bvh" else f"bvh{int(st.bvh_width)}",
+                   "chunk": int(st.chunk)},
         "roofline": {"bound": "valu", "achieved": round(achieved, 3), "peak": peak,
                      "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": None,
                      "kernel": f"render_kernel<{a.precision}, {accel}>",
                      "kernel_ms_avg": round(avg_ms, 3),
                      "flops_per_launch": int(flops),
                      "segments_per_sample": round(st.segments / max(st.samples, 1), 4),
+                     "bvh_width": int(st.bvh_width),
                      "node_visits_per_segment": round(st.node_visits / max(st.segments, 1), 3),
                      "sphere_tests_per_segment": round(st.sphere_tests / max(st.segments, 1), 3),
                      "lambertian_per_sample": round(st.lambertian / max(st.samples, 1), 4)},

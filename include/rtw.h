@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define RTW_ABI_VERSION 1
+#define RTW_ABI_VERSION 2
 
 /* error codes */
 #define RTW_OK 0
@@ -110,6 +110,8 @@ typedef struct rtw_stats {
     uint32_t chunk;               /* samples per work item */
     uint64_t node_visits;         /* BVH inner nodes entered (RTW_ACCEL_BVH) */
     uint64_t sphere_tests;        /* ray-sphere discriminant evaluations */
+    uint32_t bvh_width;           /* child boxes tested per node visit (4, 2; 0 = no BVH) */
+    uint32_t reserved;
 } rtw_stats;
 
 typedef struct rtw_ctx rtw_ctx;
@@ -125,7 +127,9 @@ int rtw_set_chunk(rtw_ctx *ctx, uint32_t chunk);
 int rtw_set_accel(rtw_ctx *ctx, int accel);
 /* scheduling knobs (benchmarking): "chunk" (samples per item, 0 = auto),
  * "auto_chunk", "group" (chunks per wave task, 0 = auto), "target_tasks",
- * "lds" (1 = stage the sphere list in LDS when it fits, 0 = read it from HBM) */
+ * "lds" (1 = stage the sphere list in LDS when it fits, 0 = read it from HBM),
+ * "bvh_kind" (2 = 4-wide octant BVH, 1 = binary while-while, 0 = binary
+ * single loop), "bvh_ww" (legacy: 1 -> bvh_kind 1, 0 -> 0), "auto_accel" */
 int rtw_set_tuning(rtw_ctx *ctx, const char *key, int64_t value);
 
 /* ---- CameraBuilder::build (camera.rs:114-218) ------------------------- */

@@ -55,11 +55,15 @@ class rtw_scene(C.Structure):
     ]
 
 
+ABI_VERSION = 2     # RTW_ABI_VERSION of include/rtw.h
+
+
 class rtw_stats(C.Structure):
     _fields_ = [
         ("samples", C.c_uint64), ("segments", C.c_uint64), ("lambertian", C.c_uint64),
         ("kernel_ms", C.c_double), ("accel", C.c_uint32), ("chunk", C.c_uint32),
         ("node_visits", C.c_uint64), ("sphere_tests", C.c_uint64),
+        ("bvh_width", C.c_uint32), ("reserved", C.c_uint32),
     ]
 
 
@@ -119,5 +123,8 @@ def load():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    if lib.rtw_abi_version() != ABI_VERSION:
+        raise ImportError(f"{LIB_PATH} has ABI {lib.rtw_abi_version()}, this mirror expects "
+                          f"{ABI_VERSION}: rebuild it")
     _lib = lib
     return lib

@@ -26,7 +26,8 @@ struct rtw_ctx {
     uint64_t target_tasks = 1u << 18;
     int world_pref = 1;           // 1: LDS-staged sphere list when it fits, 0: global
     int auto_accel = RTW_ACCEL_AUTO;    // RTW_ACCEL_AUTO resolves to this (AUTO: by scene size)
-    int bvh_ww = 1;               // BVH traversal: 1 = while-while + leaf postponing, 0 = one loop
+    int bvh_kind = 1;             // BVH traversal: 1 = binary while-while with leaf postponing,
+                                  // 2 = 4-wide octant tree, 0 = binary single loop
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     // ring of per-render event triples: [start, after render kernel, after reduce]
@@ -96,6 +97,8 @@ std::vector<unsigned char> stage_scene(const rtw_scene* s, rtw::DevScene<R>* ds,
     const size_t o_nodes = reserve(sizeof(rtw::BvhNode<R>) * bb.nodes.size());
     const size_t o_bsph = reserve(sizeof(R4) * s->n_spheres);
     const size_t o_bid = reserve(sizeof(uint32_t) * s->n_spheres);
+    const rtw::Bvh4Build b4 = rtw::collapse_bvh4(bb);
+    const size_t o_nodes4 = reserve(sizeof(rtw::Bvh4Node<R>) * 8 * b4.nodes.size());
     std::vector<unsigned char> blob(align_up(off, 64) + 64, 0);
     unsigned char* b = blob.data();
     for (uint32_t k = 0; k < s->n_spheres; ++k) {
@@ -168,6 +171,43 @@ std::vector<unsigned char> stage_scene(const rtw_scene* s, rtw::DevScene<R>* ds,
         reinterpret_cast<R4*>(b + o_bsph)[k] = reinterpret_cast<const R4*>(b + o_sph)[id];
         reinterpret_cast<uint32_t*>(b + o_bid)[k] = id;
     }
+    // 4-wide tree, one copy per ray octant: slots in that octant's
+    // front-to-back order, slab planes pre-selected as near/far (see Bvh4Node)
+    const size_t n4 = b4.nodes.size();
+    for (int oct = 0; oct < 8; ++oct) {
+        for (size_t k = 0; k < n4; ++k) {
+            const rtw::Bvh4Build::Node& n = b4.nodes[k];
+            rtw::Bvh4Node<R> d{};
+            for (uint32_t q = 0; q < 4; ++q) {
+                const uint32_t slot = n.order[oct][q];
+                const bool valid = q < n.n;
+                R nr[3], fr[3];
+                for (int a = 0; a < 3; ++a) {
+                    const bool neg = (oct >> a) & 1;
+                    const R lo = valid ? down(n.lo[slot][a]) : (R)INFINITY;
+                    const R hi = valid ? up(n.hi[slot][a]) : (R)-INFINITY;
+                    // a ray going -a enters through hi and leaves through lo;
+                    // an empty slot maps to near = +inf, far = -inf in ray space
+                    nr[a] = neg ? hi : lo;
+                    fr[a] = neg ? lo : hi;
+                }
+                const int32_t link = valid ? n.child[slot] : rtw::leaf_code(0, 0);
+                R lr = 0;   // the link's bits in an R slot (low 32 bits for double)
+                if constexpr (sizeof(R) == 4) {
+                    memcpy(&lr, &link, 4);
+                } else {
+                    const int64_t l64 = (int64_t)(uint32_t)link;
+                    memcpy(&lr, &l64, 8);
+                }
+                d.a[q] = rtw::R4<R>{nr[0], nr[1], nr[2], fr[0]};
+                d.b[q] = rtw::R4<R>{fr[1], fr[2], lr, (R)0};
+            }
+            reinterpret_cast<rtw::Bvh4Node<R>*>(b + o_nodes4)[oct * n4 + k] = d;
+        }
+    }
+    ds->bvh4 = reinterpret_cast<const rtw::Bvh4Node<R>*>(base + o_nodes4);
+    ds->n_nodes4 = (uint32_t)n4;
+    ds->bvh4_stack = b4.max_stack;
     ds->bvh = reinterpret_cast<const rtw::BvhNode<R>*>(base + o_nodes);
     ds->bsph = reinterpret_cast<const R4*>(base + o_bsph);
     ds->bid = reinterpret_cast<const uint32_t*>(base + o_bid);
@@ -279,10 +319,20 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
     int accel = c->accel == RTW_ACCEL_AUTO ? c->auto_accel : c->accel;
     if (accel == RTW_ACCEL_AUTO) accel = p.sc.n_sph >= 64 ? RTW_ACCEL_BVH : RTW_ACCEL_BRUTE;
     int world = (c->world_pref == 0 || lds > kLdsLimit) ? rtw::kWorldGlobal : rtw::kWorldLds;
+    p.stack = rtw::kBvhStack;
+    uint32_t bvh_width = 0;
     if (accel == RTW_ACCEL_BVH) {
-        if (p.sc.bvh_depth > rtw::kBvhStack)
+        // 4-wide unless its stack bound does not fit (binary needs <= depth)
+        if (c->bvh_kind == 2 && p.sc.bvh4_stack + 1 <= rtw::kBvhStack) {
+            world = rtw::kWorldBvh4;
+            p.stack = p.sc.bvh4_stack + 1;
+            bvh_width = 4;
+        } else if (p.sc.bvh_depth <= rtw::kBvhStack) {
+            world = c->bvh_kind ? rtw::kWorldBvhWW : rtw::kWorldBvh;
+            bvh_width = 2;
+        } else {
             return fail(c, RTW_E_UNSUPPORTED, "BVH deeper than the kernel's traversal stack");
-        world = c->bvh_ww ? rtw::kWorldBvhWW : rtw::kWorldBvh;
+        }
     }
     hipEvent_t* ev = c->ring[c->n_renders % rtw_ctx::kRing];
     HIP_TRY(c, hipEventRecord(c->ev0, stream));
@@ -304,6 +354,7 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
     c->last = rtw_stats{};
     c->last.samples = (uint64_t)rtw_rows_for_rank(p.H, rank, nranks) * p.W * p.spp;
     c->last.accel = (uint32_t)accel;
+    c->last.bvh_width = bvh_width;
     c->last_n_sph = p.sc.n_sph;
     c->last.chunk = chunk;
     return RTW_OK;
@@ -374,7 +425,8 @@ int rtw_set_tuning(rtw_ctx* c, const char* key, int64_t value) {
     else if (k == "group") c->group = (uint32_t)value;
     else if (k == "target_tasks") c->target_tasks = std::max<uint64_t>(1, (uint64_t)value);
     else if (k == "lds") c->world_pref = value ? 1 : 0;
-    else if (k == "bvh_ww") c->bvh_ww = value ? 1 : 0;
+    else if (k == "bvh_ww") c->bvh_kind = value ? 1 : 0;
+    else if (k == "bvh_kind") c->bvh_kind = (int)std::min<int64_t>(value, 2);
     else if (k == "auto_accel") c->auto_accel = (int)std::min<int64_t>(value, RTW_ACCEL_BVH);
     else return fail(c, RTW_E_INVALID, "unknown tuning key " + k);
     return RTW_OK;
@@ -473,7 +525,8 @@ int rtw_set_scene(rtw_ctx* c, const rtw_scene* s) {
     int rc = validate_scene(c, s);
     if (rc) return rc;
     HIP_TRY(c, hipSetDevice(c->device));
-    // stage once against base 0, then rebase the device pointers
+    // stage once against base 0, then rebase the device pointers (EVERY
+    // pointer member of DevScene must be listed in `rebase`)
     rtw::DevScene<float> tmp32{};
     rtw::DevScene<double> tmp64{};
     std::vector<unsigned char> blob = c->precision == RTW_F32 ? stage_scene<float>(s, &tmp32, 0)
@@ -494,7 +547,10 @@ int rtw_set_scene(rtw_ctx* c, const rtw_scene* s) {
         };
         fix(ds.sph); fix(ds.sph_r); fix(ds.sph_mat); fix(ds.planes); fix(ds.plane_mat);
         fix(ds.mat_type); fix(ds.mat_p); fix(ds.lights); fix(ds.bvh); fix(ds.bsph); fix(ds.bid);
+        fix(ds.bvh4);
     };
+    static_assert(sizeof(rtw::DevScene<float>) == 12 * sizeof(void*) + 8 * sizeof(uint32_t),
+                  "DevScene gained a member: update rebase");
     if (c->precision == RTW_F32) {
         rebase(tmp32);
         c->sc32 = tmp32;

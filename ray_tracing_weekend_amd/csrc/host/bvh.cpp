@@ -181,4 +181,136 @@ BvhBuild build_bvh(const double* spheres, uint32_t n, double pad_rel) {
     return out;
 }
 
+namespace {
+
+struct Collapser {
+    const BvhBuild& b;
+    Bvh4Build& out;
+
+    static double area(const double* lo, const double* hi) {
+        const double dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
+        if (!(dx >= 0) || !(dy >= 0) || !(dz >= 0)) return 0.0;
+        return dx * dy + dx * dz + dy * dz;
+    }
+
+    // a child slot: child `side` of binary node `parent`
+    struct Ref {
+        int32_t parent;
+        int side;
+    };
+
+    // front-to-back order (slot indices) of the final children below binary
+    // node `node` for octant `oct` (bit a set: the ray goes -a); `opened`
+    // holds the binary nodes that were opened into this 4-wide node
+    void order(int32_t node, const std::vector<int32_t>& opened, const std::vector<Ref>& slots, int oct,
+               std::vector<int>& seq) const {
+        const BvhBuild::Node& nd = b.nodes[node];
+        // split axis: the largest separation of the two child box centres
+        int axis = 0;
+        double best = -1.0;
+        for (int a = 0; a < 3; ++a) {
+            const double c0 = nd.lo[0][a] + nd.hi[0][a], c1 = nd.lo[1][a] + nd.hi[1][a];
+            const double sep = fabs(c1 - c0);
+            if (std::isfinite(sep) && sep > best) {
+                best = sep;
+                axis = a;
+            }
+        }
+        const double c0 = nd.lo[0][axis] + nd.hi[0][axis], c1 = nd.lo[1][axis] + nd.hi[1][axis];
+        const bool neg = (oct >> axis) & 1;
+        int first = (c0 <= c1) ? 0 : 1;
+        if (neg) first ^= 1;
+        for (int side : {first, first ^ 1}) {
+            const int32_t ch = nd.child[side];
+            if (ch >= 0 && std::find(opened.begin(), opened.end(), ch) != opened.end()) {
+                order(ch, opened, slots, oct, seq);
+            } else {
+                for (size_t k = 0; k < slots.size(); ++k)
+                    if (slots[k].parent == node && slots[k].side == side) seq.push_back((int)k);
+            }
+        }
+    }
+
+    // emit the 4-wide node rooted at binary inner node `bn`; returns its index
+    int32_t emit(int32_t bn, uint32_t level, uint32_t* stack_need) {
+        std::vector<Ref> slots = {{bn, 0}, {bn, 1}};
+        std::vector<int32_t> opened = {bn};
+        while (slots.size() < 4) {
+            int pick = -1;
+            double best = -1.0;
+            for (size_t k = 0; k < slots.size(); ++k) {
+                const int32_t ch = b.nodes[slots[k].parent].child[slots[k].side];
+                if (ch < 0) continue;
+                const BvhBuild::Node& p = b.nodes[slots[k].parent];
+                const double a = area(p.lo[slots[k].side], p.hi[slots[k].side]);
+                if (a > best) {
+                    best = a;
+                    pick = (int)k;
+                }
+            }
+            if (pick < 0) break;
+            const int32_t ch = b.nodes[slots[pick].parent].child[slots[pick].side];
+            slots.erase(slots.begin() + pick);
+            slots.push_back({ch, 0});
+            slots.push_back({ch, 1});
+            opened.push_back(ch);
+        }
+        // drop empty leaves (the root's padding child of a tiny scene)
+        slots.erase(std::remove_if(slots.begin(), slots.end(),
+                                   [&](const Ref& r) {
+                                       const int32_t ch = b.nodes[r.parent].child[r.side];
+                                       return ch < 0 && (((uint32_t)~ch) & 15u) == 0;
+                                   }),
+                    slots.end());
+        const int32_t idx = (int32_t)out.nodes.size();
+        out.nodes.emplace_back();
+        out.depth = std::max(out.depth, level + 1);
+        Bvh4Build::Node nd{};
+        nd.n = (uint32_t)slots.size();
+        for (int k = 0; k < 4; ++k) {
+            nd.child[k] = leaf_code(0, 0);
+            for (int a = 0; a < 3; ++a) {
+                nd.lo[k][a] = INFINITY;
+                nd.hi[k][a] = -INFINITY;
+            }
+        }
+        for (int oct = 0; oct < 8; ++oct) {
+            std::vector<int> seq;
+            order(bn, opened, slots, oct, seq);
+            for (int k = 0; k < 4; ++k) nd.order[oct][k] = (uint8_t)(k < (int)seq.size() ? seq[k] : k);
+        }
+        uint32_t below = 0;
+        for (size_t k = 0; k < slots.size(); ++k) {
+            const BvhBuild::Node& p = b.nodes[slots[k].parent];
+            for (int a = 0; a < 3; ++a) {
+                nd.lo[k][a] = p.lo[slots[k].side][a];
+                nd.hi[k][a] = p.hi[slots[k].side][a];
+            }
+            const int32_t ch = p.child[slots[k].side];
+            if (ch >= 0) {
+                uint32_t need = 0;
+                nd.child[k] = emit(ch, level + 1, &need);
+                below = std::max(below, need);
+            } else {
+                nd.child[k] = ch;
+            }
+        }
+        out.nodes[idx] = nd;
+        *stack_need = (nd.n ? nd.n - 1 : 0) + below;
+        return idx;
+    }
+};
+
+}  // namespace
+
+Bvh4Build collapse_bvh4(const BvhBuild& b) {
+    Bvh4Build out;
+    if (b.nodes.empty()) return out;
+    Collapser c{b, out};
+    uint32_t need = 0;
+    c.emit(0, 0, &need);
+    out.max_stack = need;
+    return out;
+}
+
 }  // namespace rtw

@@ -38,4 +38,23 @@ inline int32_t leaf_code(uint32_t first, uint32_t count) { return ~(int32_t)((fi
 // box (absorbs the rounding of the device slab test in the kernel precision).
 BvhBuild build_bvh(const double* spheres, uint32_t n, double pad_rel);
 
+// 4-wide BVH collapsed from the binary one (same leaves, same boxes): every
+// node takes the up-to-4 descendants reached by repeatedly opening its
+// largest-area inner child.  For each of the 8 ray-direction octants the
+// children get a front-to-back order from the binary splits they came from
+// (near side first along each split axis), so the kernel needs no sort.
+struct Bvh4Build {
+    struct Node {
+        double lo[4][3], hi[4][3];   // child boxes; slots >= n are empty
+        int32_t child[4];            // >= 0 inner node; < 0 leaf code (leaf_code(0,0) if empty)
+        uint8_t order[8][4];         // per octant: slot of the 1st, 2nd, ... child to visit
+        uint32_t n;
+    };
+    std::vector<Node> nodes;         // nodes[0] is the root
+    uint32_t max_stack = 0;          // most traversal-stack entries any path can hold
+    uint32_t depth = 0;
+};
+
+Bvh4Build collapse_bvh4(const BvhBuild& b);
+
 }  // namespace rtw

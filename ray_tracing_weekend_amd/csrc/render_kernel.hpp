@@ -85,33 +85,43 @@ __device__ __forceinline__ void sweep_spheres(const R4<double>* __restrict__ sph
         }
     }
 }
-// f32 (speed mode): branch-free body so that the compiler keeps a batch of
-// sphere loads in flight.  Both roots come from one reciprocal of a = d.d.
-// The range test "t in [tmin, tb)" is ONE unsigned compare on
-// u = bits(t) - bits(tmin): for t >= 0 float bits are monotonic, while every
-// t < tmin (negative, or in [0, tmin)) and NaN maps above bits(+inf) -
-// bits(tmin) >= any live bound.  Since t0 <= t1, min_u32(u0, u1) is the
-// near root when it is >= tmin, else the far root (sphere.rs:71-80).  A
-// negative discriminant gives sqrt = NaN and so no hit; disc == 0 exactly (a
-// tangent ray) counts as a hit here, where the reference needs disc > 0.
+// f32 (speed mode): the per-sphere test, shared by the brute-force sweep and
+// the BVH leaves so both give bit-identical t; every FMA is spelled out so
+// that contraction cannot differ between the two call sites.  Both roots come
+// from one reciprocal of a = d.d.  The range test "t in [tmin, tb)" is ONE
+// unsigned compare on u = bits(t) - bits(tmin): for t >= 0 float bits are
+// monotonic, while every t < tmin (negative, or in [0, tmin)) and NaN maps
+// above bits(+inf) - bits(tmin) >= any live bound.  Since t0 <= t1,
+// min_u32(u0, u1) is the near root when it is >= tmin, else the far root
+// (sphere.rs:71-80).  A negative discriminant gives sqrt = NaN and so no hit;
+// disc == 0 exactly (a tangent ray) counts as a hit here, where the
+// reference needs disc > 0.
+__device__ __forceinline__ uint32_t sphere_u(const R4<float>& s, V3<float> o, V3<float> d, float a,
+                                             float ia, uint32_t tminb) {
+    const float ocx = o.x - s.x, ocy = o.y - s.y, ocz = o.z - s.z;
+    const float hb = __builtin_fmaf(d.z, ocz, __builtin_fmaf(d.y, ocy, d.x * ocx));
+    const float c = __builtin_fmaf(ocx, ocx, __builtin_fmaf(ocy, ocy, __builtin_fmaf(ocz, ocz, -s.w)));
+    const float ac = a * c;
+    const float disc = __builtin_fmaf(hb, hb, -ac);
+    const float sq = __builtin_amdgcn_sqrtf(disc);   // NaN when disc < 0
+    const float nb = -hb * ia;
+    const float t0 = __builtin_fmaf(-sq, ia, nb), t1 = __builtin_fmaf(sq, ia, nb);
+    return min(__float_as_uint(t0) - tminb, __float_as_uint(t1) - tminb);
+}
+__device__ __forceinline__ float len2_f32(V3<float> d) {
+    return __builtin_fmaf(d.z, d.z, __builtin_fmaf(d.y, d.y, d.x * d.x));
+}
+// Branch-free body so that the compiler keeps a batch of sphere loads in flight.
 __device__ __forceinline__ void sweep_spheres(const R4<float>* __restrict__ sph, uint32_t n,
                                               int32_t base, V3<float> o, V3<float> d, float tmin,
                                               float& tb, int32_t& best) {
-    const float a = dot(d, d);
+    const float a = len2_f32(d);
     const float ia = __builtin_amdgcn_rcpf(a);
     const uint32_t tminb = __float_as_uint(tmin);
     uint32_t ub = __float_as_uint(tb) - tminb;
 #pragma unroll 8
     for (uint32_t k = 0; k < n; ++k) {
-        const R4<float> s = sph[k];
-        const float ocx = o.x - s.x, ocy = o.y - s.y, ocz = o.z - s.z;
-        const float hb = d.x * ocx + d.y * ocy + d.z * ocz;
-        const float c = ocx * ocx + (ocy * ocy + (ocz * ocz - s.w));
-        const float disc = hb * hb - a * c;
-        const float sq = __builtin_amdgcn_sqrtf(disc);   // NaN when disc < 0
-        const float nb = -hb * ia;
-        const float t0 = nb - sq * ia, t1 = nb + sq * ia;
-        const uint32_t u = min(__float_as_uint(t0) - tminb, __float_as_uint(t1) - tminb);
+        const uint32_t u = sphere_u(sph[k], o, d, a, ia, tminb);
         const bool h = u < ub;
         ub = h ? u : ub;
         best = h ? base + (int32_t)k : best;
@@ -197,14 +207,7 @@ struct SphereTester<float> {    // the f32 sweep's arithmetic (see sweep_spheres
     int32_t best;
     __device__ __forceinline__ float bound() const { return __uint_as_float(ub + tminb); }
     __device__ __forceinline__ void test(const R4<float>& s, int32_t id) {
-        const float ocx = o.x - s.x, ocy = o.y - s.y, ocz = o.z - s.z;
-        const float hb = d.x * ocx + d.y * ocy + d.z * ocz;
-        const float c = ocx * ocx + (ocy * ocy + (ocz * ocz - s.w));
-        const float disc = hb * hb - a * c;
-        const float sq = __builtin_amdgcn_sqrtf(disc);
-        const float nb = -hb * ia;
-        const float t0 = nb - sq * ia, t1 = nb + sq * ia;
-        const uint32_t u = min(__float_as_uint(t0) - tminb, __float_as_uint(t1) - tminb);
+        const uint32_t u = sphere_u(s, o, d, a, ia, tminb);
         if (u < ub || (u == ub && id < best)) {
             ub = u;
             best = id;
@@ -269,6 +272,33 @@ __device__ __forceinline__ void bvh_traverse(const DevScene<R>& sc, int32_t base
     }
 }
 
+// Test a parked leaf (<= kLeafMax = 4 spheres, contiguous in bsph/bid).  All
+// four slots are fetched at once (indices clamped to the leaf, so a short
+// leaf re-tests its last sphere -- a no-op: same t, same id, and ties only
+// move to a LOWER id) and tested without a data-dependent trip count.
+template <typename R>
+__device__ __forceinline__ void test_leaf(const DevScene<R>& sc, int32_t base, int32_t leaf,
+                                          SphereTester<R>& T, uint32_t& ntest) {
+    const uint32_t code = (uint32_t)~leaf;
+    const uint32_t first = code >> 4, cnt = code & 15u;
+    if (cnt == 0) return;
+    R4<R> s[4];
+    int32_t id[4];
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {
+        const uint32_t i = first + (k < cnt ? k : cnt - 1);
+        s[k] = sc.bsph[i];
+        id[k] = (int32_t)sc.bid[i];
+    }
+    if constexpr (sizeof(R) == 4) {
+        asm volatile("" : "+v"(s[0].x), "+v"(s[1].x), "+v"(s[2].x), "+v"(s[3].x), "+v"(id[0]), "+v"(id[1]),
+                     "+v"(id[2]), "+v"(id[3]));
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) T.test(s[k], base + id[k]);
+    ntest += cnt;
+}
+
 // "While-while" traversal with leaf postponing (Aila & Laine 2009): inner
 // nodes and leaves are processed in separate wave-uniform phases, so the
 // SIMD never runs the box-test and the sphere-test code under one divergent
@@ -323,40 +353,141 @@ __device__ __forceinline__ void bvh_traverse_ww(const DevScene<R>& sc, int32_t b
         }
         if (!__any(leaf != 0)) break;   // no parked leaves: every lane is done
         if (leaf != 0) {
-            const uint32_t code = (uint32_t)~leaf;
-            const uint32_t first = code >> 4, cnt = code & 15u;
-            for (uint32_t k = 0; k < cnt; ++k)
-                T.test(sc.bsph[first + k], base + (int32_t)sc.bid[first + k]);
-            ntest += cnt;
+            test_leaf(sc, base, leaf, T, ntest);
             leaf = 0;
         }
     }
 }
 
-template <bool kWW>
+__device__ __forceinline__ uint32_t sign_bit(float x) { return __float_as_uint(x) >> 31; }
+__device__ __forceinline__ int32_t link_of(float x) { return (int32_t)__float_as_uint(x); }
+__device__ __forceinline__ int32_t link_of(double x) { return (int32_t)__double_as_longlong(x); }
+__device__ __forceinline__ uint32_t sign_bit(double x) {
+    return (uint32_t)(__double_as_longlong(x) >> 63) & 1u;
+}
+
+// Fetch a whole 4-wide node.  For f32 the eight 16-B loads are issued back
+// to back and completed together (the empty asm takes every word as an
+// operand); left alone, the scheduler interleaves them with the slab tests
+// and waits for each child's second half separately -- four dependent memory
+// round trips per visit instead of one.
+__device__ __forceinline__ void load_node4(const Bvh4Node<float>& nd, R4<float> (&A)[4], R4<float> (&B)[4]) {
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    const f4* p = reinterpret_cast<const f4*>(&nd);
+    f4 v0 = p[0], v1 = p[1], v2 = p[2], v3 = p[3], v4 = p[4], v5 = p[5], v6 = p[6], v7 = p[7];
+    asm volatile("" : "+v"(v0), "+v"(v1), "+v"(v2), "+v"(v3), "+v"(v4), "+v"(v5), "+v"(v6), "+v"(v7));
+    const f4 v[8] = {v0, v1, v2, v3, v4, v5, v6, v7};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        A[c] = R4<float>{v[c].x, v[c].y, v[c].z, v[c].w};
+        B[c] = R4<float>{v[4 + c].x, v[4 + c].y, v[4 + c].z, v[4 + c].w};
+    }
+}
+__device__ __forceinline__ void load_node4(const Bvh4Node<double>& nd, R4<double> (&A)[4], R4<double> (&B)[4]) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        A[c] = nd.a[c];
+        B[c] = nd.b[c];
+    }
+}
+
+// 4-wide version of bvh_traverse_ww on the octant copies of the tree
+// (Bvh4Node): the ray's octant picks the copy, whose children are already in
+// front-to-back order and whose slab planes are already near/far for this
+// octant.  The first hit child is visited next; the other hit children are
+// pushed far-to-near (each store is unconditional, only the stack pointer
+// advance is predicated, so a visit has no divergent branch).  The stack
+// holds at most sc.bvh4_stack entries (host-computed bound) and is written
+// one past its top.
+template <typename R>
+__device__ __forceinline__ void bvh4_traverse(const DevScene<R>& sc, int32_t base, V3<R> o, V3<R> d,
+                                              SphereTester<R>& T, int32_t* __restrict__ stk,
+                                              uint32_t& nvis, uint32_t& ntest) {
+    constexpr int32_t kDone = 0x7fffffff;
+    const R ix = inv_(d.x), iy = inv_(d.y), iz = inv_(d.z);
+    const R oix = o.x * ix, oiy = o.y * iy, oiz = o.z * iz;
+    const uint32_t oct = sign_bit(ix) | (sign_bit(iy) << 1) | (sign_bit(iz) << 2);
+    const Bvh4Node<R>* __restrict__ nodes = sc.bvh4 + oct * sc.n_nodes4;
+    int32_t sp = 0;
+    int32_t node = 0;   // inner node index, leaf code (< 0) or kDone
+    int32_t leaf = 0;   // parked leaf code, 0 = none
+    for (;;) {
+        for (;;) {
+            if (node < 0 && leaf == 0) {   // park the leaf, continue with the stack
+                leaf = node;
+                node = sp ? stk[--sp * 64] : kDone;
+            }
+            const bool inner = node >= 0 && node != kDone;
+            if (!__any(inner) || __all(leaf != 0 || node == kDone)) break;
+            if (inner) {
+                ++nvis;
+                R4<R> NA[4], NB[4];
+                load_node4(nodes[node], NA, NB);
+                const R tb = T.bound();
+                bool h[4];
+                int32_t ch[4];
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const R4<R> A = NA[c], B = NB[c];
+                    const R xn = A.x * ix - oix, yn = A.y * iy - oiy, zn = A.z * iz - oiz;
+                    const R xf = A.w * ix - oix, yf = B.x * iy - oiy, zf = B.y * iz - oiz;
+                    const R tn = fmax(fmax(xn, yn), fmax(zn, (R)0));
+                    const R tf = fmin(fmin(xf, yf), fmin(zf, tb));
+                    h[c] = tn <= tf;
+                    ch[c] = link_of(B.z);
+                }
+                const int32_t c0 = ch[0], c1 = ch[1], c2 = ch[2], c3 = ch[3];
+                stk[sp * 64] = c3;
+                sp += (h[3] && (h[0] || h[1] || h[2])) ? 1 : 0;
+                stk[sp * 64] = c2;
+                sp += (h[2] && (h[0] || h[1])) ? 1 : 0;
+                stk[sp * 64] = c1;
+                sp += (h[1] && h[0]) ? 1 : 0;
+                if (h[0] | h[1] | h[2] | h[3])
+                    node = h[0] ? c0 : (h[1] ? c1 : (h[2] ? c2 : c3));
+                else
+                    node = sp ? stk[--sp * 64] : kDone;
+            }
+        }
+        if (!__any(leaf != 0)) break;   // no parked leaves: every lane is done
+        if (leaf != 0) {
+            test_leaf(sc, base, leaf, T, ntest);
+            leaf = 0;
+        }
+    }
+}
+
+template <int kKind, typename R>
+__device__ __forceinline__ void bvh_dispatch(const DevScene<R>& sc, int32_t base, V3<R> o, V3<R> d,
+                                             SphereTester<R>& T, int32_t* stk, uint32_t& nvis,
+                                             uint32_t& ntest) {
+    if constexpr (kKind == kWorldBvh4) bvh4_traverse(sc, base, o, d, T, stk, nvis, ntest);
+    else if constexpr (kKind == kWorldBvhWW) bvh_traverse_ww(sc, base, o, d, T, stk, nvis, ntest);
+    else bvh_traverse(sc, base, o, d, T, stk, nvis, ntest);
+}
+
+template <int kKind>
 __device__ __forceinline__ void bvh_closest(const DevScene<double>& sc, int32_t base, V3<double> o,
                                             V3<double> d, double tmin, double& tb, int32_t& best,
                                             int32_t* stk, uint32_t& nvis, uint32_t& ntest) {
     SphereTester<double> T{o, d, tmin, tb, best};
-    if constexpr (kWW) bvh_traverse_ww(sc, base, o, d, T, stk, nvis, ntest);
-    else bvh_traverse(sc, base, o, d, T, stk, nvis, ntest);
+    bvh_dispatch<kKind>(sc, base, o, d, T, stk, nvis, ntest);
     tb = T.tb;
     best = T.best;
 }
-template <bool kWW>
+template <int kKind>
 __device__ __forceinline__ void bvh_closest(const DevScene<float>& sc, int32_t base, V3<float> o,
                                             V3<float> d, float tmin, float& tb, int32_t& best,
                                             int32_t* stk, uint32_t& nvis, uint32_t& ntest) {
     SphereTester<float> T;
     T.o = o;
     T.d = d;
-    T.a = dot(d, d);
+    T.a = len2_f32(d);
     T.ia = __builtin_amdgcn_rcpf(T.a);
     T.tminb = __float_as_uint(tmin);
     T.ub = __float_as_uint(tb) - T.tminb;
     T.best = best;
-    if constexpr (kWW) bvh_traverse_ww(sc, base, o, d, T, stk, nvis, ntest);
-    else bvh_traverse(sc, base, o, d, T, stk, nvis, ntest);
+    bvh_dispatch<kKind>(sc, base, o, d, T, stk, nvis, ntest);
     tb = T.bound();
     best = T.best;
 }
@@ -488,10 +619,10 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? 5 : 1) render_kernel(
                     best = k;
                 }
             }
-            if constexpr (kWorld == kWorldBvh || kWorld == kWorldBvhWW) {
-                bvh_closest<kWorld == kWorldBvhWW>(p.sc, nplanes, o, d, tmin, tb, best,
-                            reinterpret_cast<int32_t*>(smem) + wave * kBvhStack * 64 + lane, nvis,
-                            ntest);
+            if constexpr (kWorld >= kWorldBvh) {
+                bvh_closest<kWorld>(p.sc, nplanes, o, d, tmin, tb, best,
+                                    reinterpret_cast<int32_t*>(smem) + wave * p.stack * 64 + lane, nvis,
+                                    ntest);
             } else {
                 sweep_spheres(sph, p.sc.n_sph, nplanes, o, d, tmin, tb, best);
             }
@@ -658,12 +789,15 @@ inline int launch_render_impl(const KParams<R>& p, int world, size_t lds_bytes, 
         if (world == kWorldLds) {
             hipLaunchKernelGGL((dev::render_kernel<R, kWorldLds>), dim3(blocks), dim3(kBlock),
                                lds_bytes, stream, p);
+        } else if (world == kWorldBvh4) {
+            hipLaunchKernelGGL((dev::render_kernel<R, kWorldBvh4>), dim3(blocks), dim3(kBlock),
+                               (size_t)kWavesPerBlock * p.stack * 64 * sizeof(int32_t), stream, p);
         } else if (world == kWorldBvhWW) {
             hipLaunchKernelGGL((dev::render_kernel<R, kWorldBvhWW>), dim3(blocks), dim3(kBlock),
-                               (size_t)kWavesPerBlock * kBvhStack * 64 * sizeof(int32_t), stream, p);
+                               (size_t)kWavesPerBlock * p.stack * 64 * sizeof(int32_t), stream, p);
         } else if (world == kWorldBvh) {
             hipLaunchKernelGGL((dev::render_kernel<R, kWorldBvh>), dim3(blocks), dim3(kBlock),
-                               (size_t)kWavesPerBlock * kBvhStack * 64 * sizeof(int32_t), stream, p);
+                               (size_t)kWavesPerBlock * p.stack * 64 * sizeof(int32_t), stream, p);
         } else {
             hipLaunchKernelGGL((dev::render_kernel<R, kWorldGlobal>), dim3(blocks), dim3(kBlock), 0,
                                stream, p);

@@ -14,7 +14,7 @@ constexpr uint32_t kWavesPerBlock = 4; // 256-thread workgroups, one tile item p
 constexpr uint32_t kBlock = 64 * kWavesPerBlock;
 
 // world query of the render kernel
-enum WorldMode : int { kWorldGlobal = 0, kWorldLds = 1, kWorldBvh = 2, kWorldBvhWW = 3 };
+enum WorldMode : int { kWorldGlobal = 0, kWorldLds = 1, kWorldBvh = 2, kWorldBvhWW = 3, kWorldBvh4 = 4 };
 
 // material kinds (same codes as RTW_LAMBERTIAN.. in include/rtw.h)
 enum : uint32_t { kMatLambertian = 0, kMatMetal = 1, kMatDielectric = 2, kMatInvisible = 3 };
@@ -36,6 +36,7 @@ struct alignas(4 * sizeof(R)) R4 {
 //   bvh      : n_nodes x BvhNode<R>            -- RTW_ACCEL_BVH
 //   bsph     : n_sph   x R4 {cx, cy, cz, r*r} in BVH leaf order
 //   bid      : n_sph   x u32 original sphere index of bsph[k]
+//   bvh4     : 8 x n_nodes4 x Bvh4Node<R>      -- RTW_ACCEL_BVH, 4-wide (default)
 template <typename R>
 struct BvhNode {
     // two child boxes per node (children tested together, the classic
@@ -45,6 +46,20 @@ struct BvhNode {
     R lo_x[2], lo_y[2], lo_z[2], hi_x[2], hi_y[2], hi_z[2];
     int32_t child[2];
     int32_t pad[2];
+};
+
+// 4-wide node, one copy of the tree per ray-direction octant (bit a of the
+// octant set: the ray goes -a).  In the copy for octant o the slab planes are
+// pre-selected -- near = the plane a ray of that octant enters through, far =
+// the one it leaves through -- and the children are stored in front-to-back
+// order for that octant, so a visit is 6 FMAs + 4 min/max per child and no
+// sort.  Child slot q is two R4s: a[q] = {near x, y, z, far x}, b[q] = {far y,
+// far z, child link (bits), 0}.  Empty slots map to near = +inf, far = -inf
+// in ray space (never hit) and an empty leaf.  Links index the same copy.
+template <typename R>
+struct alignas(sizeof(R) == 4 ? 128 : 256) Bvh4Node {
+    R4<R> a[4];
+    R4<R> b[4];
 };
 
 template <typename R>
@@ -60,7 +75,9 @@ struct DevScene {
     const BvhNode<R>* bvh;
     const R4<R>* bsph;
     const uint32_t* bid;
+    const Bvh4Node<R>* bvh4;          // 8 x n_nodes4 (octant copies)
     uint32_t n_sph, n_planes, n_mat, n_lights, n_nodes, bvh_depth;
+    uint32_t n_nodes4, bvh4_stack;
 };
 
 constexpr uint32_t kBvhStack = 32;    // per-lane traversal stack entries (LDS)
@@ -79,6 +96,7 @@ struct KParams {
     uint32_t group, n_groups;         // chunks per wave task, tasks per tile
     uint32_t tiles_x, n_local_tiles, rank, nranks;
     uint32_t n_tasks;                 // n_local_tiles * n_groups
+    uint32_t stack;                   // BVH traversal stack entries per lane (LDS)
 };
 
 // Host-side launch helpers (defined in render_f32.hip / render_f64.hip).

@@ -25,10 +25,12 @@ def _scene(n=11):
     return soa, builder
 
 
-def _render_gpu(soa, cam, seed, precision, chunk=0, accel=rtw.RTW_ACCEL_AUTO):
+def _render_gpu(soa, cam, seed, precision, chunk=0, accel=rtw.RTW_ACCEL_AUTO, bvh_kind=None):
     with rtw.Renderer(device=0, precision=precision) as r:
         if chunk:
             r.set_chunk(chunk)
+        if bvh_kind is not None:
+            r.set_tuning("bvh_kind", bvh_kind)
         r.set_accel(accel)
         r.set_scene(soa)
         img = r.render(cam, seed)
@@ -193,15 +195,53 @@ def _same(a, b):
 
 @pytest.mark.parametrize("prec", [rtw.RTW_F32, rtw.RTW_F64])
 @pytest.mark.parametrize("n", [11, 30])
-def test_bvh_equals_brute_force(prec, n):
+@pytest.mark.parametrize("kind", [2, 1, 0])
+def test_bvh_equals_brute_force(prec, n, kind):
     """RTW_ACCEL_BVH only culls: the closest hit, hence every pixel, must be
-    bit-identical to the brute-force sweep (same per-sphere arithmetic)."""
+    bit-identical to the brute-force sweep (same per-sphere arithmetic), for
+    every traversal (2: 4-wide octant tree, 1: binary while-while, 0: binary
+    single loop)."""
     soa, b = _scene(n)
     cam = b.with_image_width(64).with_image_height(40).with_samples_per_pixel(6).with_max_depth(50).build()
     brute, _, cb = _render_gpu(soa, cam, 13, prec, accel=rtw.RTW_ACCEL_BRUTE)
-    bvh, _, cv = _render_gpu(soa, cam, 13, prec, accel=rtw.RTW_ACCEL_BVH)
+    bvh, _, cv = _render_gpu(soa, cam, 13, prec, accel=rtw.RTW_ACCEL_BVH, bvh_kind=kind)
     assert _same(brute, bvh)
     assert cb == cv
+
+
+def test_bvh4_stats_and_width():
+    soa, b = _scene(11)
+    cam = b.with_image_width(48).with_image_height(32).with_samples_per_pixel(4).with_max_depth(50).build()
+    with rtw.Renderer(device=0, precision=rtw.RTW_F32) as r:
+        r.set_scene(soa)
+        r.set_tuning("bvh_kind", 2)
+        r.render(cam, 5)
+        st = r.stats
+        assert st.accel == rtw.RTW_ACCEL_BVH and st.bvh_width == 4
+        assert 0 < st.node_visits and 0 < st.sphere_tests
+        r.set_tuning("bvh_kind", 1)
+        r.render(cam, 5)
+        assert r.stats.bvh_width == 2 and r.stats.segments == st.segments
+
+
+def test_bvh_large_random_scene_equals_brute_force():
+    """20k small spheres: deep trees (4-wide stack bound > 13), many leaves
+    per ray; f32 BVH must still be bit-identical to brute force."""
+    world = rtw.HittableList()
+    rng = np.random.default_rng(11)
+    mats = [rtw.Lambertian((0.5, 0.5, 0.5)), rtw.Metal((0.8, 0.8, 0.8), 0.1), rtw.Dialectric(1.5)]
+    for k in range(20000):
+        c = (rng.uniform(-20, 20), rng.uniform(0, 3), rng.uniform(-20, 20))
+        world.add(rtw.Sphere(c, float(rng.uniform(0.02, 0.15)), mats[k % 3]))
+    world.add(rtw.Plane((0, 0, 0), (0, 1, 0), mats[0]))
+    lights = rtw.HittableList([rtw.Sphere((0, 8, 0), 2.0)])
+    soa = rtw.flatten(world, lights)
+    cam = rtw.CameraBuilder().with_image_width(40).with_image_height(24).with_samples_per_pixel(3) \
+        .with_max_depth(20).with_lookfrom((15, 6, 15)).with_lookat((0, 0, 0)).with_vfov(40) \
+        .with_background((0.7, 0.8, 1.0)).build()
+    brute, _, cb = _render_gpu(soa, cam, 23, rtw.RTW_F32, accel=rtw.RTW_ACCEL_BRUTE)
+    bvh, _, cv = _render_gpu(soa, cam, 23, rtw.RTW_F32, accel=rtw.RTW_ACCEL_BVH)
+    assert _same(brute, bvh) and cb == cv
 
 
 def test_bvh_f64_matches_oracle_custom_scene():
@@ -222,3 +262,33 @@ def test_bvh_f64_matches_oracle_custom_scene():
     ref, _ = _render_oracle(soa, cam, 17, chunk)
     mae, exact = _compare_f64(gpu, ref, 4)
     assert mae < F64_MAE_TOL and exact > 0.999
+
+
+def test_f64_matches_golden_fixtures():
+    """The committed golden renders (tests/golden/make_golden.py, oracle at
+    fixed seeds): the f64 kernel must reproduce them bit for bit -- the C1
+    window (BASELINE configs[0] geometry, 100 spp) and a full 48x27 frame."""
+    import json
+    import os
+    here = os.path.join(os.path.dirname(__file__), "golden")
+    with open(os.path.join(here, "simple_scene_5EED0001.json")) as f:
+        js = json.load(f)
+    soa = rtw.SceneSoA(**{k: np.asarray(js[k], dtype=np.uint32 if k.endswith("mat") or k == "mat_type"
+                                        else np.float64) for k in
+                          ("spheres", "sphere_mat", "planes", "plane_mat", "mat_type", "mat_params", "lights")})
+    gen, builder = rtw.scenes.simple_soa(js["seed"])
+    assert np.array_equal(np.asarray(gen.spheres).reshape(-1), np.asarray(soa.spheres).reshape(-1))
+    gold = np.load(os.path.join(here, "golden_renders.npz"))
+    cases = {"c1_window": (400, 225, 100, (104, 112), (184, 216)),
+             "simple_48x27": (48, 27, 16, None, None)}
+    for name, (w, h, spp, rows, cols) in cases.items():
+        chunk = int(gold[name + "_meta"][0])
+        cam = builder.copy().with_image_width(w).with_image_height(h).with_samples_per_pixel(spp) \
+            .with_max_depth(50).build()
+        img, used, _ = _render_gpu(soa, cam, 0xC0FFEE, rtw.RTW_F64, chunk=chunk)
+        assert used == chunk
+        if rows is not None:
+            img = img[rows[0]:rows[1], cols[0]:cols[1]]
+        ref = gold[name]
+        mae, exact = _compare_f64(img, ref, spp)
+        assert mae < F64_MAE_TOL and exact == 1.0, (name, mae, exact)

@@ -5,10 +5,10 @@ ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$ROOT"
 OUT="$ROOT/gpurun_out"; mkdir -p "$OUT"
 TAG="${1:-q}"
-fatal() { case "$1" in 0|1) return 1;; *) return 0;; esac; }
 timeout -k 10 600 python -m pytest tests -m gpu -q -rfE -x > "$OUT/pytest_gpu_$TAG.log" 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -4 "$OUT/pytest_gpu_$TAG.log"
-if fatal $rc; then exit $rc; fi
+# any failure ends the GPU session here (a failing kernel may have faulted)
+if [ $rc -ne 0 ]; then exit $rc; fi
 if [ -n "${SWEEP:-}" ]; then
   timeout -k 10 600 python tools/sweep.py $SWEEP > "$OUT/sweep_$TAG.log" 2>&1
   rc=$?; echo "sweep rc=$rc"; cat "$OUT/sweep_$TAG.log" | tail -30

@@ -12,7 +12,7 @@ bad() { case "$1" in 124|134|137|139) return 0;; *) return 1;; esac; }
 if [ ! -f "$OUT/rocprof_counters.txt" ]; then
   timeout -k 10 120 rocprofv3 -L > "$OUT/rocprof_counters.txt" 2>&1; echo "list rc=$?"
 fi
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$TAG" -o trace --output-format csv \
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$TAG" -o trace --output-format csv \
   -- python3 "$ROOT/bench.py" $ARGS > "$OUT/prof_${TAG}_trace.log" 2>&1
 rc=$?; echo "trace rc=$rc"; if bad $rc; then exit $rc; fi
 # counter sets separated by ';' (PMC_SETS overrides the default list)
@@ -21,7 +21,7 @@ i=0
 IFS=';' read -ra SETLIST <<< "$SETS"
 for set in "${SETLIST[@]}"; do
   i=$((i+1))
-  timeout -k 10 600 rocprofv3 --pmc $set -d "$OUT/prof_$TAG/pmc$i" -o pmc --output-format csv \
+  timeout -k 10 240 rocprofv3 --pmc $set -d "$OUT/prof_$TAG/pmc$i" -o pmc --output-format csv \
     -- python3 "$ROOT/bench.py" $ARGS > "$OUT/prof_${TAG}_pmc$i.log" 2>&1
   rc=$?; echo "pmc$i ($set) rc=$rc"; if bad $rc; then exit $rc; fi
 done
