@@ -128,8 +128,10 @@ int rtw_set_accel(rtw_ctx *ctx, int accel);
 /* scheduling knobs (benchmarking): "chunk" (samples per item, 0 = auto),
  * "auto_chunk", "group" (chunks per wave task, 0 = auto), "target_tasks",
  * "lds" (1 = stage the sphere list in LDS when it fits, 0 = read it from HBM),
- * "bvh_kind" (2 = 4-wide octant BVH, 1 = binary while-while, 0 = binary
- * single loop), "bvh_ww" (legacy: 1 -> bvh_kind 1, 0 -> 0), "auto_accel" */
+ * "bvh_kind" (3 = binary while-while on the tree staged in LDS, the
+ * default, 1 = binary while-while from L1/L2, 2 = 4-wide octant BVH, 0 =
+ * binary single loop), "bvh_lds_max" (LDS bytes per workgroup bvh_kind 3 may
+ * use), "bvh_ww" (legacy: 1 -> bvh_kind 1, 0 -> 0), "auto_accel" */
 int rtw_set_tuning(rtw_ctx *ctx, const char *key, int64_t value);
 
 /* ---- CameraBuilder::build (camera.rs:114-218) ------------------------- */

@@ -26,8 +26,11 @@ struct rtw_ctx {
     uint64_t target_tasks = 1u << 18;
     int world_pref = 1;           // 1: LDS-staged sphere list when it fits, 0: global
     int auto_accel = RTW_ACCEL_AUTO;    // RTW_ACCEL_AUTO resolves to this (AUTO: by scene size)
-    int bvh_kind = 1;             // BVH traversal: 1 = binary while-while with leaf postponing,
-                                  // 2 = 4-wide octant tree, 0 = binary single loop
+    int bvh_kind = 3;             // BVH traversal: 3 = binary while-while + leaf postponing on the
+                                  // tree staged in LDS (falls back to 1 when it does not fit),
+                                  // 1 = the same from L1/L2, 2 = 4-wide octant tree, 0 = binary
+                                  // single loop
+    size_t bvh_lds_max = 32 * 1024;   // LDS per workgroup allowed for bvh_kind 3
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     // ring of per-render event triples: [start, after render kernel, after reduce]
@@ -321,15 +324,26 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
     int world = (c->world_pref == 0 || lds > kLdsLimit) ? rtw::kWorldGlobal : rtw::kWorldLds;
     p.stack = rtw::kBvhStack;
     uint32_t bvh_width = 0;
+    size_t launch_lds = lds;
     if (accel == RTW_ACCEL_BVH) {
-        // 4-wide unless its stack bound does not fit (binary needs <= depth)
+        // binary traversal pushes at most one entry per inner level
+        const uint32_t bin_stack = p.sc.bvh_depth + 1;
+        const size_t stacks = (size_t)rtw::kWavesPerBlock * 64 * sizeof(int32_t);
+        const size_t tree_lds = stacks * bin_stack + (size_t)p.sc.n_nodes * sizeof(rtw::BvhNode<R>) +
+                                (size_t)p.sc.n_sph * (sizeof(rtw::R4<R>) + sizeof(uint32_t));
         if (c->bvh_kind == 2 && p.sc.bvh4_stack + 1 <= rtw::kBvhStack) {
-            world = rtw::kWorldBvh4;
+            world = rtw::kWorldBvh4;       // 4-wide, when its stack bound fits
             p.stack = p.sc.bvh4_stack + 1;
             bvh_width = 4;
-        } else if (p.sc.bvh_depth <= rtw::kBvhStack) {
-            world = c->bvh_kind ? rtw::kWorldBvhWW : rtw::kWorldBvh;
+        } else if (bin_stack <= rtw::kBvhStack) {
+            p.stack = bin_stack;
             bvh_width = 2;
+            if (c->bvh_kind == 3 && tree_lds <= c->bvh_lds_max) {
+                world = rtw::kWorldBvhLds;
+                launch_lds = tree_lds;
+            } else {
+                world = c->bvh_kind ? rtw::kWorldBvhWW : rtw::kWorldBvh;
+            }
         } else {
             return fail(c, RTW_E_UNSUPPORTED, "BVH deeper than the kernel's traversal stack");
         }
@@ -343,9 +357,9 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
         HIP_TRY(c, hipMemsetAsync(d_out, 0, need_out, stream));
         HIP_TRY(c, hipEventRecord(ev[1], stream));
     } else if constexpr (std::is_same<R, float>::value) {
-        lrc = rtw::launch_render_f32(p, world, lds, reinterpret_cast<float*>(d_out), stream, ev[1]);
+        lrc = rtw::launch_render_f32(p, world, launch_lds, reinterpret_cast<float*>(d_out), stream, ev[1]);
     } else {
-        lrc = rtw::launch_render_f64(p, world, lds, reinterpret_cast<double*>(d_out), stream, ev[1]);
+        lrc = rtw::launch_render_f64(p, world, launch_lds, reinterpret_cast<double*>(d_out), stream, ev[1]);
     }
     if (lrc) return fail(c, RTW_E_DEVICE, std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
     HIP_TRY(c, hipEventRecord(c->ev1, stream));
@@ -426,7 +440,8 @@ int rtw_set_tuning(rtw_ctx* c, const char* key, int64_t value) {
     else if (k == "target_tasks") c->target_tasks = std::max<uint64_t>(1, (uint64_t)value);
     else if (k == "lds") c->world_pref = value ? 1 : 0;
     else if (k == "bvh_ww") c->bvh_kind = value ? 1 : 0;
-    else if (k == "bvh_kind") c->bvh_kind = (int)std::min<int64_t>(value, 2);
+    else if (k == "bvh_kind") c->bvh_kind = (int)std::min<int64_t>(value, 3);
+    else if (k == "bvh_lds_max") c->bvh_lds_max = (size_t)std::min<int64_t>(value, kLdsLimit);
     else if (k == "auto_accel") c->auto_accel = (int)std::min<int64_t>(value, RTW_ACCEL_BVH);
     else return fail(c, RTW_E_INVALID, "unknown tuning key " + k);
     return RTW_OK;

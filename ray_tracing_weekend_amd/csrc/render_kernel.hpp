@@ -510,6 +510,29 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? 5 : 1) render_kernel(
     }
     const R4<R>* __restrict__ sph = kWorld == kWorldLds ? s_sph : p.sc.sph;
     const R4<R>* __restrict__ li = kWorld == kWorldLds ? s_li : p.sc.lights;
+    // World view of the closest-hit query.  kWorldBvhLds: the BVH nodes and
+    // the leaf-ordered spheres + ids are copied into LDS once per workgroup
+    // (after the traversal stacks), so traversal fetches go to the LDS
+    // instead of the vector-memory (TA/L1) path the shading loads use.
+    DevScene<R> scw = p.sc;
+    if constexpr (kWorld == kWorldBvhLds) {
+        unsigned char* base = smem + (size_t)kWavesPerBlock * p.stack * 64 * sizeof(int32_t);
+        BvhNode<R>* l_nodes = reinterpret_cast<BvhNode<R>*>(base);
+        R4<R>* l_bsph = reinterpret_cast<R4<R>*>(l_nodes + p.sc.n_nodes);
+        uint32_t* l_bid = reinterpret_cast<uint32_t*>(l_bsph + p.sc.n_sph);
+        const R4<R>* g_nodes = reinterpret_cast<const R4<R>*>(p.sc.bvh);
+        constexpr uint32_t kNodeR4 = sizeof(BvhNode<R>) / sizeof(R4<R>);
+        for (uint32_t k = threadIdx.x; k < p.sc.n_nodes * kNodeR4; k += kBlock)
+            reinterpret_cast<R4<R>*>(l_nodes)[k] = g_nodes[k];
+        for (uint32_t k = threadIdx.x; k < p.sc.n_sph; k += kBlock) {
+            l_bsph[k] = p.sc.bsph[k];
+            l_bid[k] = p.sc.bid[k];
+        }
+        __syncthreads();
+        scw.bvh = l_nodes;
+        scw.bsph = l_bsph;
+        scw.bid = l_bid;
+    }
 
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint32_t task = blockIdx.x * kWavesPerBlock + wave;
@@ -620,7 +643,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? 5 : 1) render_kernel(
                 }
             }
             if constexpr (kWorld >= kWorldBvh) {
-                bvh_closest<kWorld>(p.sc, nplanes, o, d, tmin, tb, best,
+                bvh_closest<kWorld == kWorldBvhLds ? kWorldBvhWW : kWorld>(scw, nplanes, o, d, tmin, tb, best,
                                     reinterpret_cast<int32_t*>(smem) + wave * p.stack * 64 + lane, nvis,
                                     ntest);
             } else {
@@ -789,6 +812,9 @@ inline int launch_render_impl(const KParams<R>& p, int world, size_t lds_bytes, 
         if (world == kWorldLds) {
             hipLaunchKernelGGL((dev::render_kernel<R, kWorldLds>), dim3(blocks), dim3(kBlock),
                                lds_bytes, stream, p);
+        } else if (world == kWorldBvhLds) {
+            hipLaunchKernelGGL((dev::render_kernel<R, kWorldBvhLds>), dim3(blocks), dim3(kBlock), lds_bytes,
+                               stream, p);
         } else if (world == kWorldBvh4) {
             hipLaunchKernelGGL((dev::render_kernel<R, kWorldBvh4>), dim3(blocks), dim3(kBlock),
                                (size_t)kWavesPerBlock * p.stack * 64 * sizeof(int32_t), stream, p);

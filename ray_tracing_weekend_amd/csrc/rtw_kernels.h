@@ -14,7 +14,14 @@ constexpr uint32_t kWavesPerBlock = 4; // 256-thread workgroups, one tile item p
 constexpr uint32_t kBlock = 64 * kWavesPerBlock;
 
 // world query of the render kernel
-enum WorldMode : int { kWorldGlobal = 0, kWorldLds = 1, kWorldBvh = 2, kWorldBvhWW = 3, kWorldBvh4 = 4 };
+enum WorldMode : int {
+    kWorldGlobal = 0,   // brute force, sphere list read from HBM/L2
+    kWorldLds = 1,      // brute force, sphere list staged in LDS
+    kWorldBvh = 2,      // binary BVH, single-loop traversal
+    kWorldBvhWW = 3,    // binary BVH, while-while + leaf postponing
+    kWorldBvh4 = 4,     // 4-wide octant BVH, while-while + leaf postponing
+    kWorldBvhLds = 5,   // kWorldBvhWW with nodes + leaf spheres staged in LDS
+};
 
 // material kinds (same codes as RTW_LAMBERTIAN.. in include/rtw.h)
 enum : uint32_t { kMatLambertian = 0, kMatMetal = 1, kMatDielectric = 2, kMatInvisible = 3 };

@@ -195,12 +195,12 @@ def _same(a, b):
 
 @pytest.mark.parametrize("prec", [rtw.RTW_F32, rtw.RTW_F64])
 @pytest.mark.parametrize("n", [11, 30])
-@pytest.mark.parametrize("kind", [2, 1, 0])
+@pytest.mark.parametrize("kind", [3, 2, 1, 0])
 def test_bvh_equals_brute_force(prec, n, kind):
     """RTW_ACCEL_BVH only culls: the closest hit, hence every pixel, must be
     bit-identical to the brute-force sweep (same per-sphere arithmetic), for
-    every traversal (2: 4-wide octant tree, 1: binary while-while, 0: binary
-    single loop)."""
+    every traversal (3: binary while-while on the tree staged in LDS, 2: 4-wide
+    octant tree, 1: binary while-while, 0: binary single loop)."""
     soa, b = _scene(n)
     cam = b.with_image_width(64).with_image_height(40).with_samples_per_pixel(6).with_max_depth(50).build()
     brute, _, cb = _render_gpu(soa, cam, 13, prec, accel=rtw.RTW_ACCEL_BRUTE)
