@@ -42,6 +42,8 @@ FLOP_PLANE = 6               # d.n (5) + compare
 FLOP_LAMBERT_BASE = 40       # mixture sample + ONB + cosine pdf, per Lambertian bounce
 FLOP_LIGHT = 17              # one light's Sphere::hit discriminant in HittablePdf::value
 ACCEL_NAMES = {1: "brute_lds", 2: "bvh"}
+KERNEL_NAMES = {0: "brute_l2", 1: "brute_lds", 2: "bvh2_loop", 3: "bvh2_ww", 4: "bvh4_octant",
+                5: "bvh2_ww_lds"}
 
 
 def parse():
@@ -198,7 +200,7 @@ def main():
                    "chunk": int(st.chunk)},
         "roofline": {"bound": "valu", "achieved": round(achieved, 3), "peak": peak,
                      "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": None,
-                     "kernel": f"render_kernel<{a.precision}, {accel}>",
+                     "kernel": f"render_kernel<{a.precision}, {KERNEL_NAMES.get(int(st.kernel), st.kernel)}>",
                      "kernel_ms_avg": round(avg_ms, 3),
                      "flops_per_launch": int(flops),
                      "segments_per_sample": round(st.segments / max(st.samples, 1), 4),

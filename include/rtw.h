@@ -111,7 +111,9 @@ typedef struct rtw_stats {
     uint64_t node_visits;         /* BVH inner nodes entered (RTW_ACCEL_BVH) */
     uint64_t sphere_tests;        /* ray-sphere discriminant evaluations */
     uint32_t bvh_width;           /* child boxes tested per node visit (4, 2; 0 = no BVH) */
-    uint32_t reserved;
+    uint32_t kernel;              /* render-kernel variant: 0 brute/L2, 1 brute/LDS, 2 BVH one
+                                     loop, 3 BVH while-while, 4 BVH 4-wide, 5 BVH while-while
+                                     with the tree in LDS */
 } rtw_stats;
 
 typedef struct rtw_ctx rtw_ctx;
@@ -128,6 +130,7 @@ int rtw_set_accel(rtw_ctx *ctx, int accel);
 /* scheduling knobs (benchmarking): "chunk" (samples per item, 0 = auto),
  * "auto_chunk", "group" (chunks per wave task, 0 = auto), "target_tasks",
  * "lds" (1 = stage the sphere list in LDS when it fits, 0 = read it from HBM),
+ * "partial_max" (bytes of chunk sums an auto chunk may use, default 8 GiB),
  * "bvh_kind" (3 = binary while-while on the tree staged in LDS, the
  * default, 1 = binary while-while from L1/L2, 2 = 4-wide octant BVH, 0 =
  * binary single loop), "bvh_lds_max" (LDS bytes per workgroup bvh_kind 3 may

@@ -12,6 +12,8 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_DIR = os.path.join(HERE, "lib")
 LIB_PATH = os.path.join(LIB_DIR, "librtw.so")
+# profiling only (tools/exp_cost.sh): an alternate build of the same library
+LIB_PATH = os.environ.get("RTW_LIB_OVERRIDE", LIB_PATH)
 
 RTW_OK = 0
 RTW_E_INVALID, RTW_E_DEVICE, RTW_E_NO_LIGHTS, RTW_E_NO_SCENE, RTW_E_UNSUPPORTED = -1, -2, -3, -4, -5
@@ -63,7 +65,7 @@ class rtw_stats(C.Structure):
         ("samples", C.c_uint64), ("segments", C.c_uint64), ("lambertian", C.c_uint64),
         ("kernel_ms", C.c_double), ("accel", C.c_uint32), ("chunk", C.c_uint32),
         ("node_visits", C.c_uint64), ("sphere_tests", C.c_uint64),
-        ("bvh_width", C.c_uint32), ("reserved", C.c_uint32),
+        ("bvh_width", C.c_uint32), ("kernel", C.c_uint32),
     ]
 
 

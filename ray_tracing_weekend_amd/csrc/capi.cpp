@@ -21,7 +21,9 @@ struct rtw_ctx {
     int precision = RTW_F32;
     int accel = RTW_ACCEL_AUTO;
     uint32_t chunk = 0;           // samples per item (0 = auto_chunk)
-    uint32_t auto_chunk = 2;
+    uint32_t auto_chunk = 1;      // one sample per item: the chunk fold is then the reference's
+                                  // sample-by-sample fold exactly
+    size_t partial_max = (size_t)8 << 30;   // cap of the chunk-sum buffer (auto chunk grows)
     uint32_t group = 0;           // chunks per wave task (0 = from target_tasks)
     uint64_t target_tasks = 1u << 18;
     int world_pref = 1;           // 1: LDS-staged sphere list when it fits, 0: global
@@ -300,6 +302,12 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
     // wavefront's dynamic item pool.  Small chunks balance the lanes of a
     // wave; enough tasks keep the dispatcher fed to the end of the launch.
     uint32_t chunk = c->chunk ? c->chunk : c->auto_chunk;
+    if (!c->chunk && p.spp) {
+        // keep the chunk sums within partial_max: bytes = ceil(spp/chunk) * tiles * 64 * 3 * sizeof(R)
+        const size_t per_chunk = (size_t)p.n_local_tiles * 64 * 3 * sizeof(R);
+        const size_t max_chunks = std::max<size_t>(1, c->partial_max / std::max<size_t>(per_chunk, 1));
+        while ((p.spp + chunk - 1) / chunk > max_chunks) ++chunk;
+    }
     chunk = std::max<uint32_t>(1, std::min<uint32_t>(chunk, std::max<uint32_t>(p.spp, 1)));
     p.chunk = chunk;
     p.n_chunks = p.spp ? (p.spp + chunk - 1) / chunk : 0;
@@ -329,8 +337,11 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
         // binary traversal pushes at most one entry per inner level
         const uint32_t bin_stack = p.sc.bvh_depth + 1;
         const size_t stacks = (size_t)rtw::kWavesPerBlock * 64 * sizeof(int32_t);
+        // kWorldBvhLds layout: stacks | nodes | leaf spheres | ids (padded to 8) | lights
         const size_t tree_lds = stacks * bin_stack + (size_t)p.sc.n_nodes * sizeof(rtw::BvhNode<R>) +
-                                (size_t)p.sc.n_sph * (sizeof(rtw::R4<R>) + sizeof(uint32_t));
+                                (size_t)p.sc.n_sph * sizeof(rtw::R4<R>) +
+                                (size_t)((p.sc.n_sph + 7u) & ~7u) * sizeof(uint32_t) +
+                                (size_t)p.sc.n_lights * sizeof(rtw::R4<R>);
         if (c->bvh_kind == 2 && p.sc.bvh4_stack + 1 <= rtw::kBvhStack) {
             world = rtw::kWorldBvh4;       // 4-wide, when its stack bound fits
             p.stack = p.sc.bvh4_stack + 1;
@@ -369,6 +380,7 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
     c->last.samples = (uint64_t)rtw_rows_for_rank(p.H, rank, nranks) * p.W * p.spp;
     c->last.accel = (uint32_t)accel;
     c->last.bvh_width = bvh_width;
+    c->last.kernel = (uint32_t)world;
     c->last_n_sph = p.sc.n_sph;
     c->last.chunk = chunk;
     return RTW_OK;
@@ -436,6 +448,7 @@ int rtw_set_tuning(rtw_ctx* c, const char* key, int64_t value) {
     if (value < 0) return fail(c, RTW_E_INVALID, "negative tuning value");
     if (k == "chunk") c->chunk = (uint32_t)value;
     else if (k == "auto_chunk") c->auto_chunk = std::max<uint32_t>(1, (uint32_t)value);
+    else if (k == "partial_max") c->partial_max = std::max<size_t>(1 << 20, (size_t)value);
     else if (k == "group") c->group = (uint32_t)value;
     else if (k == "target_tasks") c->target_tasks = std::max<uint64_t>(1, (uint64_t)value);
     else if (k == "lds") c->world_pref = value ? 1 : 0;

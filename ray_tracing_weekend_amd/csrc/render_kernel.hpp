@@ -208,10 +208,9 @@ struct SphereTester<float> {    // the f32 sweep's arithmetic (see sweep_spheres
     __device__ __forceinline__ float bound() const { return __uint_as_float(ub + tminb); }
     __device__ __forceinline__ void test(const R4<float>& s, int32_t id) {
         const uint32_t u = sphere_u(s, o, d, a, ia, tminb);
-        if (u < ub || (u == ub && id < best)) {
-            ub = u;
-            best = id;
-        }
+        const bool upd = u < ub || (u == ub && id < best);
+        ub = upd ? u : ub;
+        best = upd ? id : best;
     }
 };
 
@@ -492,6 +491,13 @@ __device__ __forceinline__ void bvh_closest(const DevScene<float>& sc, int32_t b
     best = T.best;
 }
 
+// RTW_EXP (profiling builds only, tools/exp_cost.sh): repeat one part of the
+// per-segment work so that the time difference prices it.  1 = closest-hit
+// query, 2 = light pdf sum, 3 = sample start (seeding + camera ray).
+#ifndef RTW_EXP
+#define RTW_EXP 0
+#endif
+
 template <typename R, int kWorld>
 // f32: ask for 5 waves per SIMD (<= 96 VGPRs; the kernel fits without
 // spilling); f64 keeps the compiler's choice.
@@ -510,6 +516,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? 5 : 1) render_kernel(
     }
     const R4<R>* __restrict__ sph = kWorld == kWorldLds ? s_sph : p.sc.sph;
     const R4<R>* __restrict__ li = kWorld == kWorldLds ? s_li : p.sc.lights;
+    R4<R>* l_li = nullptr;   // kWorldBvhLds: the light list in LDS
     // World view of the closest-hit query.  kWorldBvhLds: the BVH nodes and
     // the leaf-ordered spheres + ids are copied into LDS once per workgroup
     // (after the traversal stacks), so traversal fetches go to the LDS
@@ -520,19 +527,24 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? 5 : 1) render_kernel(
         BvhNode<R>* l_nodes = reinterpret_cast<BvhNode<R>*>(base);
         R4<R>* l_bsph = reinterpret_cast<R4<R>*>(l_nodes + p.sc.n_nodes);
         uint32_t* l_bid = reinterpret_cast<uint32_t*>(l_bsph + p.sc.n_sph);
-        const R4<R>* g_nodes = reinterpret_cast<const R4<R>*>(p.sc.bvh);
-        constexpr uint32_t kNodeR4 = sizeof(BvhNode<R>) / sizeof(R4<R>);
-        for (uint32_t k = threadIdx.x; k < p.sc.n_nodes * kNodeR4; k += kBlock)
-            reinterpret_cast<R4<R>*>(l_nodes)[k] = g_nodes[k];
+        static_assert(sizeof(BvhNode<R>) % 16 == 0, "nodes are copied in 16-B units");
+        const uint4* g_nodes = reinterpret_cast<const uint4*>(p.sc.bvh);
+        constexpr uint32_t kNode16 = sizeof(BvhNode<R>) / 16;
+        for (uint32_t k = threadIdx.x; k < p.sc.n_nodes * kNode16; k += kBlock)
+            reinterpret_cast<uint4*>(l_nodes)[k] = g_nodes[k];
         for (uint32_t k = threadIdx.x; k < p.sc.n_sph; k += kBlock) {
             l_bsph[k] = p.sc.bsph[k];
             l_bid[k] = p.sc.bid[k];
         }
+        // the light list follows, 32-B aligned (read by the light pdf / sampling)
+        l_li = reinterpret_cast<R4<R>*>(l_bid + ((p.sc.n_sph + 7u) & ~7u));
+        for (uint32_t k = threadIdx.x; k < p.sc.n_lights; k += kBlock) l_li[k] = p.sc.lights[k];
         __syncthreads();
         scw.bvh = l_nodes;
         scw.bsph = l_bsph;
         scw.bid = l_bid;
     }
+    if constexpr (kWorld == kWorldBvhLds) li = l_li;
 
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint32_t task = blockIdx.x * kWavesPerBlock + wave;
@@ -643,6 +655,16 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? 5 : 1) render_kernel(
                 }
             }
             if constexpr (kWorld >= kWorldBvh) {
+#if RTW_EXP == 1
+                {
+                    R tb2 = tb;
+                    int32_t best2 = best;
+                    bvh_closest<kWorld == kWorldBvhLds ? kWorldBvhWW : kWorld>(scw, nplanes, o, d, tmin, tb2, best2,
+                                        reinterpret_cast<int32_t*>(smem) + wave * p.stack * 64 + lane, nvis,
+                                        ntest);
+                    segs += best2 == -7 ? 1u : 0u;
+                }
+#endif
                 bvh_closest<kWorld == kWorldBvhLds ? kWorldBvhWW : kWorld>(scw, nplanes, o, d, tmin, tb, best,
                                     reinterpret_cast<int32_t*>(smem) + wave * p.stack * 64 + lane, nvis,
                                     ntest);
@@ -721,6 +743,9 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? 5 : 1) render_kernel(
                     const V3<R> ndir = PR::normalize(dir);
                     const R cos_w = PR::over_pi(dot(ndir, uvw.w));
                     const R acc = lights_pdf_sum(li, p.sc.n_lights, pnt, dir);   // hittable_list.rs:408-412
+#if RTW_EXP == 2
+                    segs += lights_pdf_sum(li, p.sc.n_lights, pnt, mk(dir.y, dir.z, dir.x)) == (R)-7 ? 1u : 0u;
+#endif
                     const R lpdf = PR::div_(acc, (R)p.sc.n_lights);
                     const R pdf = lpdf * (R)0.5 + PR::max_(cos_w, (R)0) * (R)0.5;
                     const R spdf = PR::max_(PR::over_pi(dot(nrm, ndir)), (R)0);
@@ -747,6 +772,13 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? 5 : 1) render_kernel(
                 part = part + col;
                 ++s;
                 if (s < s_end) {
+#if RTW_EXP == 3
+                    start_sample();
+                    segs += d.x == (R)-7 ? 1u : 0u;
+                    ++s;
+                    start_sample();
+                    --s;
+#endif
                     start_sample();
                 } else {
                     R* dst = p.partial + (((size_t)c * p.n_local_tiles + lt) * 64 + px) * 3;

@@ -25,15 +25,26 @@ def _scene(n=11):
     return soa, builder
 
 
+# render-kernel variants (rtw_stats.kernel)
+K_BVH_LOOP, K_BVH_WW, K_BVH4, K_BVH_LDS = 2, 3, 4, 5
+BVH_KIND_KERNEL = {0: K_BVH_LOOP, 1: K_BVH_WW, 2: K_BVH4, 3: K_BVH_LDS}
+LAST = {}
+
+
 def _render_gpu(soa, cam, seed, precision, chunk=0, accel=rtw.RTW_ACCEL_AUTO, bvh_kind=None):
     with rtw.Renderer(device=0, precision=precision) as r:
         if chunk:
             r.set_chunk(chunk)
         if bvh_kind is not None:
             r.set_tuning("bvh_kind", bvh_kind)
+            r.set_tuning("bvh_lds_max", 64 * 1024)    # the f64 tree needs > 32 KiB
         r.set_accel(accel)
         r.set_scene(soa)
         img = r.render(cam, seed)
+        LAST["kernel"] = r.stats.kernel
+        if bvh_kind is not None:
+            # bvh_kind 3 falls back to 1 when the tree does not fit in LDS
+            assert r.stats.kernel == BVH_KIND_KERNEL[bvh_kind] or (bvh_kind == 3 and r.stats.kernel == K_BVH_WW)
         return img, r.stats.chunk, (r.stats.segments, r.stats.lambertian)
 
 
@@ -205,6 +216,8 @@ def test_bvh_equals_brute_force(prec, n, kind):
     cam = b.with_image_width(64).with_image_height(40).with_samples_per_pixel(6).with_max_depth(50).build()
     brute, _, cb = _render_gpu(soa, cam, 13, prec, accel=rtw.RTW_ACCEL_BRUTE)
     bvh, _, cv = _render_gpu(soa, cam, 13, prec, accel=rtw.RTW_ACCEL_BVH, bvh_kind=kind)
+    if kind == 3 and n == 11:
+        assert LAST["kernel"] == K_BVH_LDS          # the C1/C2 scene's tree fits in LDS
     assert _same(brute, bvh)
     assert cb == cv
 
@@ -292,3 +305,19 @@ def test_f64_matches_golden_fixtures():
         ref = gold[name]
         mae, exact = _compare_f64(img, ref, spp)
         assert mae < F64_MAE_TOL and exact == 1.0, (name, mae, exact)
+
+
+def test_partial_buffer_cap_grows_the_chunk():
+    """With the chunk-sum buffer capped (tuning "partial_max"), the auto chunk
+    grows to fit and the render still matches the oracle at that chunk."""
+    soa, b = _scene()
+    cam = b.with_image_width(64).with_image_height(64).with_samples_per_pixel(100).with_max_depth(8).build()
+    with rtw.Renderer(device=0, precision=rtw.RTW_F64) as r:
+        r.set_tuning("partial_max", 1 << 20)     # 64 tiles x 64 px x 3 x 8 B = 96 KiB per chunk
+        r.set_scene(soa)
+        gpu = r.render(cam, 29)
+        chunk = r.stats.chunk
+    assert chunk == 10
+    ref, _ = _render_oracle(soa, cam, 29, chunk)
+    mae, exact = _compare_f64(gpu, ref, 100)
+    assert mae < F64_MAE_TOL and exact > 0.999
