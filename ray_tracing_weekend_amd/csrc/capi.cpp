@@ -33,6 +33,8 @@ struct rtw_ctx {
                                   // 1 = the same from L1/L2, 2 = 4-wide octant tree, 0 = binary
                                   // single loop
     size_t bvh_lds_max = 32 * 1024;   // LDS per workgroup allowed for bvh_kind 3
+    uint32_t light_bvh_min = 64;      // light lists at least this long use the light BVH
+                                      // (C2, 19 lights: the linear masked loop is faster)
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     // ring of per-render event triples: [start, after render kernel, after reduce]
@@ -104,6 +106,13 @@ std::vector<unsigned char> stage_scene(const rtw_scene* s, rtw::DevScene<R>* ds,
     const size_t o_bid = reserve(sizeof(uint32_t) * s->n_spheres);
     const rtw::Bvh4Build b4 = rtw::collapse_bvh4(bb);
     const size_t o_nodes4 = reserve(sizeof(rtw::Bvh4Node<R>) * 8 * b4.nodes.size());
+    // BVH over the light spheres for the light pdf (a query for EVERY light
+    // the ray hits, so boxes only cull; the sum itself keeps list order in f64)
+    const rtw::BvhBuild lb = rtw::build_bvh(s->lights, s->n_lights,
+                                            std::is_same<R, float>::value ? 1e-5 : 1e-12);
+    const size_t o_lnodes = reserve(sizeof(rtw::BvhNode<R>) * lb.nodes.size());
+    const size_t o_lsph = reserve(sizeof(R4) * s->n_lights);
+    const size_t o_lid = reserve(sizeof(uint32_t) * s->n_lights);
     std::vector<unsigned char> blob(align_up(off, 64) + 64, 0);
     unsigned char* b = blob.data();
     for (uint32_t k = 0; k < s->n_spheres; ++k) {
@@ -157,8 +166,7 @@ std::vector<unsigned char> stage_scene(const rtw_scene* s, rtw::DevScene<R>* ds,
         R r = (R)x;
         return (double)r < x ? std::nextafter(r, (R)INFINITY) : r;
     };
-    for (size_t k = 0; k < bb.nodes.size(); ++k) {
-        const rtw::BvhBuild::Node& n = bb.nodes[k];
+    auto pack_node = [&](const rtw::BvhBuild::Node& n) {
         rtw::BvhNode<R> d{};
         for (int c = 0; c < 2; ++c) {
             d.lo_x[c] = down(n.lo[c][0]);
@@ -169,8 +177,10 @@ std::vector<unsigned char> stage_scene(const rtw_scene* s, rtw::DevScene<R>* ds,
             d.hi_z[c] = up(n.hi[c][2]);
             d.child[c] = n.child[c];
         }
-        reinterpret_cast<rtw::BvhNode<R>*>(b + o_nodes)[k] = d;
-    }
+        return d;
+    };
+    for (size_t k = 0; k < bb.nodes.size(); ++k)
+        reinterpret_cast<rtw::BvhNode<R>*>(b + o_nodes)[k] = pack_node(bb.nodes[k]);
     for (uint32_t k = 0; k < s->n_spheres; ++k) {
         const uint32_t id = bb.order[k];
         reinterpret_cast<R4*>(b + o_bsph)[k] = reinterpret_cast<const R4*>(b + o_sph)[id];
@@ -210,6 +220,18 @@ std::vector<unsigned char> stage_scene(const rtw_scene* s, rtw::DevScene<R>* ds,
             reinterpret_cast<rtw::Bvh4Node<R>*>(b + o_nodes4)[oct * n4 + k] = d;
         }
     }
+    for (size_t k = 0; k < lb.nodes.size(); ++k)
+        reinterpret_cast<rtw::BvhNode<R>*>(b + o_lnodes)[k] = pack_node(lb.nodes[k]);
+    for (uint32_t k = 0; k < s->n_lights; ++k) {
+        const uint32_t id = lb.order[k];
+        reinterpret_cast<R4*>(b + o_lsph)[k] = reinterpret_cast<const R4*>(b + o_li)[id];
+        reinterpret_cast<uint32_t*>(b + o_lid)[k] = id;
+    }
+    ds->lbvh = reinterpret_cast<const rtw::BvhNode<R>*>(base + o_lnodes);
+    ds->lsph = reinterpret_cast<const R4*>(base + o_lsph);
+    ds->lid = reinterpret_cast<const uint32_t*>(base + o_lid);
+    ds->n_lnodes = (uint32_t)lb.nodes.size();
+    ds->lbvh_depth = lb.depth;
     ds->bvh4 = reinterpret_cast<const rtw::Bvh4Node<R>*>(base + o_nodes4);
     ds->n_nodes4 = (uint32_t)n4;
     ds->bvh4_stack = b4.max_stack;
@@ -333,9 +355,15 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
     p.stack = rtw::kBvhStack;
     uint32_t bvh_width = 0;
     size_t launch_lds = lds;
+    p.light_bvh = 0;
     if (accel == RTW_ACCEL_BVH) {
+        // the light pdf goes through the light BVH (same per-lane stack) for
+        // longer light lists
+        const uint32_t light_stack = p.sc.lbvh_depth + 1;
+        p.light_bvh = (p.sc.n_lights >= c->light_bvh_min && light_stack <= rtw::kBvhStack) ? 1u : 0u;
+        const uint32_t min_stack = p.light_bvh ? light_stack : 1u;
         // binary traversal pushes at most one entry per inner level
-        const uint32_t bin_stack = p.sc.bvh_depth + 1;
+        const uint32_t bin_stack = std::max(p.sc.bvh_depth + 1, min_stack);
         const size_t stacks = (size_t)rtw::kWavesPerBlock * 64 * sizeof(int32_t);
         // kWorldBvhLds layout: stacks | nodes | leaf spheres | ids (padded to 8) | lights
         const size_t tree_lds = stacks * bin_stack + (size_t)p.sc.n_nodes * sizeof(rtw::BvhNode<R>) +
@@ -344,7 +372,7 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
                                 (size_t)p.sc.n_lights * sizeof(rtw::R4<R>);
         if (c->bvh_kind == 2 && p.sc.bvh4_stack + 1 <= rtw::kBvhStack) {
             world = rtw::kWorldBvh4;       // 4-wide, when its stack bound fits
-            p.stack = p.sc.bvh4_stack + 1;
+            p.stack = std::max(p.sc.bvh4_stack + 1, min_stack);
             bvh_width = 4;
         } else if (bin_stack <= rtw::kBvhStack) {
             p.stack = bin_stack;
@@ -448,6 +476,7 @@ int rtw_set_tuning(rtw_ctx* c, const char* key, int64_t value) {
     if (value < 0) return fail(c, RTW_E_INVALID, "negative tuning value");
     if (k == "chunk") c->chunk = (uint32_t)value;
     else if (k == "auto_chunk") c->auto_chunk = std::max<uint32_t>(1, (uint32_t)value);
+    else if (k == "light_bvh_min") c->light_bvh_min = (uint32_t)std::min<int64_t>(value, 1u << 30);
     else if (k == "partial_max") c->partial_max = std::max<size_t>(1 << 20, (size_t)value);
     else if (k == "group") c->group = (uint32_t)value;
     else if (k == "target_tasks") c->target_tasks = std::max<uint64_t>(1, (uint64_t)value);
@@ -575,9 +604,9 @@ int rtw_set_scene(rtw_ctx* c, const rtw_scene* s) {
         };
         fix(ds.sph); fix(ds.sph_r); fix(ds.sph_mat); fix(ds.planes); fix(ds.plane_mat);
         fix(ds.mat_type); fix(ds.mat_p); fix(ds.lights); fix(ds.bvh); fix(ds.bsph); fix(ds.bid);
-        fix(ds.bvh4);
+        fix(ds.bvh4); fix(ds.lbvh); fix(ds.lsph); fix(ds.lid);
     };
-    static_assert(sizeof(rtw::DevScene<float>) == 12 * sizeof(void*) + 8 * sizeof(uint32_t),
+    static_assert(sizeof(rtw::DevScene<float>) == 15 * sizeof(void*) + 10 * sizeof(uint32_t),
                   "DevScene gained a member: update rebase");
     if (c->precision == RTW_F32) {
         rebase(tmp32);

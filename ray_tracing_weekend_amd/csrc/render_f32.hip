@@ -1,5 +1,6 @@
 // render_f32.hip -- speed-mode (f32) instantiation of the render kernels.
-// Built with -ffp-contract=fast (FMA) and native sqrt/rcp/rsq/sin/cos.
+// Built with -ffp-contract=on (FMA within a source expression) and native
+// sqrt/rcp/rsq/sin/cos.
 #include "render_kernel.hpp"
 
 namespace rtw {

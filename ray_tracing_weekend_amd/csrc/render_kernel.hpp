@@ -491,9 +491,115 @@ __device__ __forceinline__ void bvh_closest(const DevScene<float>& sc, int32_t b
     best = T.best;
 }
 
+// Light pdf through the light BVH (KParams::light_bvh): every light sphere the
+// ray (o, d) hits with t in [0, inf] contributes its solid-angle pdf
+// (HittableList::pdf_value, hittable_list.rs:408-412; sphere.rs:101-111).
+// Boxes only cull.  The traversal reuses the lane's LDS stack.
+//
+// Both children of a node are slab-tested against [0, inf); the visit order
+// does not matter for an all-hits query.
+template <typename R, typename Leaf>
+__device__ __forceinline__ void light_bvh_walk(const DevScene<R>& sc, V3<R> o, V3<R> d,
+                                               int32_t* __restrict__ stk, Leaf&& leaf) {
+    const R ix = inv_(d.x), iy = inv_(d.y), iz = inv_(d.z);
+    const R oix = o.x * ix, oiy = o.y * iy, oiz = o.z * iz;
+    int32_t sp = 0;
+    int32_t node = 0;
+    for (;;) {
+        if (node >= 0) {
+            const BvhNode<R>& nd = sc.lbvh[node];
+            bool h[2];
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                const R x0 = nd.lo_x[c] * ix - oix, x1 = nd.hi_x[c] * ix - oix;
+                const R y0 = nd.lo_y[c] * iy - oiy, y1 = nd.hi_y[c] * iy - oiy;
+                const R z0 = nd.lo_z[c] * iz - oiz, z1 = nd.hi_z[c] * iz - oiz;
+                const R tn = fmax(fmax(fmin(x0, x1), fmin(y0, y1)), fmax(fmin(z0, z1), (R)0));
+                const R tf = fmin(fmax(x0, x1), fmin(fmax(y0, y1), fmax(z0, z1)));
+                h[c] = tn <= tf;
+            }
+            const int32_t c0 = nd.child[0], c1 = nd.child[1];
+            if (h[0] && h[1]) {
+                stk[sp * 64] = c1;
+                ++sp;
+                node = c0;
+                continue;
+            }
+            if (h[0] | h[1]) {
+                node = h[0] ? c0 : c1;
+                continue;
+            }
+        } else {
+            const uint32_t code = (uint32_t)~node;
+            const uint32_t first = code >> 4, cnt = code & 15u;
+            for (uint32_t k = 0; k < cnt; ++k) leaf(first + k);
+        }
+        if (sp == 0) break;
+        --sp;
+        node = stk[sp * 64];
+    }
+}
+
+// f32: sqrt-free hit test as in lights_pdf_sum; pdfs summed in walk order.
+__device__ __forceinline__ float lights_pdf_bvh(const DevScene<float>& sc, V3<float> o, V3<float> d,
+                                                int32_t* __restrict__ stk) {
+    const float a = len2_f32(d);
+    float acc = 0.f;
+    light_bvh_walk(sc, o, d, stk, [&](uint32_t k) {
+        const R4<float> L = sc.lsph[k];
+        const float ocx = o.x - L.x, ocy = o.y - L.y, ocz = o.z - L.z;
+        const float hb = d.x * ocx + d.y * ocy + d.z * ocz;
+        const float c = ocx * ocx + (ocy * ocy + (ocz * ocz - L.w * L.w));
+        const float disc = hb * hb - a * c;
+        if ((disc > 0.f) & ((hb <= 0.f) | (c <= 0.f))) {
+            const float dist2 = ocx * ocx + ocy * ocy + ocz * ocz;
+            const float cos_max = __builtin_amdgcn_sqrtf(1.f - L.w * L.w * __builtin_amdgcn_rcpf(dist2));
+            acc += __builtin_amdgcn_rcpf(6.283185307179586f * (1.f - cos_max));
+        }
+    });
+    return acc;
+}
+// f64 (parity mode): collect the hit lights' list indices, then sum their
+// pdfs in LIST order with the reference arithmetic -- bit-identical to the
+// linear sum (misses add +0.0, which changes nothing).  More than 8 hits
+// falls back to the linear loop.
+__device__ __forceinline__ double lights_pdf_bvh(const DevScene<double>& sc, V3<double> o, V3<double> d,
+                                                 int32_t* __restrict__ stk) {
+    constexpr uint32_t kMax = 8;
+    uint32_t ids[kMax];
+    uint32_t n = 0;
+    bool overflow = false;
+    light_bvh_walk(sc, o, d, stk, [&](uint32_t k) {
+        const R4<double> L = sc.lsph[k];
+        double t;
+        if (sphere_t(mk(L.x, L.y, L.z), L.w * L.w, o, d, 0.0, t)) {
+            if (n < kMax) {
+                // insertion by list index
+                uint32_t id = sc.lid[k], q = n;
+                while (q > 0 && ids[q - 1] > id) {
+                    ids[q] = ids[q - 1];
+                    --q;
+                }
+                ids[q] = id;
+                ++n;
+            } else {
+                overflow = true;
+            }
+        }
+    });
+    if (overflow) return lights_pdf_sum(sc.lights, sc.n_lights, o, d);
+    double acc = 0.0;
+    for (uint32_t q = 0; q < n; ++q) {
+        const R4<double> L = sc.lights[ids[q]];
+        acc = acc + sphere_pdf_value(mk(L.x, L.y, L.z), L.w, o, d);
+    }
+    return acc;
+}
+
 // RTW_EXP (profiling builds only, tools/exp_cost.sh): repeat one part of the
 // per-segment work so that the time difference prices it.  1 = closest-hit
-// query, 2 = light pdf sum, 3 = sample start (seeding + camera ray).
+// query, 2 = light pdf sum, 3 = stream seeding, 4 = Lambertian direction
+// sampling, 5 = plane tests.
 #ifndef RTW_EXP
 #define RTW_EXP 0
 #endif
@@ -645,6 +751,15 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? 5 : 1) render_kernel(
             // ---- world.hit(&r, EPSILON..=INFINITY): closest over all primitives
             R tb = (R)INFINITY;
             int32_t best = -1;
+#if RTW_EXP == 5
+            for (int32_t k = 0; k < nplanes; ++k) {
+                R t;
+                const R* pl = p.sc.planes + 12 * k;
+                if (aabb_hit_ref(pl + 6, pl + 9, o, mk(d.y, d.x, d.z), tmin) &&
+                    plane_t(pl, o, mk(d.y, d.x, d.z), tmin, t) && t == (R)-7)
+                    ++segs;
+            }
+#endif
             for (int32_t k = 0; k < nplanes; ++k) {
                 R t;
                 const R* pl = p.sc.planes + 12 * k;
@@ -740,9 +855,31 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? 5 : 1) render_kernel(
                     } else {
                         dir = uvw.transform(cosine_hemisphere<R>(g));
                     }
+#if RTW_EXP == 4
+                    {
+                        Rng g2 = g;
+                        V3<R> dir2;
+                        if (PR::u_std(g2.next()) < (R)0.5) {
+                            const R4<R> L = li[g2.index(p.sc.n_lights)];
+                            dir2 = sphere_random(mk(L.x, L.y, L.z), L.w, pnt, g2);
+                        } else {
+                            dir2 = uvw.transform(cosine_hemisphere<R>(g2));
+                        }
+                        segs += dir2.x == (R)-7 ? 1u : 0u;
+                    }
+#endif
                     const V3<R> ndir = PR::normalize(dir);
                     const R cos_w = PR::over_pi(dot(ndir, uvw.w));
-                    const R acc = lights_pdf_sum(li, p.sc.n_lights, pnt, dir);   // hittable_list.rs:408-412
+                    R acc;                                                // hittable_list.rs:408-412
+                    if constexpr (kWorld >= kWorldBvh) {
+                        if (p.light_bvh)
+                            acc = lights_pdf_bvh(p.sc, pnt, dir,
+                                                 reinterpret_cast<int32_t*>(smem) + wave * p.stack * 64 + lane);
+                        else
+                            acc = lights_pdf_sum(li, p.sc.n_lights, pnt, dir);
+                    } else {
+                        acc = lights_pdf_sum(li, p.sc.n_lights, pnt, dir);
+                    }
 #if RTW_EXP == 2
                     segs += lights_pdf_sum(li, p.sc.n_lights, pnt, mk(dir.y, dir.z, dir.x)) == (R)-7 ? 1u : 0u;
 #endif
@@ -773,11 +910,11 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? 5 : 1) render_kernel(
                 ++s;
                 if (s < s_end) {
 #if RTW_EXP == 3
-                    start_sample();
-                    segs += d.x == (R)-7 ? 1u : 0u;
-                    ++s;
-                    start_sample();
-                    --s;
+                    {
+                        Rng g2;
+                        g2.seed(p.seed ^ 0x55u, pix, s);
+                        segs += (g2.next() & 0xfffu) == 7u ? 1u : 0u;
+                    }
 #endif
                     start_sample();
                 } else {

@@ -43,7 +43,9 @@ struct alignas(4 * sizeof(R)) R4 {
 //   bvh      : n_nodes x BvhNode<R>            -- RTW_ACCEL_BVH
 //   bsph     : n_sph   x R4 {cx, cy, cz, r*r} in BVH leaf order
 //   bid      : n_sph   x u32 original sphere index of bsph[k]
-//   bvh4     : 8 x n_nodes4 x Bvh4Node<R>      -- RTW_ACCEL_BVH, 4-wide (default)
+//   bvh4     : 8 x n_nodes4 x Bvh4Node<R>      -- RTW_ACCEL_BVH, 4-wide
+//   lbvh     : n_lnodes x BvhNode<R>           -- light pdf query (BVH kernels)
+//   lsph/lid : n_li x R4 {c, r} / u32 in light-BVH leaf order
 template <typename R>
 struct BvhNode {
     // two child boxes per node (children tested together, the classic
@@ -83,8 +85,11 @@ struct DevScene {
     const R4<R>* bsph;
     const uint32_t* bid;
     const Bvh4Node<R>* bvh4;          // 8 x n_nodes4 (octant copies)
+    const BvhNode<R>* lbvh;           // binary BVH over the light spheres
+    const R4<R>* lsph;                // lights {cx, cy, cz, r} in light-BVH leaf order
+    const uint32_t* lid;              // light-list index of lsph[k]
     uint32_t n_sph, n_planes, n_mat, n_lights, n_nodes, bvh_depth;
-    uint32_t n_nodes4, bvh4_stack;
+    uint32_t n_nodes4, bvh4_stack, n_lnodes, lbvh_depth;
 };
 
 constexpr uint32_t kBvhStack = 32;    // per-lane traversal stack entries (LDS)
@@ -104,6 +109,7 @@ struct KParams {
     uint32_t tiles_x, n_local_tiles, rank, nranks;
     uint32_t n_tasks;                 // n_local_tiles * n_groups
     uint32_t stack;                   // BVH traversal stack entries per lane (LDS)
+    uint32_t light_bvh;               // 1: light pdf through sc.lbvh (BVH kernels only)
 };
 
 // Host-side launch helpers (defined in render_f32.hip / render_f64.hip).

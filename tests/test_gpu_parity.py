@@ -31,10 +31,12 @@ BVH_KIND_KERNEL = {0: K_BVH_LOOP, 1: K_BVH_WW, 2: K_BVH4, 3: K_BVH_LDS}
 LAST = {}
 
 
-def _render_gpu(soa, cam, seed, precision, chunk=0, accel=rtw.RTW_ACCEL_AUTO, bvh_kind=None):
+def _render_gpu(soa, cam, seed, precision, chunk=0, accel=rtw.RTW_ACCEL_AUTO, bvh_kind=None, tuning=None):
     with rtw.Renderer(device=0, precision=precision) as r:
         if chunk:
             r.set_chunk(chunk)
+        for k, v in (tuning or {}).items():
+            r.set_tuning(k, v)
         if bvh_kind is not None:
             r.set_tuning("bvh_kind", bvh_kind)
             r.set_tuning("bvh_lds_max", 64 * 1024)    # the f64 tree needs > 32 KiB
@@ -214,8 +216,12 @@ def test_bvh_equals_brute_force(prec, n, kind):
     octant tree, 1: binary while-while, 0: binary single loop)."""
     soa, b = _scene(n)
     cam = b.with_image_width(64).with_image_height(40).with_samples_per_pixel(6).with_max_depth(50).build()
+    # the brute-force kernels sum the light pdf linearly; in f32 the light
+    # BVH's walk-order sum rounds differently, so it is off here (it has its
+    # own test below)
     brute, _, cb = _render_gpu(soa, cam, 13, prec, accel=rtw.RTW_ACCEL_BRUTE)
-    bvh, _, cv = _render_gpu(soa, cam, 13, prec, accel=rtw.RTW_ACCEL_BVH, bvh_kind=kind)
+    bvh, _, cv = _render_gpu(soa, cam, 13, prec, accel=rtw.RTW_ACCEL_BVH, bvh_kind=kind,
+                             tuning={"light_bvh_min": 1 << 30})
     if kind == 3 and n == 11:
         assert LAST["kernel"] == K_BVH_LDS          # the C1/C2 scene's tree fits in LDS
     assert _same(brute, bvh)
@@ -253,7 +259,8 @@ def test_bvh_large_random_scene_equals_brute_force():
         .with_max_depth(20).with_lookfrom((15, 6, 15)).with_lookat((0, 0, 0)).with_vfov(40) \
         .with_background((0.7, 0.8, 1.0)).build()
     brute, _, cb = _render_gpu(soa, cam, 23, rtw.RTW_F32, accel=rtw.RTW_ACCEL_BRUTE)
-    bvh, _, cv = _render_gpu(soa, cam, 23, rtw.RTW_F32, accel=rtw.RTW_ACCEL_BVH)
+    bvh, _, cv = _render_gpu(soa, cam, 23, rtw.RTW_F32, accel=rtw.RTW_ACCEL_BVH,
+                             tuning={"light_bvh_min": 1 << 30})
     assert _same(brute, bvh) and cb == cv
 
 
@@ -321,3 +328,42 @@ def test_partial_buffer_cap_grows_the_chunk():
     ref, _ = _render_oracle(soa, cam, 29, chunk)
     mae, exact = _compare_f64(gpu, ref, 100)
     assert mae < F64_MAE_TOL and exact > 0.999
+
+
+@pytest.mark.parametrize("prec", [rtw.RTW_F64, rtw.RTW_F32])
+def test_light_bvh_equals_linear_light_sum(prec):
+    """The light pdf through the light BVH (tuning light_bvh_min) against the
+    linear loop over the light list (hittable_list.rs:408-412): f64 sums the
+    hit lights in list order, so the images are bit-identical; f32 sums in
+    walk order, so only the path statistics are compared."""
+    world = rtw.HittableList()
+    rng = np.random.default_rng(5)
+    lights = rtw.HittableList()
+    for k in range(300):
+        c = (float(rng.uniform(-6, 6)), float(rng.uniform(0.1, 0.4)), float(rng.uniform(-6, 6)))
+        r = float(rng.uniform(0.1, 0.3))
+        if k % 3 == 0:
+            world.add(rtw.Sphere(c, r, rtw.Dialectric(1.5)))
+            lights.add(rtw.Sphere(c, r))
+        else:
+            world.add(rtw.Sphere(c, r, rtw.Lambertian(tuple(rng.uniform(0.2, 0.9, 3)))))
+    world.add(rtw.Plane((0, 0, 0), (0, 1, 0), rtw.Lambertian((0.5, 0.5, 0.5))))
+    soa = rtw.flatten(world, lights)
+    cam = rtw.CameraBuilder().with_image_width(40).with_image_height(24).with_samples_per_pixel(4) \
+        .with_max_depth(12).with_lookfrom((8, 3, 8)).with_lookat((0, 0, 0)).with_vfov(45) \
+        .with_background((0.7, 0.8, 1.0)).build()
+    out = {}
+    for mode, m in (("bvh", 1), ("linear", 1 << 30)):
+        with rtw.Renderer(device=0, precision=prec) as r:
+            r.set_tuning("light_bvh_min", m)
+            r.set_scene(soa)
+            out[mode] = (r.render(cam, 31), r.stats.segments, r.stats.lambertian)
+    if prec == rtw.RTW_F64:
+        assert _same(out["bvh"][0], out["linear"][0]) and out["bvh"][1:] == out["linear"][1:]
+        ref, st = _render_oracle(soa, cam, 31, 1)
+        mae, exact = _compare_f64(out["bvh"][0], ref, 4)
+        assert mae < F64_MAE_TOL and exact > 0.999
+    else:
+        a, b = out["bvh"][0], out["linear"][0]
+        ok = ~(np.isnan(a).any(-1) | np.isnan(b).any(-1))
+        assert abs(a[ok].mean() - b[ok].mean()) < 0.02 * b[ok].mean()
