@@ -130,6 +130,8 @@ int rtw_set_accel(rtw_ctx *ctx, int accel);
 /* scheduling knobs (benchmarking): "chunk" (samples per item, 0 = auto),
  * "auto_chunk", "group" (chunks per wave task, 0 = auto), "target_tasks",
  * "lds" (1 = stage the sphere list in LDS when it fits, 0 = read it from HBM),
+ * "robust" (f32 ray-sphere tests in closest-approach form: 1 on, 0 off,
+ * 2 = by the scene's distance-to-radius ratio, the default),
  * "light_bvh_min" (light lists this long or longer take the light BVH in
  * the BVH kernels, default 64), "partial_max" (bytes of chunk sums an auto chunk may use, default 8 GiB),
  * "bvh_kind" (3 = binary while-while on the tree staged in LDS, the

@@ -2,6 +2,7 @@
 // build, the render entry points, scenes::simple and the PPM encoding.
 #include <hip/hip_runtime.h>
 #include <math.h>
+#include <stddef.h>
 #include <stdio.h>
 #include <string.h>
 
@@ -33,6 +34,8 @@ struct rtw_ctx {
                                   // 1 = the same from L1/L2, 2 = 4-wide octant tree, 0 = binary
                                   // single loop
     size_t bvh_lds_max = 32 * 1024;   // LDS per workgroup allowed for bvh_kind 3
+    int robust = 2;                   // f32 closest-approach tests: 1 on, 0 off, 2 by scene scale
+    double scene_extent = 0.0, min_radius = 0.0;   // of the staged scene (robust = 2)
     uint32_t light_bvh_min = 64;      // light lists at least this long use the light BVH
                                       // (C2, 19 lights: the linear masked loop is faster)
     hipStream_t stream = nullptr;
@@ -355,6 +358,17 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
     p.stack = rtw::kBvhStack;
     uint32_t bvh_width = 0;
     size_t launch_lds = lds;
+    // f32 sphere/light tests: the reference's hb^2 - a c loses r^2 to
+    // rounding once (distance / radius)^2 * 2^-24 is no longer small (C3/C5
+    // seen from afar); the closest-approach form is then used.
+    {
+        const double far = std::max(c->scene_extent, sqrt((double)p.center[0] * p.center[0] +
+                                                          (double)p.center[1] * p.center[1] +
+                                                          (double)p.center[2] * p.center[2]));
+        const double rel = std::isfinite(c->min_radius) ? (far / c->min_radius) * (far / c->min_radius) * 5.96e-8
+                                                        : 0.0;
+        p.sc.robust = c->robust == 2 ? (rel > 1e-3 ? 1u : 0u) : (uint32_t)c->robust;
+    }
     p.light_bvh = 0;
     if (accel == RTW_ACCEL_BVH) {
         // the light pdf goes through the light BVH (same per-lane stack) for
@@ -476,6 +490,7 @@ int rtw_set_tuning(rtw_ctx* c, const char* key, int64_t value) {
     if (value < 0) return fail(c, RTW_E_INVALID, "negative tuning value");
     if (k == "chunk") c->chunk = (uint32_t)value;
     else if (k == "auto_chunk") c->auto_chunk = std::max<uint32_t>(1, (uint32_t)value);
+    else if (k == "robust") c->robust = (int)std::min<int64_t>(value, 2);
     else if (k == "light_bvh_min") c->light_bvh_min = (uint32_t)std::min<int64_t>(value, 1u << 30);
     else if (k == "partial_max") c->partial_max = std::max<size_t>(1 << 20, (size_t)value);
     else if (k == "group") c->group = (uint32_t)value;
@@ -596,6 +611,19 @@ int rtw_set_scene(rtw_ctx* c, const rtw_scene* s) {
         HIP_TRY(c, hipMalloc(&c->d_scene, blob.size()));
         c->scene_bytes = blob.size();
     }
+    // scale of the scene for the f32 test choice (render_device_t)
+    c->scene_extent = 0.0;
+    c->min_radius = INFINITY;
+    for (uint32_t k = 0; k < s->n_spheres; ++k) {
+        const double* q = s->spheres + 4 * k;
+        const double r = fabs(q[3]);
+        c->scene_extent = std::max(c->scene_extent, std::max(fabs(q[0]), std::max(fabs(q[1]), fabs(q[2]))) + r);
+        if (r > 0) c->min_radius = std::min(c->min_radius, r);
+    }
+    for (uint32_t k = 0; k < s->n_lights; ++k) {
+        const double r = fabs(s->lights[4 * k + 3]);
+        if (r > 0) c->min_radius = std::min(c->min_radius, r);
+    }
     const uintptr_t base = reinterpret_cast<uintptr_t>(c->d_scene);
     auto rebase = [base](auto& ds) {
         auto fix = [base](auto*& ptr) {
@@ -606,8 +634,8 @@ int rtw_set_scene(rtw_ctx* c, const rtw_scene* s) {
         fix(ds.mat_type); fix(ds.mat_p); fix(ds.lights); fix(ds.bvh); fix(ds.bsph); fix(ds.bid);
         fix(ds.bvh4); fix(ds.lbvh); fix(ds.lsph); fix(ds.lid);
     };
-    static_assert(sizeof(rtw::DevScene<float>) == 15 * sizeof(void*) + 10 * sizeof(uint32_t),
-                  "DevScene gained a member: update rebase");
+    static_assert(offsetof(rtw::DevScene<float>, n_sph) == 15 * sizeof(void*),
+                  "DevScene gained a pointer: update rebase");
     if (c->precision == RTW_F32) {
         rebase(tmp32);
         c->sc32 = tmp32;

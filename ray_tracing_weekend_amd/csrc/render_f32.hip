@@ -7,15 +7,6 @@ namespace rtw {
 
 int launch_render_f32(const KParams<float>& p, int world, size_t lds_bytes, float* out,
                       hipStream_t stream, hipEvent_t mid) {
-    // dynamic LDS above 64 KiB must be allowed per kernel
-    if (world == kWorldLds && lds_bytes > 65536)
-        (void)hipFuncSetAttribute(
-            reinterpret_cast<const void*>(&dev::render_kernel<float, kWorldLds>),
-            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
-    if (world == kWorldBvhLds && lds_bytes > 65536)
-        (void)hipFuncSetAttribute(
-            reinterpret_cast<const void*>(&dev::render_kernel<float, kWorldBvhLds>),
-            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
     return launch_render_impl<float>(p, world, lds_bytes, out, stream, mid);
 }
 

@@ -7,15 +7,6 @@ namespace rtw {
 
 int launch_render_f64(const KParams<double>& p, int world, size_t lds_bytes, double* out,
                       hipStream_t stream, hipEvent_t mid) {
-    // dynamic LDS above 64 KiB must be allowed per kernel
-    if (world == kWorldLds && lds_bytes > 65536)
-        (void)hipFuncSetAttribute(
-            reinterpret_cast<const void*>(&dev::render_kernel<double, kWorldLds>),
-            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
-    if (world == kWorldBvhLds && lds_bytes > 65536)
-        (void)hipFuncSetAttribute(
-            reinterpret_cast<const void*>(&dev::render_kernel<double, kWorldBvhLds>),
-            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
     return launch_render_impl<double>(p, world, lds_bytes, out, stream, mid);
 }
 

@@ -22,6 +22,8 @@
 // chunk >= spp the f64 result is the reference's fold order bit for bit.
 #pragma once
 
+#include <type_traits>
+
 #include "rtw_device.hpp"
 #include "rtw_kernels.h"
 
@@ -72,6 +74,7 @@ __device__ __forceinline__ bool aabb_hit_ref(const R* lo, const R* hi, V3<R> o, 
 // far root (sphere.rs:71-80); the smallest t wins, the lowest id on ties.
 //
 // f64 (parity mode): the reference's exact arithmetic, divisions included.
+template <bool kRobust>
 __device__ __forceinline__ void sweep_spheres(const R4<double>* __restrict__ sph, uint32_t n,
                                               int32_t base, V3<double> o, V3<double> d, double tmin,
                                               double& tb, int32_t& best) {
@@ -87,31 +90,52 @@ __device__ __forceinline__ void sweep_spheres(const R4<double>* __restrict__ sph
 }
 // f32 (speed mode): the per-sphere test, shared by the brute-force sweep and
 // the BVH leaves so both give bit-identical t; every FMA is spelled out so
-// that contraction cannot differ between the two call sites.  Both roots come
-// from one reciprocal of a = d.d.  The range test "t in [tmin, tb)" is ONE
-// unsigned compare on u = bits(t) - bits(tmin): for t >= 0 float bits are
-// monotonic, while every t < tmin (negative, or in [0, tmin)) and NaN maps
-// above bits(+inf) - bits(tmin) >= any live bound.  Since t0 <= t1,
+// that contraction cannot differ between the two call sites.
+//
+// Closest-approach form (Haines et al., "Precision Improvements for Ray/Sphere
+// Intersection", Ray Tracing Gems ch. 7): with f = o - c, the ray's closest
+// point to the centre is at tc = -(f.d)/a and l = f + tc d is the offset from
+// the centre to it; the discriminant is a (r^2 - l.l).  The reference's
+// hb^2 - a c cancels catastrophically in f32 once |f| >> r (C5's 1M-sphere
+// field seen from ~700 units: the error exceeds r^2 itself); l.l does not.
+// Roots t = tc -/+ sqrt((r^2 - l.l) / a).  Scenes whose extent is small next
+// to their radii (C2) keep the cheaper reference form (DevScene::robust = 0,
+// chosen per launch by the host).  The range test "t in [tmin, tb)"
+// is ONE unsigned compare on u = bits(t) - bits(tmin): for t >= 0 float bits
+// are monotonic, while every t < tmin (negative, or in [0, tmin)) and NaN
+// maps above bits(+inf) - bits(tmin) >= any live bound.  Since t0 <= t1,
 // min_u32(u0, u1) is the near root when it is >= tmin, else the far root
-// (sphere.rs:71-80).  A negative discriminant gives sqrt = NaN and so no hit;
-// disc == 0 exactly (a tangent ray) counts as a hit here, where the
-// reference needs disc > 0.
+// (sphere.rs:71-80).  A miss gives sqrt(negative) = NaN and so no hit.
+template <bool kRobust>
 __device__ __forceinline__ uint32_t sphere_u(const R4<float>& s, V3<float> o, V3<float> d, float a,
                                              float ia, uint32_t tminb) {
-    const float ocx = o.x - s.x, ocy = o.y - s.y, ocz = o.z - s.z;
-    const float hb = __builtin_fmaf(d.z, ocz, __builtin_fmaf(d.y, ocy, d.x * ocx));
-    const float c = __builtin_fmaf(ocx, ocx, __builtin_fmaf(ocy, ocy, __builtin_fmaf(ocz, ocz, -s.w)));
-    const float ac = a * c;
-    const float disc = __builtin_fmaf(hb, hb, -ac);
-    const float sq = __builtin_amdgcn_sqrtf(disc);   // NaN when disc < 0
-    const float nb = -hb * ia;
-    const float t0 = __builtin_fmaf(-sq, ia, nb), t1 = __builtin_fmaf(sq, ia, nb);
+    const float fx = o.x - s.x, fy = o.y - s.y, fz = o.z - s.z;
+    const float hb = __builtin_fmaf(d.z, fz, __builtin_fmaf(d.y, fy, d.x * fx));
+    float t0, t1;
+    if constexpr (kRobust) {
+        const float tc = -hb * ia;
+        const float lx = __builtin_fmaf(tc, d.x, fx), ly = __builtin_fmaf(tc, d.y, fy),
+                    lz = __builtin_fmaf(tc, d.z, fz);
+        const float l2 = __builtin_fmaf(lx, lx, __builtin_fmaf(ly, ly, lz * lz));
+        const float h = __builtin_amdgcn_sqrtf((s.w - l2) * ia);   // NaN on a miss
+        t0 = tc - h;
+        t1 = tc + h;
+    } else {
+        // the reference's form: c = f.f - r^2, disc = hb^2 - a c
+        const float c = __builtin_fmaf(fx, fx, __builtin_fmaf(fy, fy, __builtin_fmaf(fz, fz, -s.w)));
+        const float disc = __builtin_fmaf(hb, hb, -(a * c));
+        const float sq = __builtin_amdgcn_sqrtf(disc);             // NaN on a miss
+        const float nb = -hb * ia;
+        t0 = __builtin_fmaf(-sq, ia, nb);
+        t1 = __builtin_fmaf(sq, ia, nb);
+    }
     return min(__float_as_uint(t0) - tminb, __float_as_uint(t1) - tminb);
 }
 __device__ __forceinline__ float len2_f32(V3<float> d) {
     return __builtin_fmaf(d.z, d.z, __builtin_fmaf(d.y, d.y, d.x * d.x));
 }
 // Branch-free body so that the compiler keeps a batch of sphere loads in flight.
+template <bool kRobust>
 __device__ __forceinline__ void sweep_spheres(const R4<float>* __restrict__ sph, uint32_t n,
                                               int32_t base, V3<float> o, V3<float> d, float tmin,
                                               float& tb, int32_t& best) {
@@ -121,7 +145,7 @@ __device__ __forceinline__ void sweep_spheres(const R4<float>* __restrict__ sph,
     uint32_t ub = __float_as_uint(tb) - tminb;
 #pragma unroll 8
     for (uint32_t k = 0; k < n; ++k) {
-        const uint32_t u = sphere_u(sph[k], o, d, a, ia, tminb);
+        const uint32_t u = sphere_u<kRobust>(sph[k], o, d, a, ia, tminb);
         const bool h = u < ub;
         ub = h ? u : ub;
         best = h ? base + (int32_t)k : best;
@@ -132,6 +156,7 @@ __device__ __forceinline__ void sweep_spheres(const R4<float>* __restrict__ sph,
 // Sum of Sphere::pdf_value over the light list in list order
 // (HittableList::pdf_value, hittable_list.rs:408-412; sphere.rs:101-111).
 // f64: the reference's arithmetic, light by light.
+template <bool kRobust = false>
 __device__ __forceinline__ double lights_pdf_sum(const R4<double>* __restrict__ li, uint32_t n,
                                                  V3<double> o, V3<double> d) {
     double acc = 0.0;
@@ -141,13 +166,47 @@ __device__ __forceinline__ double lights_pdf_sum(const R4<double>* __restrict__ 
     }
     return acc;
 }
-// f32: pass 1 finds the lights the ray hits without a square root -- with
+// f32 light test: does the ray hit the light sphere with t in [0, inf)?  The
+// closest-approach offset l (see sphere_u) gives disc > 0 <=> l.l < r^2
+// without cancellation; the far root is >= 0 exactly when tc >= 0 or the
+// origin is inside (|f|^2 <= r^2).
+template <bool kRobust>
+__device__ __forceinline__ bool light_hit_f32(const R4<float>& L, V3<float> o, V3<float> d, float a, float ia) {
+    const float fx = o.x - L.x, fy = o.y - L.y, fz = o.z - L.z;
+    const float hb = __builtin_fmaf(d.z, fz, __builtin_fmaf(d.y, fy, d.x * fx));
+    const float r2 = L.w * L.w;
+    if constexpr (kRobust) {
+        const float tc = -hb * ia;
+        const float lx = __builtin_fmaf(tc, d.x, fx), ly = __builtin_fmaf(tc, d.y, fy),
+                    lz = __builtin_fmaf(tc, d.z, fz);
+        const float l2 = __builtin_fmaf(lx, lx, __builtin_fmaf(ly, ly, lz * lz));
+        const float f2 = __builtin_fmaf(fx, fx, __builtin_fmaf(fy, fy, fz * fz));
+        return (l2 < r2) & ((hb <= 0.f) | (f2 <= r2));
+    } else {
+        // disc = hb^2 - a c > 0 with c = f.f - r^2
+        const float c = __builtin_fmaf(fx, fx, __builtin_fmaf(fy, fy, __builtin_fmaf(fz, fz, -r2)));
+        const float disc = __builtin_fmaf(hb, hb, -(a * c));
+        return (disc > 0.f) & ((hb <= 0.f) | (c <= 0.f));
+    }
+}
+// its solid-angle pdf, 1 / (2 pi (1 - cos_max)) with 1 - cos_max = x / (1 +
+// sqrt(1 - x)), x = r^2/d^2 (no cancellation for far lights)
+__device__ __forceinline__ float light_pdf_f32(const R4<float>& L, V3<float> o) {
+    const float cx = L.x - o.x, cy = L.y - o.y, cz = L.z - o.z;
+    const float dist2 = __builtin_fmaf(cx, cx, __builtin_fmaf(cy, cy, cz * cz));
+    const float x = L.w * L.w * __builtin_amdgcn_rcpf(dist2);
+    const float one_minus_cos = x * __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_sqrtf(1.f - x));
+    return __builtin_amdgcn_rcpf(6.283185307179586f * one_minus_cos);
+}
+// f32: pass 1 finds the lights the ray hits (light_hit_f32, no square root) -- with
 // disc > 0 the far root (-hb + sqrt(disc)) / a is >= 0 exactly when hb <= 0
 // or c <= 0 -- into a bit mask; pass 2 adds the hit lights' solid-angle pdfs
 // in list order.  Most rays hit zero or one light.
+template <bool kRobust>
 __device__ __forceinline__ float lights_pdf_sum(const R4<float>* __restrict__ li, uint32_t n,
                                                 V3<float> o, V3<float> d) {
-    const float a = dot(d, d);
+    const float a = len2_f32(d);
+    const float ia = __builtin_amdgcn_rcpf(a);
     float acc = 0.f;
     for (uint32_t base = 0; base < n; base += 32) {
         const uint32_t m = min(32u, n - base);
@@ -155,21 +214,14 @@ __device__ __forceinline__ float lights_pdf_sum(const R4<float>* __restrict__ li
 #pragma unroll 4
         for (uint32_t k = 0; k < m; ++k) {
             const R4<float> L = li[base + k];
-            const float ocx = o.x - L.x, ocy = o.y - L.y, ocz = o.z - L.z;
-            const float hb = d.x * ocx + d.y * ocy + d.z * ocz;
-            const float c = ocx * ocx + (ocy * ocy + (ocz * ocz - L.w * L.w));
-            const float disc = hb * hb - a * c;
-            const bool hit = (disc > 0.f) & ((hb <= 0.f) | (c <= 0.f));
+            const bool hit = light_hit_f32<kRobust>(L, o, d, a, ia);
             mask |= (hit ? 1u : 0u) << k;
         }
         while (mask) {
             const uint32_t k = (uint32_t)__builtin_ctz(mask);
             mask &= mask - 1u;
             const R4<float> L = li[base + k];
-            const float cx = L.x - o.x, cy = L.y - o.y, cz = L.z - o.z;
-            const float dist2 = cx * cx + cy * cy + cz * cz;
-            const float cos_max = __builtin_amdgcn_sqrtf(1.f - L.w * L.w * __builtin_amdgcn_rcpf(dist2));
-            acc += __builtin_amdgcn_rcpf(6.283185307179586f * (1.f - cos_max));
+            acc += light_pdf_f32(L, o);
         }
     }
     return acc;
@@ -180,11 +232,11 @@ __device__ __forceinline__ float lights_pdf_sum(const R4<float>* __restrict__ li
 // sphere goes through the same per-sphere arithmetic as the brute-force
 // sweep, and the lowest id wins ties, so the result is the brute-force result.
 // ---------------------------------------------------------------------------
-template <typename R>
+template <typename R, bool kRobust>
 struct SphereTester;
 
-template <>
-struct SphereTester<double> {   // exact reference arithmetic (sphere.rs:61-80)
+template <bool kRobust>
+struct SphereTester<double, kRobust> {   // exact reference arithmetic (sphere.rs:61-80)
     V3<double> o, d;
     double tmin, tb;
     int32_t best;
@@ -199,15 +251,15 @@ struct SphereTester<double> {   // exact reference arithmetic (sphere.rs:61-80)
     }
 };
 
-template <>
-struct SphereTester<float> {    // the f32 sweep's arithmetic (see sweep_spheres)
+template <bool kRobust>
+struct SphereTester<float, kRobust> {    // the f32 sweep's arithmetic (see sphere_u)
     V3<float> o, d;
     float a, ia;
     uint32_t tminb, ub;
     int32_t best;
     __device__ __forceinline__ float bound() const { return __uint_as_float(ub + tminb); }
     __device__ __forceinline__ void test(const R4<float>& s, int32_t id) {
-        const uint32_t u = sphere_u(s, o, d, a, ia, tminb);
+        const uint32_t u = sphere_u<kRobust>(s, o, d, a, ia, tminb);
         const bool upd = u < ub || (u == ub && id < best);
         ub = upd ? u : ub;
         best = upd ? id : best;
@@ -219,9 +271,9 @@ __device__ __forceinline__ float inv_(float x) { return __builtin_amdgcn_rcpf(x)
 
 // Near-child-first traversal with a per-lane stack in LDS (stk[entry * 64]).
 // Slab test on padded child boxes against [0, tb].
-template <typename R>
+template <typename R, typename TT>
 __device__ __forceinline__ void bvh_traverse(const DevScene<R>& sc, int32_t base, V3<R> o, V3<R> d,
-                                             SphereTester<R>& T, int32_t* __restrict__ stk,
+                                             TT& T, int32_t* __restrict__ stk,
                                              uint32_t& nvis, uint32_t& ntest) {
     const R ix = inv_(d.x), iy = inv_(d.y), iz = inv_(d.z);
     const R oix = o.x * ix, oiy = o.y * iy, oiz = o.z * iz;
@@ -275,9 +327,9 @@ __device__ __forceinline__ void bvh_traverse(const DevScene<R>& sc, int32_t base
 // four slots are fetched at once (indices clamped to the leaf, so a short
 // leaf re-tests its last sphere -- a no-op: same t, same id, and ties only
 // move to a LOWER id) and tested without a data-dependent trip count.
-template <typename R>
+template <typename R, typename TT>
 __device__ __forceinline__ void test_leaf(const DevScene<R>& sc, int32_t base, int32_t leaf,
-                                          SphereTester<R>& T, uint32_t& ntest) {
+                                          TT& T, uint32_t& ntest) {
     const uint32_t code = (uint32_t)~leaf;
     const uint32_t first = code >> 4, cnt = code & 15u;
     if (cnt == 0) return;
@@ -304,9 +356,9 @@ __device__ __forceinline__ void test_leaf(const DevScene<R>& sc, int32_t base, i
 // branch.  A lane that reaches a leaf parks it and keeps descending until it
 // holds a second leaf; the inner phase ends when every lane holds a leaf (or
 // is done), then all parked leaves are tested together.
-template <typename R>
+template <typename R, typename TT>
 __device__ __forceinline__ void bvh_traverse_ww(const DevScene<R>& sc, int32_t base, V3<R> o, V3<R> d,
-                                                SphereTester<R>& T, int32_t* __restrict__ stk,
+                                                TT& T, int32_t* __restrict__ stk,
                                                 uint32_t& nvis, uint32_t& ntest) {
     constexpr int32_t kDone = 0x7fffffff;
     const R ix = inv_(d.x), iy = inv_(d.y), iz = inv_(d.z);
@@ -398,9 +450,9 @@ __device__ __forceinline__ void load_node4(const Bvh4Node<double>& nd, R4<double
 // advance is predicated, so a visit has no divergent branch).  The stack
 // holds at most sc.bvh4_stack entries (host-computed bound) and is written
 // one past its top.
-template <typename R>
+template <typename R, typename TT>
 __device__ __forceinline__ void bvh4_traverse(const DevScene<R>& sc, int32_t base, V3<R> o, V3<R> d,
-                                              SphereTester<R>& T, int32_t* __restrict__ stk,
+                                              TT& T, int32_t* __restrict__ stk,
                                               uint32_t& nvis, uint32_t& ntest) {
     constexpr int32_t kDone = 0x7fffffff;
     const R ix = inv_(d.x), iy = inv_(d.y), iz = inv_(d.z);
@@ -456,29 +508,29 @@ __device__ __forceinline__ void bvh4_traverse(const DevScene<R>& sc, int32_t bas
     }
 }
 
-template <int kKind, typename R>
+template <int kKind, typename R, typename TT>
 __device__ __forceinline__ void bvh_dispatch(const DevScene<R>& sc, int32_t base, V3<R> o, V3<R> d,
-                                             SphereTester<R>& T, int32_t* stk, uint32_t& nvis,
+                                             TT& T, int32_t* stk, uint32_t& nvis,
                                              uint32_t& ntest) {
     if constexpr (kKind == kWorldBvh4) bvh4_traverse(sc, base, o, d, T, stk, nvis, ntest);
     else if constexpr (kKind == kWorldBvhWW) bvh_traverse_ww(sc, base, o, d, T, stk, nvis, ntest);
     else bvh_traverse(sc, base, o, d, T, stk, nvis, ntest);
 }
 
-template <int kKind>
+template <int kKind, bool kRobust>
 __device__ __forceinline__ void bvh_closest(const DevScene<double>& sc, int32_t base, V3<double> o,
                                             V3<double> d, double tmin, double& tb, int32_t& best,
                                             int32_t* stk, uint32_t& nvis, uint32_t& ntest) {
-    SphereTester<double> T{o, d, tmin, tb, best};
+    SphereTester<double, kRobust> T{o, d, tmin, tb, best};
     bvh_dispatch<kKind>(sc, base, o, d, T, stk, nvis, ntest);
     tb = T.tb;
     best = T.best;
 }
-template <int kKind>
+template <int kKind, bool kRobust>
 __device__ __forceinline__ void bvh_closest(const DevScene<float>& sc, int32_t base, V3<float> o,
                                             V3<float> d, float tmin, float& tb, int32_t& best,
                                             int32_t* stk, uint32_t& nvis, uint32_t& ntest) {
-    SphereTester<float> T;
+    SphereTester<float, kRobust> T;
     T.o = o;
     T.d = d;
     T.a = len2_f32(d);
@@ -540,22 +592,17 @@ __device__ __forceinline__ void light_bvh_walk(const DevScene<R>& sc, V3<R> o, V
     }
 }
 
-// f32: sqrt-free hit test as in lights_pdf_sum; pdfs summed in walk order.
+// f32: light_hit_f32 / light_pdf_f32 as in lights_pdf_sum; pdfs summed in walk order.
+template <bool kRobust>
 __device__ __forceinline__ float lights_pdf_bvh(const DevScene<float>& sc, V3<float> o, V3<float> d,
                                                 int32_t* __restrict__ stk) {
     const float a = len2_f32(d);
+    const float ia = __builtin_amdgcn_rcpf(a);
     float acc = 0.f;
     light_bvh_walk(sc, o, d, stk, [&](uint32_t k) {
         const R4<float> L = sc.lsph[k];
-        const float ocx = o.x - L.x, ocy = o.y - L.y, ocz = o.z - L.z;
-        const float hb = d.x * ocx + d.y * ocy + d.z * ocz;
-        const float c = ocx * ocx + (ocy * ocy + (ocz * ocz - L.w * L.w));
-        const float disc = hb * hb - a * c;
-        if ((disc > 0.f) & ((hb <= 0.f) | (c <= 0.f))) {
-            const float dist2 = ocx * ocx + ocy * ocy + ocz * ocz;
-            const float cos_max = __builtin_amdgcn_sqrtf(1.f - L.w * L.w * __builtin_amdgcn_rcpf(dist2));
-            acc += __builtin_amdgcn_rcpf(6.283185307179586f * (1.f - cos_max));
-        }
+        const bool hit = light_hit_f32<kRobust>(L, o, d, a, ia);
+        if (hit) acc += light_pdf_f32(L, o);
     });
     return acc;
 }
@@ -563,6 +610,7 @@ __device__ __forceinline__ float lights_pdf_bvh(const DevScene<float>& sc, V3<fl
 // pdfs in LIST order with the reference arithmetic -- bit-identical to the
 // linear sum (misses add +0.0, which changes nothing).  More than 8 hits
 // falls back to the linear loop.
+template <bool kRobust>
 __device__ __forceinline__ double lights_pdf_bvh(const DevScene<double>& sc, V3<double> o, V3<double> d,
                                                  int32_t* __restrict__ stk) {
     constexpr uint32_t kMax = 8;
@@ -604,11 +652,18 @@ __device__ __forceinline__ double lights_pdf_bvh(const DevScene<double>& sc, V3<
 #define RTW_EXP 0
 #endif
 
-template <typename R, int kWorld>
+// kOpt: compile-time options, chosen per launch by the host
+//   kOptRobust   (f32) closest-approach sphere and light tests (far geometry)
+//   kOptLightBvh (BVH kernels) light pdf through the light BVH (long light lists)
+enum : int { kOptRobust = 1, kOptLightBvh = 2 };
+
+template <typename R, int kWorld, int kOpt>
 // f32: ask for 5 waves per SIMD (<= 96 VGPRs; the kernel fits without
 // spilling); f64 keeps the compiler's choice.
 __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? 5 : 1) render_kernel(const KParams<R> p) {
     using PR = P<R>;
+    constexpr bool kRobust = (kOpt & kOptRobust) != 0;
+    constexpr bool kLightBvh = (kOpt & kOptLightBvh) != 0 && kWorld >= kWorldBvh;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     R4<R>* s_sph = reinterpret_cast<R4<R>*>(smem);
     R4<R>* s_li = s_sph + p.sc.n_sph;
@@ -774,17 +829,17 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? 5 : 1) render_kernel(
                 {
                     R tb2 = tb;
                     int32_t best2 = best;
-                    bvh_closest<kWorld == kWorldBvhLds ? kWorldBvhWW : kWorld>(scw, nplanes, o, d, tmin, tb2, best2,
+                    bvh_closest<kWorld == kWorldBvhLds ? kWorldBvhWW : kWorld, kRobust>(scw, nplanes, o, d, tmin, tb2, best2,
                                         reinterpret_cast<int32_t*>(smem) + wave * p.stack * 64 + lane, nvis,
                                         ntest);
                     segs += best2 == -7 ? 1u : 0u;
                 }
 #endif
-                bvh_closest<kWorld == kWorldBvhLds ? kWorldBvhWW : kWorld>(scw, nplanes, o, d, tmin, tb, best,
+                bvh_closest<kWorld == kWorldBvhLds ? kWorldBvhWW : kWorld, kRobust>(scw, nplanes, o, d, tmin, tb, best,
                                     reinterpret_cast<int32_t*>(smem) + wave * p.stack * 64 + lane, nvis,
                                     ntest);
             } else {
-                sweep_spheres(sph, p.sc.n_sph, nplanes, o, d, tmin, tb, best);
+                sweep_spheres<kRobust>(sph, p.sc.n_sph, nplanes, o, d, tmin, tb, best);
             }
             ++segs;
 
@@ -871,17 +926,13 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? 5 : 1) render_kernel(
                     const V3<R> ndir = PR::normalize(dir);
                     const R cos_w = PR::over_pi(dot(ndir, uvw.w));
                     R acc;                                                // hittable_list.rs:408-412
-                    if constexpr (kWorld >= kWorldBvh) {
-                        if (p.light_bvh)
-                            acc = lights_pdf_bvh(p.sc, pnt, dir,
-                                                 reinterpret_cast<int32_t*>(smem) + wave * p.stack * 64 + lane);
-                        else
-                            acc = lights_pdf_sum(li, p.sc.n_lights, pnt, dir);
-                    } else {
-                        acc = lights_pdf_sum(li, p.sc.n_lights, pnt, dir);
-                    }
+                    if constexpr (kLightBvh)
+                        acc = lights_pdf_bvh<kRobust>(p.sc, pnt, dir,
+                                                      reinterpret_cast<int32_t*>(smem) + wave * p.stack * 64 + lane);
+                    else
+                        acc = lights_pdf_sum<kRobust>(li, p.sc.n_lights, pnt, dir);
 #if RTW_EXP == 2
-                    segs += lights_pdf_sum(li, p.sc.n_lights, pnt, mk(dir.y, dir.z, dir.x)) == (R)-7 ? 1u : 0u;
+                    segs += lights_pdf_sum<kRobust>(li, p.sc.n_lights, pnt, mk(dir.y, dir.z, dir.x)) == (R)-7 ? 1u : 0u;
 #endif
                     const R lpdf = PR::div_(acc, (R)p.sc.n_lights);
                     const R pdf = lpdf * (R)0.5 + PR::max_(cos_w, (R)0) * (R)0.5;
@@ -973,29 +1024,67 @@ __global__ void __launch_bounds__(256) reduce_chunks_kernel(const KParams<R> p, 
 
 }  // namespace dev
 
+// dynamic LDS above 64 KiB must be allowed per kernel
+template <typename R, int kWorld, int kOpt>
+inline void allow_lds(size_t lds_bytes) {
+    if (lds_bytes > 65536)
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&dev::render_kernel<R, kWorld, kOpt>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
+}
+
+template <typename R, int kOpt>
+inline void launch_world(const KParams<R>& p, int world, size_t lds_bytes, uint32_t blocks,
+                         hipStream_t stream) {
+    const size_t stacks = (size_t)kWavesPerBlock * p.stack * 64 * sizeof(int32_t);
+    constexpr int kBrute = kOpt & ~dev::kOptLightBvh;   // the light BVH needs the BVH kernels' stack
+    switch (world) {
+    case kWorldLds:
+        allow_lds<R, kWorldLds, kBrute>(lds_bytes);
+        hipLaunchKernelGGL((dev::render_kernel<R, kWorldLds, kBrute>), dim3(blocks), dim3(kBlock), lds_bytes,
+                           stream, p);
+        break;
+    case kWorldBvhLds:
+        allow_lds<R, kWorldBvhLds, kOpt>(lds_bytes);
+        hipLaunchKernelGGL((dev::render_kernel<R, kWorldBvhLds, kOpt>), dim3(blocks), dim3(kBlock), lds_bytes,
+                           stream, p);
+        break;
+    case kWorldBvh4:
+        hipLaunchKernelGGL((dev::render_kernel<R, kWorldBvh4, kOpt>), dim3(blocks), dim3(kBlock), stacks,
+                           stream, p);
+        break;
+    case kWorldBvhWW:
+        hipLaunchKernelGGL((dev::render_kernel<R, kWorldBvhWW, kOpt>), dim3(blocks), dim3(kBlock), stacks,
+                           stream, p);
+        break;
+    case kWorldBvh:
+        hipLaunchKernelGGL((dev::render_kernel<R, kWorldBvh, kOpt>), dim3(blocks), dim3(kBlock), stacks,
+                           stream, p);
+        break;
+    default:
+        hipLaunchKernelGGL((dev::render_kernel<R, kWorldGlobal, kBrute>), dim3(blocks), dim3(kBlock), 0, stream,
+                           p);
+        break;
+    }
+}
+
+// Options per launch: the f32 sphere-test form (DevScene::robust; f64 keeps
+// the reference arithmetic only) and the light BVH (KParams::light_bvh).
 template <typename R>
 inline int launch_render_impl(const KParams<R>& p, int world, size_t lds_bytes, R* out,
                               hipStream_t stream, hipEvent_t mid) {
     const uint32_t blocks = (p.n_tasks + kWavesPerBlock - 1) / kWavesPerBlock;
     if (blocks) {
-        if (world == kWorldLds) {
-            hipLaunchKernelGGL((dev::render_kernel<R, kWorldLds>), dim3(blocks), dim3(kBlock),
-                               lds_bytes, stream, p);
-        } else if (world == kWorldBvhLds) {
-            hipLaunchKernelGGL((dev::render_kernel<R, kWorldBvhLds>), dim3(blocks), dim3(kBlock), lds_bytes,
-                               stream, p);
-        } else if (world == kWorldBvh4) {
-            hipLaunchKernelGGL((dev::render_kernel<R, kWorldBvh4>), dim3(blocks), dim3(kBlock),
-                               (size_t)kWavesPerBlock * p.stack * 64 * sizeof(int32_t), stream, p);
-        } else if (world == kWorldBvhWW) {
-            hipLaunchKernelGGL((dev::render_kernel<R, kWorldBvhWW>), dim3(blocks), dim3(kBlock),
-                               (size_t)kWavesPerBlock * p.stack * 64 * sizeof(int32_t), stream, p);
-        } else if (world == kWorldBvh) {
-            hipLaunchKernelGGL((dev::render_kernel<R, kWorldBvh>), dim3(blocks), dim3(kBlock),
-                               (size_t)kWavesPerBlock * p.stack * 64 * sizeof(int32_t), stream, p);
+        const bool robust = sizeof(R) == 4 && p.sc.robust;
+        const bool lbvh = p.light_bvh != 0;
+        if constexpr (sizeof(R) == 4) {
+            if (robust && lbvh) launch_world<R, dev::kOptRobust | dev::kOptLightBvh>(p, world, lds_bytes, blocks, stream);
+            else if (robust) launch_world<R, dev::kOptRobust>(p, world, lds_bytes, blocks, stream);
+            else if (lbvh) launch_world<R, dev::kOptLightBvh>(p, world, lds_bytes, blocks, stream);
+            else launch_world<R, 0>(p, world, lds_bytes, blocks, stream);
         } else {
-            hipLaunchKernelGGL((dev::render_kernel<R, kWorldGlobal>), dim3(blocks), dim3(kBlock), 0,
-                               stream, p);
+            (void)robust;
+            if (lbvh) launch_world<R, dev::kOptLightBvh>(p, world, lds_bytes, blocks, stream);
+            else launch_world<R, 0>(p, world, lds_bytes, blocks, stream);
         }
         if (hipGetLastError() != hipSuccess) return -1;
     }

@@ -303,9 +303,18 @@ __device__ __forceinline__ R sphere_pdf_value(V3<R> c, R radius, V3<R> o, V3<R> 
     if (!sphere_t(c, radius * radius, o, d, (R)0, t)) return (R)0;
     V3<R> co = c - o;
     R dist2 = dot(co, co);
-    R cos_theta_max = P<R>::sqrt_((R)1 - P<R>::div_(radius * radius, dist2));
-    R solid_angle = ((R)2 * P<R>::kPi) * ((R)1 - cos_theta_max);
-    return P<R>::div_((R)1, solid_angle);
+    if constexpr (sizeof(R) == 4) {
+        // f32: 1 - sqrt(1 - x) = x / (1 + sqrt(1 - x)) -- for a far light
+        // (x = r^2/d^2 below 2^-24) the reference form rounds to 0 and the
+        // pdf to inf in f32
+        const float x = radius * radius * __builtin_amdgcn_rcpf(dist2);
+        const float one_minus_cos = x * __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_sqrtf(1.f - x));
+        return __builtin_amdgcn_rcpf((2.f * P<float>::kPi) * one_minus_cos);
+    } else {
+        R cos_theta_max = P<R>::sqrt_((R)1 - P<R>::div_(radius * radius, dist2));
+        R solid_angle = ((R)2 * P<R>::kPi) * ((R)1 - cos_theta_max);
+        return P<R>::div_((R)1, solid_angle);
+    }
 }
 
 // Sphere::random, sphere.rs:114-127
@@ -316,12 +325,22 @@ __device__ __forceinline__ V3<R> sphere_random(V3<R> c, R radius, V3<R> o, Rng& 
     Onb<R> uvw(direction);
     R r1 = P<R>::u_std(g.next());
     R r2 = P<R>::u_std(g.next());
-    R z = (R)1 + r1 * (P<R>::sqrt_((R)1 - P<R>::div_(radius * radius, distance * distance)) - (R)1);
     R s, cph;
     P<R>::sincos_2pi(r2, &s, &cph);
-    R x = cph * P<R>::sqrt_((R)1 - z * z);
-    R y = s * P<R>::sqrt_((R)1 - z * z);
-    return uvw.transform(mk(x, y, z));
+    if constexpr (sizeof(R) == 4) {
+        // f32: w = 1 - z = r1 (1 - cos_max) and 1 - z^2 = w (2 - w), both
+        // without cancellation for the narrow cone of a far light
+        const float q = radius * radius * __builtin_amdgcn_rcpf(distance * distance);
+        const float w = r1 * (q * __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_sqrtf(1.f - q)));
+        const float z = 1.f - w;
+        const float sxy = __builtin_amdgcn_sqrtf(w * (2.f - w));
+        return uvw.transform(mk(cph * sxy, s * sxy, z));
+    } else {
+        R z = (R)1 + r1 * (P<R>::sqrt_((R)1 - P<R>::div_(radius * radius, distance * distance)) - (R)1);
+        R x = cph * P<R>::sqrt_((R)1 - z * z);
+        R y = s * P<R>::sqrt_((R)1 - z * z);
+        return uvw.transform(mk(x, y, z));
+    }
 }
 
 // Dialectric::reflectance, material.rs:450-454; powi(5) = x * ((x*x)*(x*x))

@@ -90,6 +90,7 @@ struct DevScene {
     const uint32_t* lid;              // light-list index of lsph[k]
     uint32_t n_sph, n_planes, n_mat, n_lights, n_nodes, bvh_depth;
     uint32_t n_nodes4, bvh4_stack, n_lnodes, lbvh_depth;
+    uint32_t robust;                  // f32: closest-approach sphere / light tests (far geometry)
 };
 
 constexpr uint32_t kBvhStack = 32;    // per-lane traversal stack entries (LDS)

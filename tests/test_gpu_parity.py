@@ -367,3 +367,49 @@ def test_light_bvh_equals_linear_light_sum(prec):
         a, b = out["bvh"][0], out["linear"][0]
         ok = ~(np.isnan(a).any(-1) | np.isnan(b).any(-1))
         assert abs(a[ok].mean() - b[ok].mean()) < 0.02 * b[ok].mean()
+
+
+# ---- the large-scene configurations of SURVEY.md §8 (C3: 10k spheres, C5: 1M)
+# at small image sizes: same scene generator and camera, fewer pixels.
+
+def test_c3_scene_f64_matches_oracle():
+    soa, b = rtw.scenes.simple_soa(SEED_SCENE, 50)
+    assert len(soa.sphere_mat) > 9000 and len(soa.lights) >= 64     # light BVH on
+    cam = b.with_image_width(96).with_image_height(54).with_samples_per_pixel(4).with_max_depth(50).build()
+    gpu, chunk, (segs, lambs) = _render_gpu(soa, cam, 41, rtw.RTW_F64)
+    ref, st = _render_oracle(soa, cam, 41, chunk)
+    mae, exact = _compare_f64(gpu, ref, 4)
+    assert mae < F64_MAE_TOL and exact > 0.999
+    assert segs == st.segments and lambs == st.lambertian
+
+
+def test_c5_scene_bvh_equals_brute_force_f32():
+    soa, b = rtw.scenes.simple_soa(SEED_SCENE, 500)
+    assert len(soa.sphere_mat) > 900_000
+    cam = b.with_image_width(24).with_image_height(16).with_samples_per_pixel(2).with_max_depth(20).build()
+    off = {"light_bvh_min": 1 << 30}
+    brute, _, cb = _render_gpu(soa, cam, 43, rtw.RTW_F32, accel=rtw.RTW_ACCEL_BRUTE, tuning=off)
+    bvh, _, cv = _render_gpu(soa, cam, 43, rtw.RTW_F32, accel=rtw.RTW_ACCEL_BVH, tuning=off)
+    assert _same(brute, bvh) and cb == cv
+
+
+def test_c5_scene_f64_matches_oracle():
+    soa, b = rtw.scenes.simple_soa(SEED_SCENE, 500)
+    cam = b.with_image_width(32).with_image_height(18).with_samples_per_pixel(2).with_max_depth(50).build()
+    gpu, chunk, (segs, lambs) = _render_gpu(soa, cam, 47, rtw.RTW_F64)
+    ref, st = _render_oracle(soa, cam, 47, chunk)
+    mae, exact = _compare_f64(gpu, ref, 2)
+    assert mae < F64_MAE_TOL and exact > 0.999
+    assert segs == st.segments and lambs == st.lambertian
+
+
+@pytest.mark.parametrize("robust", [0, 1])
+def test_f32_sphere_test_forms_bvh_equals_brute(robust):
+    """Both f32 ray-sphere forms (tuning "robust": the reference's hb^2 - a c,
+    or the closest-approach form used for far geometry) give BVH == brute."""
+    soa, b = _scene(11)
+    cam = b.with_image_width(48).with_image_height(32).with_samples_per_pixel(4).with_max_depth(50).build()
+    t = {"robust": robust, "light_bvh_min": 1 << 30}
+    brute, _, cb = _render_gpu(soa, cam, 19, rtw.RTW_F32, accel=rtw.RTW_ACCEL_BRUTE, tuning=t)
+    bvh, _, cv = _render_gpu(soa, cam, 19, rtw.RTW_F32, accel=rtw.RTW_ACCEL_BVH, tuning=t)
+    assert _same(brute, bvh) and cb == cv
