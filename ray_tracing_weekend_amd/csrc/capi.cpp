@@ -107,6 +107,14 @@ std::vector<unsigned char> stage_scene(const rtw_scene* s, rtw::DevScene<R>* ds,
     const size_t o_nodes = reserve(sizeof(rtw::BvhNode<R>) * bb.nodes.size());
     const size_t o_bsph = reserve(sizeof(R4) * s->n_spheres);
     const size_t o_bid = reserve(sizeof(uint32_t) * s->n_spheres);
+    // isolated spheres (self-hit shortcut): bit 31 of sphere_mat.  The margin
+    // covers the rounding of the hit point the next segment starts from and
+    // of the precision-R sphere tests of nearby spheres (grazing hits).
+    double scale = 0.0;
+    for (uint32_t k = 0; k < s->n_spheres; ++k)
+        for (int a = 0; a < 3; ++a) scale = std::max(scale, fabs(s->spheres[4 * k + a]) + fabs(s->spheres[4 * k + 3]));
+    const double iso_margin = std::is_same<R, float>::value ? 1e-2 + 1e-5 * scale : 1e-6 + 1e-12 * scale;
+    const std::vector<uint8_t> iso = rtw::isolated_spheres(s->spheres, s->n_spheres, bb, iso_margin);
     const rtw::Bvh4Build b4 = rtw::collapse_bvh4(bb);
     const size_t o_nodes4 = reserve(sizeof(rtw::Bvh4Node<R>) * 8 * b4.nodes.size());
     // BVH over the light spheres for the light pdf (a query for EVERY light
@@ -127,6 +135,8 @@ std::vector<unsigned char> stage_scene(const rtw_scene* s, rtw::DevScene<R>* ds,
         reinterpret_cast<R*>(b + o_r)[k] = r;
         reinterpret_cast<uint32_t*>(b + o_smat)[k] = s->sphere_mat[k];
     }
+    for (uint32_t k = 0; k < s->n_spheres; ++k)
+        if (iso[k]) reinterpret_cast<uint32_t*>(b + o_smat)[k] |= 0x80000000u;
     for (uint32_t k = 0; k < s->n_planes; ++k) {
         // {point, normal, AABB lo, AABB hi}: Plane::get_aabbox (plane.rs:218-242)
         // pins the normal axis at 0 and leaves the others infinite

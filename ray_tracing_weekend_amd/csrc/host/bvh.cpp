@@ -303,6 +303,51 @@ struct Collapser {
 
 }  // namespace
 
+std::vector<uint8_t> isolated_spheres(const double* spheres, uint32_t n, const BvhBuild& b, double margin) {
+    std::vector<uint8_t> iso(n, 0);
+    if (b.nodes.empty()) return iso;
+    std::vector<int32_t> stack;
+    for (uint32_t i = 0; i < n; ++i) {
+        const double* si = spheres + 4 * i;
+        if (!(si[3] >= 0)) continue;
+        const double reach = si[3] + margin;
+        double lo[3], hi[3];
+        for (int a = 0; a < 3; ++a) {
+            lo[a] = si[a] - reach;
+            hi[a] = si[a] + reach;
+        }
+        bool alone = true;
+        stack.clear();
+        stack.push_back(0);
+        while (alone && !stack.empty()) {
+            const int32_t node = stack.back();
+            stack.pop_back();
+            if (node >= 0) {
+                const BvhBuild::Node& nd = b.nodes[node];
+                for (int c = 0; c < 2; ++c) {
+                    bool overlap = true;
+                    for (int a = 0; a < 3; ++a)
+                        overlap = overlap && nd.lo[c][a] <= hi[a] && nd.hi[c][a] >= lo[a];
+                    if (overlap) stack.push_back(nd.child[c]);
+                }
+            } else {
+                const uint32_t code = ~(uint32_t)node;
+                for (uint32_t k = 0; k < (code & 15u) && alone; ++k) {
+                    const uint32_t j = b.order[(code >> 4) + k];
+                    if (j == i) continue;
+                    const double* sj = spheres + 4 * j;
+                    if (!(sj[3] >= 0)) continue;
+                    const double dx = si[0] - sj[0], dy = si[1] - sj[1], dz = si[2] - sj[2];
+                    const double lim = si[3] + sj[3] + margin;
+                    if (dx * dx + dy * dy + dz * dz <= lim * lim) alone = false;
+                }
+            }
+        }
+        iso[i] = alone ? 1 : 0;
+    }
+    return iso;
+}
+
 Bvh4Build collapse_bvh4(const BvhBuild& b) {
     Bvh4Build out;
     if (b.nodes.empty()) return out;

@@ -57,4 +57,11 @@ struct Bvh4Build {
 
 Bvh4Build collapse_bvh4(const BvhBuild& b);
 
+// Spheres whose closed ball is at least `margin` away from every other
+// sphere's (negative radii never hit and are ignored).  A ray that starts on
+// such a sphere and hits it again reaches that hit along a chord of the ball,
+// which no other sphere touches -- so that hit is the closest sphere hit and
+// the render kernel skips the traversal for it (self-hit shortcut).
+std::vector<uint8_t> isolated_spheres(const double* spheres, uint32_t n, const BvhBuild& b, double margin);
+
 }  // namespace rtw

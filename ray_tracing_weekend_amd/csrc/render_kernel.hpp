@@ -241,14 +241,17 @@ struct SphereTester<double, kRobust> {   // exact reference arithmetic (sphere.r
     double tmin, tb;
     int32_t best;
     __device__ __forceinline__ double bound() const { return tb; }
-    __device__ __forceinline__ void test(const R4<double>& s, int32_t id) {
+    // returns whether the sphere is hit at all (t in [tmin, inf])
+    __device__ __forceinline__ bool test_hit(const R4<double>& s, int32_t id) {
         double t;
-        if (sphere_t(mk(s.x, s.y, s.z), s.w, o, d, tmin, t) &&
-            (best < 0 || t < tb || (t == tb && id < best))) {
+        const bool hit = sphere_t(mk(s.x, s.y, s.z), s.w, o, d, tmin, t);
+        if (hit && (best < 0 || t < tb || (t == tb && id < best))) {
             tb = t;
             best = id;
         }
+        return hit;
     }
+    __device__ __forceinline__ void test(const R4<double>& s, int32_t id) { (void)test_hit(s, id); }
 };
 
 template <bool kRobust>
@@ -264,6 +267,14 @@ struct SphereTester<float, kRobust> {    // the f32 sweep's arithmetic (see sphe
         ub = upd ? u : ub;
         best = upd ? id : best;
     }
+    // returns whether the sphere is hit at all (t in [tmin, inf])
+    __device__ __forceinline__ bool test_hit(const R4<float>& s, int32_t id) {
+        const uint32_t u = sphere_u<kRobust>(s, o, d, a, ia, tminb);
+        const bool upd = u < ub || (u == ub && id < best);
+        ub = upd ? u : ub;
+        best = upd ? id : best;
+        return u <= 0x7f800000u - tminb;
+    }
 };
 
 __device__ __forceinline__ double inv_(double x) { return 1.0 / x; }
@@ -274,7 +285,8 @@ __device__ __forceinline__ float inv_(float x) { return __builtin_amdgcn_rcpf(x)
 template <typename R, typename TT>
 __device__ __forceinline__ void bvh_traverse(const DevScene<R>& sc, int32_t base, V3<R> o, V3<R> d,
                                              TT& T, int32_t* __restrict__ stk,
-                                             uint32_t& nvis, uint32_t& ntest) {
+                                             uint32_t& nvis, uint32_t& ntest, bool skip) {
+    if (skip) return;
     const R ix = inv_(d.x), iy = inv_(d.y), iz = inv_(d.z);
     const R oix = o.x * ix, oiy = o.y * iy, oiz = o.z * iz;
     const BvhNode<R>* __restrict__ nodes = sc.bvh;
@@ -359,13 +371,13 @@ __device__ __forceinline__ void test_leaf(const DevScene<R>& sc, int32_t base, i
 template <typename R, typename TT>
 __device__ __forceinline__ void bvh_traverse_ww(const DevScene<R>& sc, int32_t base, V3<R> o, V3<R> d,
                                                 TT& T, int32_t* __restrict__ stk,
-                                                uint32_t& nvis, uint32_t& ntest) {
+                                                uint32_t& nvis, uint32_t& ntest, bool skip) {
     constexpr int32_t kDone = 0x7fffffff;
     const R ix = inv_(d.x), iy = inv_(d.y), iz = inv_(d.z);
     const R oix = o.x * ix, oiy = o.y * iy, oiz = o.z * iz;
     const BvhNode<R>* __restrict__ nodes = sc.bvh;
     int32_t sp = 0;
-    int32_t node = 0;   // inner node index, leaf code (< 0) or kDone
+    int32_t node = skip ? kDone : 0;   // inner node index, leaf code (< 0) or kDone
     int32_t leaf = 0;   // parked leaf code, 0 = none
     for (;;) {
         for (;;) {
@@ -453,14 +465,14 @@ __device__ __forceinline__ void load_node4(const Bvh4Node<double>& nd, R4<double
 template <typename R, typename TT>
 __device__ __forceinline__ void bvh4_traverse(const DevScene<R>& sc, int32_t base, V3<R> o, V3<R> d,
                                               TT& T, int32_t* __restrict__ stk,
-                                              uint32_t& nvis, uint32_t& ntest) {
+                                              uint32_t& nvis, uint32_t& ntest, bool skip) {
     constexpr int32_t kDone = 0x7fffffff;
     const R ix = inv_(d.x), iy = inv_(d.y), iz = inv_(d.z);
     const R oix = o.x * ix, oiy = o.y * iy, oiz = o.z * iz;
     const uint32_t oct = sign_bit(ix) | (sign_bit(iy) << 1) | (sign_bit(iz) << 2);
     const Bvh4Node<R>* __restrict__ nodes = sc.bvh4 + oct * sc.n_nodes4;
     int32_t sp = 0;
-    int32_t node = 0;   // inner node index, leaf code (< 0) or kDone
+    int32_t node = skip ? kDone : 0;   // inner node index, leaf code (< 0) or kDone
     int32_t leaf = 0;   // parked leaf code, 0 = none
     for (;;) {
         for (;;) {
@@ -508,28 +520,36 @@ __device__ __forceinline__ void bvh4_traverse(const DevScene<R>& sc, int32_t bas
     }
 }
 
+// `self` >= 0: the ray starts on that (isolated) sphere; it is tested first
+// and, when the ray hits it again, that hit is the closest sphere hit (see
+// isolated_spheres, host/bvh.hpp) and the traversal is skipped.
 template <int kKind, typename R, typename TT>
 __device__ __forceinline__ void bvh_dispatch(const DevScene<R>& sc, int32_t base, V3<R> o, V3<R> d,
                                              TT& T, int32_t* stk, uint32_t& nvis,
-                                             uint32_t& ntest) {
-    if constexpr (kKind == kWorldBvh4) bvh4_traverse(sc, base, o, d, T, stk, nvis, ntest);
-    else if constexpr (kKind == kWorldBvhWW) bvh_traverse_ww(sc, base, o, d, T, stk, nvis, ntest);
-    else bvh_traverse(sc, base, o, d, T, stk, nvis, ntest);
+                                             uint32_t& ntest, int32_t self) {
+    bool skip = false;
+    if (self >= 0) {
+        skip = T.test_hit(sc.sph[self], base + self);
+        ++ntest;
+    }
+    if constexpr (kKind == kWorldBvh4) bvh4_traverse(sc, base, o, d, T, stk, nvis, ntest, skip);
+    else if constexpr (kKind == kWorldBvhWW) bvh_traverse_ww(sc, base, o, d, T, stk, nvis, ntest, skip);
+    else bvh_traverse(sc, base, o, d, T, stk, nvis, ntest, skip);
 }
 
 template <int kKind, bool kRobust>
 __device__ __forceinline__ void bvh_closest(const DevScene<double>& sc, int32_t base, V3<double> o,
                                             V3<double> d, double tmin, double& tb, int32_t& best,
-                                            int32_t* stk, uint32_t& nvis, uint32_t& ntest) {
+                                            int32_t* stk, uint32_t& nvis, uint32_t& ntest, int32_t self) {
     SphereTester<double, kRobust> T{o, d, tmin, tb, best};
-    bvh_dispatch<kKind>(sc, base, o, d, T, stk, nvis, ntest);
+    bvh_dispatch<kKind>(sc, base, o, d, T, stk, nvis, ntest, self);
     tb = T.tb;
     best = T.best;
 }
 template <int kKind, bool kRobust>
 __device__ __forceinline__ void bvh_closest(const DevScene<float>& sc, int32_t base, V3<float> o,
                                             V3<float> d, float tmin, float& tb, int32_t& best,
-                                            int32_t* stk, uint32_t& nvis, uint32_t& ntest) {
+                                            int32_t* stk, uint32_t& nvis, uint32_t& ntest, int32_t self) {
     SphereTester<float, kRobust> T;
     T.o = o;
     T.d = d;
@@ -538,7 +558,7 @@ __device__ __forceinline__ void bvh_closest(const DevScene<float>& sc, int32_t b
     T.tminb = __float_as_uint(tmin);
     T.ub = __float_as_uint(tb) - T.tminb;
     T.best = best;
-    bvh_dispatch<kKind>(sc, base, o, d, T, stk, nvis, ntest);
+    bvh_dispatch<kKind>(sc, base, o, d, T, stk, nvis, ntest, self);
     tb = T.bound();
     best = T.best;
 }
@@ -734,6 +754,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? 5 : 1) render_kernel(
     Rng g;
     V3<R> o = zero, d = zero, mult = zero, res = zero;
     uint32_t depth = 0;
+    int32_t self_s = -1;          // isolated sphere the current ray starts on (else -1)
     uint32_t segs = 0, lambs = 0, nvis = 0, ntest = 0;
     bool active = false, need = true;
 
@@ -753,6 +774,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? 5 : 1) render_kernel(
         mult = mk<R>(1, 1, 1);
         res = zero;
         depth = p.max_depth;
+        self_s = -1;
     };
     // Give every lane that needs one a valid item (or none: pool drained).
     auto acquire = [&]() {
@@ -831,13 +853,13 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? 5 : 1) render_kernel(
                     int32_t best2 = best;
                     bvh_closest<kWorld == kWorldBvhLds ? kWorldBvhWW : kWorld, kRobust>(scw, nplanes, o, d, tmin, tb2, best2,
                                         reinterpret_cast<int32_t*>(smem) + wave * p.stack * 64 + lane, nvis,
-                                        ntest);
+                                        ntest, self_s);
                     segs += best2 == -7 ? 1u : 0u;
                 }
 #endif
                 bvh_closest<kWorld == kWorldBvhLds ? kWorldBvhWW : kWorld, kRobust>(scw, nplanes, o, d, tmin, tb, best,
                                     reinterpret_cast<int32_t*>(smem) + wave * p.stack * 64 + lane, nvis,
-                                    ntest);
+                                    ntest, self_s);
             } else {
                 sweep_spheres<kRobust>(sph, p.sc.n_sph, nplanes, o, d, tmin, tb, best);
             }
@@ -853,6 +875,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? 5 : 1) render_kernel(
                 V3<R> pnt = o + d * tb;
                 V3<R> outward;
                 uint32_t m;
+                int32_t next_self = -1;
                 if (best < nplanes) {
                     const R* pl = p.sc.planes + 12 * best;
                     outward = mk(pl[3], pl[4], pl[5]);
@@ -861,7 +884,9 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? 5 : 1) render_kernel(
                     const uint32_t k = (uint32_t)(best - nplanes);
                     const R4<R> sk = p.sc.sph[k];
                     outward = PR::divs(pnt - mk(sk.x, sk.y, sk.z), p.sc.sph_r[k]);  // sphere.rs:82-83
-                    m = p.sc.sph_mat[k];
+                    const uint32_t mw = p.sc.sph_mat[k];
+                    m = mw & 0x7fffffffu;
+                    next_self = (mw >> 31) ? (int32_t)k : -1;   // bit 31: isolated sphere
                 }
                 const bool front = dot(d, outward) < (R)0;
                 const V3<R> nrm = front ? outward : -outward;
@@ -878,6 +903,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? 5 : 1) render_kernel(
                     } else {
                         mult = mult * mk(mp.x, mp.y, mp.z);            // Reflect, camera.rs:488-500
                         o = pnt;
+                        self_s = next_self;
                         d = dir;
                     }
                 } else if (mtype == kMatDielectric) {
@@ -894,6 +920,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? 5 : 1) render_kernel(
                         dir = refract(unit, nrm, ratio);
                     // mult * Colour(1, 1, 1) is the identity on every value
                     o = pnt;
+                    self_s = next_self;
                     d = dir;
                 } else if (mtype == kMatLambertian) {
                     // Lambertian + MixturePdf(HittablePdf(lights), CosinePdf):
@@ -942,6 +969,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? 5 : 1) render_kernel(
                     res = res + mult * emitted;
                     mult = new_mult;
                     o = pnt;
+                    self_s = next_self;
                     d = dir;
                 } else {
                     // Invisible (material.rs:321-325): scatter() == None
