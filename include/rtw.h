@@ -132,7 +132,8 @@ int rtw_set_accel(rtw_ctx *ctx, int accel);
  * "lds" (1 = stage the sphere list in LDS when it fits, 0 = read it from HBM),
  * "robust" (f32 ray-sphere tests in closest-approach form: 1 on, 0 off,
  * 2 = by the scene's distance-to-radius ratio, the default),
- * "light_bvh_min" (light lists this long or longer take the light BVH in
+ * "bvh_leaf" (spheres per BVH leaf, 1..15, default 4; takes effect at the
+ * next rtw_set_scene), "light_bvh_min" (light lists this long or longer take the light BVH in
  * the BVH kernels, default 64), "partial_max" (bytes of chunk sums an auto chunk may use, default 8 GiB),
  * "bvh_kind" (3 = binary while-while on the tree staged in LDS, the
  * default, 1 = binary while-while from L1/L2, 2 = 4-wide octant BVH, 0 =

@@ -36,6 +36,7 @@ struct rtw_ctx {
     size_t bvh_lds_max = 32 * 1024;   // LDS per workgroup allowed for bvh_kind 3
     int robust = 2;                   // f32 closest-approach tests: 1 on, 0 off, 2 by scene scale
     double scene_extent = 0.0, min_radius = 0.0;   // of the staged scene (robust = 2)
+    uint32_t bvh_leaf = 4;            // spheres per BVH leaf (set before rtw_set_scene)
     uint32_t light_bvh_min = 64;      // light lists at least this long use the light BVH
                                       // (C2, 19 lights: the linear masked loop is faster)
     hipStream_t stream = nullptr;
@@ -84,7 +85,8 @@ size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 // Convert the caller's f64 SoA into the device layout of precision R, in one
 // host staging blob, and fill the DevScene pointers relative to `base`.
 template <typename R>
-std::vector<unsigned char> stage_scene(const rtw_scene* s, rtw::DevScene<R>* ds, uintptr_t base) {
+std::vector<unsigned char> stage_scene(const rtw_scene* s, rtw::DevScene<R>* ds, uintptr_t base,
+                                       uint32_t leaf_max) {
     using R4 = rtw::R4<R>;
     size_t off = 0;
     auto reserve = [&](size_t bytes) {
@@ -103,7 +105,7 @@ std::vector<unsigned char> stage_scene(const rtw_scene* s, rtw::DevScene<R>* ds,
     // BVH over the spheres; boxes padded outward by a margin that absorbs the
     // rounding of the slab test in precision R (it only ever culls)
     const rtw::BvhBuild bb = rtw::build_bvh(s->spheres, s->n_spheres,
-                                            std::is_same<R, float>::value ? 1e-5 : 1e-12);
+                                            std::is_same<R, float>::value ? 1e-5 : 1e-12, leaf_max);
     const size_t o_nodes = reserve(sizeof(rtw::BvhNode<R>) * bb.nodes.size());
     const size_t o_bsph = reserve(sizeof(R4) * s->n_spheres);
     const size_t o_bid = reserve(sizeof(uint32_t) * s->n_spheres);
@@ -501,6 +503,7 @@ int rtw_set_tuning(rtw_ctx* c, const char* key, int64_t value) {
     if (k == "chunk") c->chunk = (uint32_t)value;
     else if (k == "auto_chunk") c->auto_chunk = std::max<uint32_t>(1, (uint32_t)value);
     else if (k == "robust") c->robust = (int)std::min<int64_t>(value, 2);
+    else if (k == "bvh_leaf") c->bvh_leaf = (uint32_t)std::max<int64_t>(1, std::min<int64_t>(value, 15));
     else if (k == "light_bvh_min") c->light_bvh_min = (uint32_t)std::min<int64_t>(value, 1u << 30);
     else if (k == "partial_max") c->partial_max = std::max<size_t>(1 << 20, (size_t)value);
     else if (k == "group") c->group = (uint32_t)value;
@@ -611,8 +614,8 @@ int rtw_set_scene(rtw_ctx* c, const rtw_scene* s) {
     // pointer member of DevScene must be listed in `rebase`)
     rtw::DevScene<float> tmp32{};
     rtw::DevScene<double> tmp64{};
-    std::vector<unsigned char> blob = c->precision == RTW_F32 ? stage_scene<float>(s, &tmp32, 0)
-                                                               : stage_scene<double>(s, &tmp64, 0);
+    std::vector<unsigned char> blob = c->precision == RTW_F32 ? stage_scene<float>(s, &tmp32, 0, c->bvh_leaf)
+                                                               : stage_scene<double>(s, &tmp64, 0, c->bvh_leaf);
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     if (c->scene_bytes < blob.size()) {
         if (c->d_scene) (void)hipFree(c->d_scene);

@@ -41,6 +41,7 @@ struct Builder {
     std::vector<Prim> prims;
     BvhBuild* out;
     double pad;
+    uint32_t leaf_max;
 
     Box padded(Box b) const {
         for (int k = 0; k < 3; ++k) {
@@ -56,7 +57,7 @@ struct Builder {
         for (uint32_t k = b; k < e; ++k) box.grow(prims[k].box);
         *box_out = padded(box);
         const uint32_t n = e - b;
-        if (n <= kLeafMax) {
+        if (n <= leaf_max) {
             std::sort(prims.begin() + b, prims.begin() + e,
                       [](const Prim& x, const Prim& y) { return x.id < y.id; });
             const uint32_t first = (uint32_t)out->order.size();
@@ -138,10 +139,11 @@ struct Builder {
 
 }  // namespace
 
-BvhBuild build_bvh(const double* spheres, uint32_t n, double pad_rel) {
+BvhBuild build_bvh(const double* spheres, uint32_t n, double pad_rel, uint32_t leaf_max) {
     BvhBuild out;
     Builder bld;
     bld.out = &out;
+    bld.leaf_max = leaf_max < 1 ? 1 : (leaf_max > 15 ? 15 : leaf_max);
     bld.prims.resize(n);
     double scale = 0.0;
     for (uint32_t k = 0; k < n; ++k) {
@@ -158,9 +160,9 @@ BvhBuild build_bvh(const double* spheres, uint32_t n, double pad_rel) {
     }
     bld.pad = pad_rel * (scale + 1.0);
     out.order.reserve(n);
-    out.nodes.reserve(n ? 2 * (n / kLeafMax + 1) : 1);
-    // the root is always an inner node (an empty right child when n <= kLeafMax)
-    if (n <= kLeafMax) {
+    out.nodes.reserve(n ? 2 * (n / bld.leaf_max + 1) : 1);
+    // the root is always an inner node (an empty right child when n <= leaf_max)
+    if (n <= bld.leaf_max) {
         out.nodes.emplace_back();
         Box lb;
         int32_t l = n ? bld.build(0, n, 1, &lb) : leaf_code(0, 0);

@@ -36,7 +36,8 @@ inline int32_t leaf_code(uint32_t first, uint32_t count) { return ~(int32_t)((fi
 
 // spheres: n x {cx, cy, cz, r}.  pad_rel: relative outward padding of every
 // box (absorbs the rounding of the device slab test in the kernel precision).
-BvhBuild build_bvh(const double* spheres, uint32_t n, double pad_rel);
+// leaf_max: spheres per leaf (1..15; the kernel tests leaves in groups of 4).
+BvhBuild build_bvh(const double* spheres, uint32_t n, double pad_rel, uint32_t leaf_max = kLeafMax);
 
 // 4-wide BVH collapsed from the binary one (same leaves, same boxes): every
 // node takes the up-to-4 descendants reached by repeatedly opening its

@@ -335,30 +335,32 @@ __device__ __forceinline__ void bvh_traverse(const DevScene<R>& sc, int32_t base
     }
 }
 
-// Test a parked leaf (<= kLeafMax = 4 spheres, contiguous in bsph/bid).  All
-// four slots are fetched at once (indices clamped to the leaf, so a short
-// leaf re-tests its last sphere -- a no-op: same t, same id, and ties only
-// move to a LOWER id) and tested without a data-dependent trip count.
+// Test a parked leaf (<= 15 spheres, contiguous in bsph/bid) in groups of
+// four: each group's slots are fetched at once (indices clamped to the leaf,
+// so a short group re-tests its last sphere -- a no-op: same t, same id, and
+// ties only move to a LOWER id) and tested without a data-dependent trip
+// count.  With the default 4-sphere leaves there is exactly one group.
 template <typename R, typename TT>
 __device__ __forceinline__ void test_leaf(const DevScene<R>& sc, int32_t base, int32_t leaf,
                                           TT& T, uint32_t& ntest) {
     const uint32_t code = (uint32_t)~leaf;
     const uint32_t first = code >> 4, cnt = code & 15u;
-    if (cnt == 0) return;
-    R4<R> s[4];
-    int32_t id[4];
+    for (uint32_t g0 = 0; g0 < cnt; g0 += 4) {
+        R4<R> s[4];
+        int32_t id[4];
 #pragma unroll
-    for (uint32_t k = 0; k < 4; ++k) {
-        const uint32_t i = first + (k < cnt ? k : cnt - 1);
-        s[k] = sc.bsph[i];
-        id[k] = (int32_t)sc.bid[i];
-    }
-    if constexpr (sizeof(R) == 4) {
-        asm volatile("" : "+v"(s[0].x), "+v"(s[1].x), "+v"(s[2].x), "+v"(s[3].x), "+v"(id[0]), "+v"(id[1]),
-                     "+v"(id[2]), "+v"(id[3]));
-    }
+        for (uint32_t k = 0; k < 4; ++k) {
+            const uint32_t i = first + min(g0 + k, cnt - 1);
+            s[k] = sc.bsph[i];
+            id[k] = (int32_t)sc.bid[i];
+        }
+        if constexpr (sizeof(R) == 4) {
+            asm volatile("" : "+v"(s[0].x), "+v"(s[1].x), "+v"(s[2].x), "+v"(s[3].x), "+v"(id[0]), "+v"(id[1]),
+                         "+v"(id[2]), "+v"(id[3]));
+        }
 #pragma unroll
-    for (int k = 0; k < 4; ++k) T.test(s[k], base + id[k]);
+        for (int k = 0; k < 4; ++k) T.test(s[k], base + id[k]);
+    }
     ntest += cnt;
 }
 

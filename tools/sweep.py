@@ -21,6 +21,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--spp", type=int, default=500)
+    ap.add_argument("--depth", type=int, default=50)
     ap.add_argument("--precision", default="f32")
     ap.add_argument("--grid", default="auto_chunk=4,8,16;target_tasks=65536,131072;lds=1,0")
     ap.add_argument("--accel", type=int, default=0)
@@ -28,7 +29,7 @@ def main():
     prec = rtw.RTW_F32 if a.precision == "f32" else rtw.RTW_F64
     scene, b = rtw.scenes.simple_soa()
     W, H = 1200, 800
-    cam = b.with_image_width(W).with_image_height(H).with_samples_per_pixel(a.spp).with_max_depth(50).build()
+    cam = b.with_image_width(W).with_image_height(H).with_samples_per_pixel(a.spp).with_max_depth(a.depth).build()
     keys, vals = [], []
     for part in a.grid.split(";"):
         k, v = part.split("=")
@@ -41,10 +42,14 @@ def main():
     buf = torch.zeros((H, W, 3), dtype=torch.float32 if prec == rtw.RTW_F32 else torch.float64,
                       device="cuda:0")
     res = {c: [] for c in combos}
+    staged = {}
     for rd in range(a.rounds + 1):
         for c in combos:
             for k, v in zip(keys, c):
                 r.set_tuning(k, v)
+            if "bvh_leaf" in keys and staged.get("leaf") != dict(zip(keys, c))["bvh_leaf"]:
+                r.set_scene(scene)        # the leaf size is a build parameter
+                staged["leaf"] = dict(zip(keys, c))["bvh_leaf"]
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             r.render_device(cam, 5 + rd, buf.data_ptr(), buf.numel() * buf.element_size())
@@ -58,7 +63,9 @@ def main():
         print(json.dumps({"cfg": dict(zip(keys, c)), "ms": round(ms, 2),
                           "msamples_s": round(W * H * a.spp / (ms * 1e-3) / 1e6, 1)}), flush=True)
     print(json.dumps({"segments_per_sample": st.segments / max(st.samples, 1),
-                      "lambertian_per_sample": st.lambertian / max(st.samples, 1)}))
+                      "lambertian_per_sample": st.lambertian / max(st.samples, 1),
+                      "node_visits_per_segment": st.node_visits / max(st.segments, 1),
+                      "sphere_tests_per_segment": st.sphere_tests / max(st.segments, 1)}))
 
 
 if __name__ == "__main__":
