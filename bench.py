@@ -66,6 +66,22 @@ def parse():
     return ap.parse_args()
 
 
+def pmc_traffic(workload, precision, world):
+    """HBM bytes per render-kernel launch from the committed rocprofv3 PMC
+    summary of this workload and kernel (tools/pmc_summary.py --traffic:
+    FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md "HBM"), or None."""
+    import glob
+    dtype = "float" if precision == "f32" else "double"
+    best = None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json"))):
+        with open(f) as fh:
+            d = json.load(fh)
+        if d.get("workload") == workload and any(
+                k.startswith(f"void rtw::dev::render_kernel<{dtype}, {world},") for k in d.get("kernel", [])):
+            best = d
+    return best
+
+
 def cpu_baseline(scene, target_s):
     """The oracle (C restatement of the reference path, oracle/) timed on this
     host on a bounded sample of the same workload: every k-th image row of the
@@ -188,6 +204,7 @@ def main():
     achieved = alg_flops / (avg_ms * 1e-3) / 1e12
     exe_achieved = exe_flops / (avg_ms * 1e-3) / 1e12
     peak = PEAK_FP32_TFLOPS if prec == rtw.RTW_F32 else PEAK_FP64_TFLOPS
+    traffic = pmc_traffic(f"book1_simple_{W}x{H}_{SPP}spp_depth{DEPTH}", a.precision, int(st.kernel))
     out = {
         "metric": "Msamples/s (pixels x spp) on Book-1 final scene",
         "value": round(value, 3),
@@ -208,7 +225,9 @@ def main():
                    "accel": accel if accel != "bvh" else f"bvh{int(st.bvh_width)}",
                    "chunk": int(st.chunk)},
         "roofline": {"bound": "valu", "achieved": round(achieved, 3), "peak": peak,
-                     "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": None,
+                     "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
+                     "traffic": traffic["bytes_per_launch"] if traffic else None,
+                     "traffic_source": traffic["source"] if traffic else None,
                      "kernel": f"render_kernel<{a.precision}, {KERNEL_NAMES.get(int(st.kernel), st.kernel)}>",
                      "kernel_ms_avg": round(avg_ms, 3),
                      "flops_per_launch": int(alg_flops),
