@@ -53,6 +53,8 @@ class _Scene(C.Structure):
         ("n_planes", C.c_uint32), ("planes", _f64p), ("plane_mat", _u32p),
         ("n_materials", C.c_uint32), ("mat_type", _u32p), ("mat_params", _f64p),
         ("n_lights", C.c_uint32), ("lights", _f64p),
+        ("n_quads", C.c_uint32), ("quads", _f64p), ("quad_mat", _u32p),
+        ("n_light_quads", C.c_uint32), ("light_quads", _f64p), ("light_kinds", _u32p),
     ]
 
 
@@ -71,6 +73,10 @@ class Scene:
     mat_type: np.ndarray     # (k,) uint32
     mat_params: np.ndarray   # (k, 5) albedo rgb, fuzz, ior
     lights: np.ndarray       # (l, 4)
+    quads: np.ndarray = None         # (q, 9) Q, u, v
+    quad_mat: np.ndarray = None      # (q,) uint32
+    light_quads: np.ndarray = None   # (lq, 9)
+    light_kinds: np.ndarray = None   # (l + lq,) 0 sphere / 1 quad, list order; None = spheres first
 
 
 _lib = None
@@ -124,6 +130,11 @@ def lib():
         L.rtwo_cosine_hemisphere.argtypes = [_u64p, _f64p]
         L.rtwo_sphere_random.argtypes = [_f64p, _f64p, _u64p, _f64p]
         L.rtwo_bvh_stats.argtypes = [C.POINTER(_Scene), _u32p, _u32p, _u32p]
+        L.rtwo_quad_hit.argtypes = [_f64p, _f64p, _f64p, C.c_double, C.c_double, _f64p]
+        L.rtwo_quad_pdf_value.argtypes = [_f64p, _f64p, _f64p]
+        L.rtwo_quad_pdf_value.restype = C.c_double
+        L.rtwo_quad_random.argtypes = [_f64p, _f64p, _u64p, _f64p]
+        L.rtwo_quad_aabb.argtypes = [_f64p, _f64p]
         _lib = L
     return _lib
 
@@ -223,10 +234,16 @@ def _scene_struct(sc: Scene):
         keep.append(a)
         return _p(a, _u32p)
 
+    quads = np.zeros((0, 9)) if sc.quads is None else sc.quads
+    qmat = np.zeros(0, np.uint32) if sc.quad_mat is None else sc.quad_mat
+    lq = np.zeros((0, 9)) if sc.light_quads is None else sc.light_quads
     s = _Scene(len(sc.sphere_mat), f(sc.spheres, 4), u(sc.sphere_mat),
                len(sc.plane_mat), f(sc.planes, 6), u(sc.plane_mat),
                len(sc.mat_type), u(sc.mat_type), f(sc.mat_params, 5),
-               len(np.asarray(sc.lights).reshape(-1, 4)), f(sc.lights, 4))
+               len(np.asarray(sc.lights).reshape(-1, 4)), f(sc.lights, 4),
+               len(np.asarray(qmat).reshape(-1)), f(quads, 9), u(qmat),
+               len(np.asarray(lq).reshape(-1, 9)), f(lq, 9),
+               None if sc.light_kinds is None else u(sc.light_kinds))
     return s, keep
 
 
@@ -289,3 +306,27 @@ class Rng:
 
     def index(self, n):
         return lib().rtwo_rand_index(self.st, n)
+
+
+# ---- Quad (quadrilateral.rs) KAT entry points
+def quad_hit(quad, o, d, tmin=2.220446049250313e-16, tmax=float("inf")):
+    """(t, alpha, beta, normal[3]) or None."""
+    out = (C.c_double * 6)()
+    hit = lib().rtwo_quad_hit(arr(quad, 9), arr(o), arr(d), tmin, tmax, out)
+    return (out[0], out[1], out[2], tuple(out[3:6])) if hit else None
+
+
+def quad_pdf_value(quad, o, d):
+    return lib().rtwo_quad_pdf_value(arr(quad, 9), arr(o), arr(d))
+
+
+def quad_random(quad, o, rng: "Rng"):
+    out = (C.c_double * 3)()
+    lib().rtwo_quad_random(arr(quad, 9), arr(o), rng.st, out)
+    return tuple(out)
+
+
+def quad_aabb(quad):
+    out = (C.c_double * 6)()
+    lib().rtwo_quad_aabb(arr(quad, 9), out)
+    return tuple(out[:3]), tuple(out[3:])

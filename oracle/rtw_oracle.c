@@ -354,6 +354,93 @@ static void aabb_enclose(aabb *a, const aabb *b) {
     }
 }
 
+/* ------------------------------------------------------------------------ */
+/* Quad (quadrilateral.rs)                                                  */
+/* ------------------------------------------------------------------------ */
+typedef struct { v3 q, u, v, w, normal; double area; aabb box; } rquad;
+
+/* Quad::new, quadrilateral.rs:37-56 */
+static rquad quad_new(const double *p) {
+    rquad Q;
+    Q.q = ld(p);
+    Q.u = ld(p + 3);
+    Q.v = ld(p + 6);
+    /* AABBox::from_points([q + (u + v) * 0.5, q, q + v, q + u, q + u + v]):
+     * the first point, then enclose (with pad_to_minimum) each of the rest */
+    v3 pts[5] = {add(Q.q, muls(add(Q.u, Q.v), 0.5)), Q.q, add(Q.q, Q.v), add(Q.q, Q.u),
+                 add(add(Q.q, Q.u), Q.v)};
+    Q.box.mn[0] = Q.box.mx[0] = pts[0].x;
+    Q.box.mn[1] = Q.box.mx[1] = pts[0].y;
+    Q.box.mn[2] = Q.box.mx[2] = pts[0].z;
+    for (int i = 1; i < 5; ++i) {
+        aabb pb = {{pts[i].x, pts[i].y, pts[i].z}, {pts[i].x, pts[i].y, pts[i].z}};
+        aabb_enclose(&Q.box, &pb);
+    }
+    v3 n = cross(Q.u, Q.v);
+    Q.w = divs(n, dot(n, n));                  /* normal / normal.square_length() */
+    Q.area = length(n);
+    Q.normal = divs(n, Q.area);
+    return Q;
+}
+
+/* Quad::hit, quadrilateral.rs:79-100 (+ get_quad_uv :58-63) */
+static inline int quad_hit_t(const rquad *Q, v3 o, v3 d, double tmin, double tmax, double *t) {
+    double denom = dot(d, Q->normal);
+    if (!(fabs(denom) > DBL_EPSILON)) return 0;
+    double tt = -(dot(sub(o, Q->q), Q->normal) / denom);
+    if (!(tt >= tmin && tt <= tmax)) return 0;
+    v3 pq = sub(at(o, d, tt), Q->q);
+    double alpha = dot(cross(pq, Q->v), Q->w);
+    double beta = dot(cross(Q->u, pq), Q->w);
+    if (!(alpha >= 0.0 && alpha <= 1.0 && beta >= 0.0 && beta <= 1.0)) return 0;
+    *t = tt;
+    return 1;
+}
+
+/* Quad::pdf_value, quadrilateral.rs:102-112 */
+static double quad_pdf_value(const rquad *Q, v3 o, v3 d) {
+    double t;
+    if (!quad_hit_t(Q, o, d, 0.0, INFINITY, &t)) return 0.0;
+    v3 n = dot(d, Q->normal) < 0.0 ? Q->normal : neg(Q->normal);   /* HitRecord::new */
+    double distance_squared = t * t * dot(d, d);
+    double cosine = fabs(dot(d, n) / length(d));
+    return distance_squared / (cosine * Q->area);
+}
+
+/* Quad::random, quadrilateral.rs:114-118 */
+static v3 quad_random(const rquad *Q, v3 o, uint64_t st[4]) {
+    double r1 = rtwo_rand_open01(st);
+    double r2 = rtwo_rand_open01(st);
+    v3 p = add(add(Q->q, muls(Q->u, r1)), muls(Q->v, r2));
+    return sub(p, o);
+}
+
+int rtwo_quad_hit(const double quad[9], const double o[3], const double d[3],
+                  double tmin, double tmax, double out[6]) {
+    rquad Q = quad_new(quad);
+    double t;
+    if (!quad_hit_t(&Q, ld(o), ld(d), tmin, tmax, &t)) return 0;
+    v3 pq = sub(at(ld(o), ld(d), t), Q.q);
+    out[0] = t;
+    out[1] = dot(cross(pq, Q.v), Q.w);
+    out[2] = dot(cross(Q.u, pq), Q.w);
+    st3(out + 3, dot(ld(d), Q.normal) < 0.0 ? Q.normal : neg(Q.normal));
+    return 1;
+}
+double rtwo_quad_pdf_value(const double quad[9], const double o[3], const double d[3]) {
+    rquad Q = quad_new(quad);
+    return quad_pdf_value(&Q, ld(o), ld(d));
+}
+void rtwo_quad_random(const double quad[9], const double o[3], uint64_t st[4], double out[3]) {
+    rquad Q = quad_new(quad);
+    st3(out, quad_random(&Q, ld(o), st));
+}
+void rtwo_quad_aabb(const double quad[9], double box[6]) {
+    rquad Q = quad_new(quad);
+    memcpy(box, Q.box.mn, 24);
+    memcpy(box + 3, Q.box.mx, 24);
+}
+
 /* Sphere::pdf_value, sphere.rs:101-111 */
 static inline double sphere_pdf_value(v3 c, double radius, v3 o, v3 d) {
     double t;
@@ -404,14 +491,15 @@ void rtwo_refract(const double v[3], const double n[3], double eta, double out[3
 /* ------------------------------------------------------------------------ */
 /* Reference BVH restatement (bvh.rs:106-188; hittable_list.rs:270-406)     */
 /* ------------------------------------------------------------------------ */
-/* Object ids: 0..n_planes-1 = planes, n_planes.. = spheres (two "type      */
-/* groups", as the TypeId-sorted RawHittableVecs of a HittableList).        */
+/* Object ids: planes, quads, spheres (three "type groups", as the          */
+/* TypeId-sorted RawHittableVecs of a HittableList).                        */
+#define NG 3
 typedef struct {
     int leaf;
     int left, right;            /* node children */
     /* leaf: up to two groups, each a list of object ids */
-    int group_start[2], group_len[2];
-    aabb group_box[2];
+    int group_start[NG], group_len[NG];
+    aabb group_box[NG];
     aabb box;                   /* leaf: HittableList.aabbox; node: cached enclose */
 } bvh_node;
 
@@ -426,8 +514,15 @@ typedef struct {
     int max_depth;
 } bvh_t;
 
+/* object ids: [0, n_planes) planes, then n_quads quads, then the spheres */
+static inline int sphere_base(const rtwo_scene *sc) { return (int)(sc->n_planes + sc->n_quads); }
+
 static aabb object_box(const rtwo_scene *sc, int id) {
     aabb b;
+    if (id >= (int)sc->n_planes && id < sphere_base(sc)) {
+        rquad Q = quad_new(sc->quads + 9 * (id - (int)sc->n_planes));
+        return Q.box;
+    }
     if (id < (int)sc->n_planes) {
         /* Plane::get_aabbox, plane.rs:218-242 */
         const double *n = sc->planes + 6 * id + 3;
@@ -440,7 +535,7 @@ static aabb object_box(const rtwo_scene *sc, int id) {
         b.mn[2] = flat_z ? 0.0 : -INFINITY; b.mx[2] = flat_z ? 0.0 : INFINITY;
     } else {
         /* Sphere::new aabox, sphere.rs:42-45 */
-        const double *s = sc->spheres + 4 * (id - (int)sc->n_planes);
+        const double *s = sc->spheres + 4 * (id - sphere_base(sc));
         for (int k = 0; k < 3; ++k) { b.mn[k] = s[k] - s[3]; b.mx[k] = s[k] + s[3]; }
     }
     return b;
@@ -457,9 +552,9 @@ static int new_node(bvh_t *t) {
 
 /* A HittableList being split: its two type groups (planes, spheres), each an
  * ordered list of ids in the group's Vec order. */
-typedef struct { int *ids[2]; int len[2]; } hlist;
+typedef struct { int *ids[NG]; int len[NG]; } hlist;
 
-static int hl_len(const hlist *h) { return h->len[0] + h->len[1]; }
+static int hl_len(const hlist *h) { return h->len[0] + h->len[1] + h->len[2]; }
 
 static aabb group_box(const bvh_t *t, const int *ids, int len) {
     /* Slice::get_aabbox: reduce(|acc, e| acc.enclose(e)) (utils.rs:152-158) */
@@ -491,7 +586,7 @@ static int build(bvh_t *t, hlist *h, int depth) {
         bvh_node *nd = &t->nodes[node];
         nd->leaf = 1;
         int have = 0;
-        for (int g = 0; g < 2; ++g) {
+        for (int g = 0; g < NG; ++g) {
             nd->group_start[g] = t->n_ids;
             nd->group_len[g] = h->len[g];
             if (h->len[g]) {
@@ -511,7 +606,7 @@ static int build(bvh_t *t, hlist *h, int depth) {
     range_t *tmp = (range_t *)malloc(sizeof(range_t) * len);
     for (int axis = 0; axis < 3; ++axis) {
         int m = 0;
-        for (int g = 0; g < 2; ++g)
+        for (int g = 0; g < NG; ++g)
             for (int k = 0; k < h->len[g]; ++k) {
                 aabb b = t->obj_box[h->ids[g][k]];
                 tmp[m].s = b.mn[axis]; tmp[m].e = b.mx[axis]; ++m;
@@ -531,11 +626,11 @@ static int build(bvh_t *t, hlist *h, int depth) {
      * start > coord goes "right"; best_split hands back (right, left). */
     hlist parts[2];
     for (int p = 0; p < 2; ++p)
-        for (int g = 0; g < 2; ++g) {
+        for (int g = 0; g < NG; ++g) {
             parts[p].ids[g] = (int *)malloc(sizeof(int) * (h->len[g] + 1));
             parts[p].len[g] = 0;
         }
-    for (int g = 0; g < 2; ++g)
+    for (int g = 0; g < NG; ++g)
         for (int k = h->len[g] - 1; k >= 0; --k) {
             int id = h->ids[g][k];
             int right = t->obj_box[id].mn[best_axis] > best_coord;
@@ -549,7 +644,7 @@ static int build(bvh_t *t, hlist *h, int depth) {
         bvh_node *nd = &t->nodes[node];
         nd->leaf = 1;
         int have = 0;
-        for (int g = 0; g < 2; ++g) {
+        for (int g = 0; g < NG; ++g) {
             nd->group_start[g] = t->n_ids;
             nd->group_len[g] = all->len[g];
             if (all->len[g]) {
@@ -573,27 +668,29 @@ static int build(bvh_t *t, hlist *h, int depth) {
         result = node;
     }
     for (int p = 0; p < 2; ++p)
-        for (int g = 0; g < 2; ++g) free(parts[p].ids[g]);
+        for (int g = 0; g < NG; ++g) free(parts[p].ids[g]);
     return result;
 }
 
 static void bvh_build(bvh_t *t, const rtwo_scene *sc) {
     memset(t, 0, sizeof(*t));
     t->sc = sc;
-    int n = (int)(sc->n_planes + sc->n_spheres);
+    int n = (int)(sc->n_planes + sc->n_quads + sc->n_spheres);
     t->obj_box = (aabb *)malloc(sizeof(aabb) * (n ? n : 1));
     t->obj_ids = (int *)malloc(sizeof(int) * (n ? n : 1));
     for (int i = 0; i < n; ++i) t->obj_box[i] = object_box(sc, i);
     hlist h;
     h.len[0] = (int)sc->n_planes;
-    h.len[1] = (int)sc->n_spheres;
-    h.ids[0] = (int *)malloc(sizeof(int) * (h.len[0] + 1));
-    h.ids[1] = (int *)malloc(sizeof(int) * (h.len[1] + 1));
-    for (int i = 0; i < h.len[0]; ++i) h.ids[0][i] = i;
-    for (int i = 0; i < h.len[1]; ++i) h.ids[1][i] = (int)sc->n_planes + i;
+    h.len[1] = (int)sc->n_quads;
+    h.len[2] = (int)sc->n_spheres;
+    int first = 0;
+    for (int g = 0; g < NG; ++g) {
+        h.ids[g] = (int *)malloc(sizeof(int) * (h.len[g] + 1));
+        for (int i = 0; i < h.len[g]; ++i) h.ids[g][i] = first + i;
+        first += h.len[g];
+    }
     t->root = build(t, &h, 1);
-    free(h.ids[0]);
-    free(h.ids[1]);
+    for (int g = 0; g < NG; ++g) free(h.ids[g]);
 }
 static void bvh_free(bvh_t *t) {
     free(t->obj_box);
@@ -617,7 +714,11 @@ static inline int object_hit_t(const rtwo_scene *sc, int id, v3 o, v3 d, double 
         const double *p = sc->planes + 6 * id;
         return plane_t(ld(p), ld(p + 3), o, d, tmin, tmax, t);
     }
-    const double *s = sc->spheres + 4 * (id - (int)sc->n_planes);
+    if (id < sphere_base(sc)) {
+        rquad Q = quad_new(sc->quads + 9 * (id - (int)sc->n_planes));
+        return quad_hit_t(&Q, o, d, tmin, tmax, t);
+    }
+    const double *s = sc->spheres + 4 * (id - sphere_base(sc));
     return sphere_t(ld(s), s[3], o, d, tmin, tmax, t);
 }
 
@@ -628,7 +729,7 @@ static cand bvh_hit(const bvh_t *t, int node, v3 o, v3 d, double tmin, double tm
     if (nd->leaf) {
         /* HittableList::hit (hittable_list.rs:395-406) over the type groups,
          * each group bounded_hit (group AABB) then Slice::hit (utils.rs:172-179) */
-        for (int g = 0; g < 2; ++g) {
+        for (int g = 0; g < NG; ++g) {
             if (!nd->group_len[g]) continue;
             if (!aabb_hit(&nd->group_box[g], o, d, tmin, tmax)) continue;
             for (int k = 0; k < nd->group_len[g]; ++k) {
@@ -697,12 +798,19 @@ static int world_hit(const ctx_t *cx, v3 o, v3 d, hitrec *rec) {
                 plane_t(ld(sc->planes + 6 * k), ld(sc->planes + 6 * k + 3), o, d, tmin, tmax, &t) &&
                 (best < 0 || t < bt)) { bt = t; best = (int)k; }
         }
+        for (uint32_t k = 0; k < sc->n_quads; ++k) {
+            /* a quad's AABB (points enclosed, thin axes padded) holds the quad */
+            rquad Q = quad_new(sc->quads + 9 * k);
+            double t;
+            if (aabb_hit(&Q.box, o, d, tmin, tmax) && quad_hit_t(&Q, o, d, tmin, tmax, &t) &&
+                (best < 0 || t < bt)) { bt = t; best = (int)(sc->n_planes + k); }
+        }
         for (uint32_t k = 0; k < sc->n_spheres; ++k) {
             const double *s = sc->spheres + 4 * k;
             double t;
             if (s[3] < 0.0) continue;
             if (sphere_t(ld(s), s[3], o, d, tmin, tmax, &t) && (best < 0 || t < bt)) {
-                bt = t; best = (int)(sc->n_planes + k);
+                bt = t; best = sphere_base(sc) + (int)k;
             }
         }
     } else {
@@ -713,31 +821,67 @@ static int world_hit(const ctx_t *cx, v3 o, v3 d, hitrec *rec) {
     if (best < 0) return 0;
     if (best < (int)sc->n_planes) {
         make_record(o, d, bt, ld(sc->planes + 6 * best + 3), sc->plane_mat[best], rec);
-    } else {
+    } else if (best < sphere_base(sc)) {
         uint32_t k = (uint32_t)best - sc->n_planes;
+        rquad Q = quad_new(sc->quads + 9 * k);
+        make_record(o, d, bt, Q.normal, sc->quad_mat[k], rec);
+    } else {
+        uint32_t k = (uint32_t)(best - sphere_base(sc));
         const double *s = sc->spheres + 4 * k;
         sphere_record(ld(s), s[3], o, d, bt, sc->sphere_mat[k], rec);
     }
     return 1;
 }
 
+/* The light list in list order: entry k is sphere light_index(k) or quad. */
+static inline uint32_t n_light_list(const rtwo_scene *sc) { return sc->n_lights + sc->n_light_quads; }
+static inline void light_entry(const rtwo_scene *sc, uint32_t k, int *is_quad, uint32_t *idx) {
+    if (!sc->light_kinds) {
+        *is_quad = k >= sc->n_lights;
+        *idx = *is_quad ? k - sc->n_lights : k;
+        return;
+    }
+    uint32_t ns = 0, nq = 0;
+    for (uint32_t i = 0; i < k; ++i) {
+        if (sc->light_kinds[i]) ++nq;
+        else ++ns;
+    }
+    *is_quad = sc->light_kinds[k] != 0;
+    *idx = *is_quad ? nq : ns;
+}
+
 /* HittableList::pdf_value, hittable_list.rs:408-412 */
 static double lights_pdf_value(const rtwo_scene *sc, v3 o, v3 d) {
     double acc = 0.0;
-    for (uint32_t k = 0; k < sc->n_lights; ++k) {
-        const double *s = sc->lights + 4 * k;
-        acc = acc + sphere_pdf_value(ld(s), s[3], o, d);
+    const uint32_t n = n_light_list(sc);
+    uint32_t ns = 0, nq = 0;
+    for (uint32_t k = 0; k < n; ++k) {
+        int is_quad = sc->light_kinds ? sc->light_kinds[k] != 0 : k >= sc->n_lights;
+        if (is_quad) {
+            rquad Q = quad_new(sc->light_quads + 9 * nq++);
+            acc = acc + quad_pdf_value(&Q, o, d);
+        } else {
+            const double *s = sc->lights + 4 * ns++;
+            acc = acc + sphere_pdf_value(ld(s), s[3], o, d);
+        }
     }
-    return acc / (double)sc->n_lights;
+    return acc / (double)n;
 }
 /* HittableList::random, hittable_list.rs:414-419: iter_hittable().choose(rng)
- * picks a light uniformly, then Sphere::random.  rand 0.8.6's
+ * picks a light uniformly, then its random().  rand 0.8.6's
  * IteratorRandom::choose reaches that uniform pick through a reservoir step
  * over the flat_map (an extra gen_index(1) draw, then gen_index(n)); the build
  * draws the uniform index directly with one gen_index(n). */
 static v3 lights_random(const rtwo_scene *sc, v3 o, uint64_t st[4]) {
-    const uint32_t pick = rtwo_rand_index(st, sc->n_lights);
-    const double *s = sc->lights + 4 * pick;
+    const uint32_t pick = rtwo_rand_index(st, n_light_list(sc));
+    int is_quad;
+    uint32_t idx;
+    light_entry(sc, pick, &is_quad, &idx);
+    if (is_quad) {
+        rquad Q = quad_new(sc->light_quads + 9 * idx);
+        return quad_random(&Q, o, st);
+    }
+    const double *s = sc->lights + 4 * idx;
     return sphere_random(ld(s), s[3], o, st);
 }
 
@@ -779,7 +923,9 @@ static v3 trace(const ctx_t *cx, uint32_t i, uint32_t j, uint32_t s, rtwo_stats 
             return add(mulv(mult, ld(c->background)), res);        /* :473-475 */
         const uint32_t m = rec.mat;
         const double *mp = sc->mat_params + 5 * m;
-        const v3 emitted = zero;                                    /* :480-482, material.rs:42-44 */
+        /* :480-482: DiffuseLight::emitted = its colour (material.rs:508-514);
+         * every other material emits black (material.rs:42-44) */
+        const v3 emitted = sc->mat_type[m] == RTWO_DIFFUSE_LIGHT ? ld(mp) : zero;
         switch (sc->mat_type[m]) {
         case RTWO_METAL: {                                          /* material.rs:407-421 */
             v3 refl = reflect(normalize(d), rec.normal);
@@ -823,7 +969,7 @@ static v3 trace(const ctx_t *cx, uint32_t i, uint32_t j, uint32_t s, rtwo_stats 
             o = rec.p; d = dir;
             break;
         }
-        default:                                                    /* Invisible: scatter None */
+        default:                      /* Invisible, DiffuseLight: scatter None (:484-486) */
             return add(mulv(mult, emitted), res);
         }
         depth -= 1;
@@ -896,7 +1042,7 @@ int rtwo_render(const rtwo_camera *cam, const rtwo_scene *sc, uint64_t seed,
                 uint32_t col_begin, uint32_t col_end,
                 double *out, rtwo_stats *stats) {
     if (!cam || !sc || !out) return -1;
-    if (has_lambertian(sc) && sc->n_lights == 0) return -1;
+    if (has_lambertian(sc) && n_light_list(sc) == 0) return -1;
     if (row_step == 0) row_step = 1;
     if (row_end > cam->image_height) row_end = cam->image_height;
     if (col_end > cam->image_width) col_end = cam->image_width;

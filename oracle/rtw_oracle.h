@@ -27,7 +27,7 @@ extern "C" {
 #endif
 
 /* Material type codes (material.rs:321-488). */
-enum { RTWO_LAMBERTIAN = 0, RTWO_METAL = 1, RTWO_DIELECTRIC = 2, RTWO_INVISIBLE = 3 };
+enum { RTWO_LAMBERTIAN = 0, RTWO_METAL = 1, RTWO_DIELECTRIC = 2, RTWO_INVISIBLE = 3, RTWO_DIFFUSE_LIGHT = 4 };
 
 /* World-acceleration choice for the closest-hit query.  All three return the
  * same closest hit (bvh.rs:164-188 keeps "min t over every primitive").
@@ -71,7 +71,16 @@ typedef struct rtwo_scene {
     const uint32_t *mat_type;   /* n */
     const double *mat_params;   /* n x {albedo r, g, b, fuzz, ior} */
     uint32_t n_lights;
-    const double *lights;       /* n x {cx, cy, cz, r}  (HittableList of Spheres) */
+    const double *lights;       /* n x {cx, cy, cz, r}  (the light list's Spheres) */
+    /* Quads (quadrilateral.rs): world quads and the light list's quads */
+    uint32_t n_quads;
+    const double *quads;        /* n x {Qx, Qy, Qz, ux, uy, uz, vx, vy, vz} */
+    const uint32_t *quad_mat;
+    uint32_t n_light_quads;
+    const double *light_quads;  /* n x 9, as quads */
+    /* light-list order: n_lights + n_light_quads kinds (0 sphere, 1 quad),
+     * each taking the next entry of its array; NULL = spheres then quads */
+    const uint32_t *light_kinds;
 } rtwo_scene;
 
 typedef struct rtwo_stats {
@@ -80,6 +89,17 @@ typedef struct rtwo_stats {
     uint64_t lambertian;        /* Scatter-branch bounces (light-list pdf loop) */
     uint64_t nan_samples;
 } rtwo_stats;
+
+/* Quad::hit (quadrilateral.rs:79-100) with Quad::new's derived fields
+ * (:37-56); out = {t, alpha, beta, normal xyz (front-face adjusted)}.
+ * Returns 1 on a hit. */
+int rtwo_quad_hit(const double quad[9], const double o[3], const double d[3],
+                  double tmin, double tmax, double out[6]);
+/* Quad::pdf_value / Quad::random (quadrilateral.rs:102-118) */
+double rtwo_quad_pdf_value(const double quad[9], const double o[3], const double d[3]);
+void rtwo_quad_random(const double quad[9], const double o[3], uint64_t st[4], double out[3]);
+/* Quad::new's AABBox::from_points (aabox.rs:199-211, padded per enclose) */
+void rtwo_quad_aabb(const double quad[9], double box[6]);
 
 /* CameraBuilder::build, camera.rs:114-218. Returns 0. */
 int rtwo_camera_build(const rtwo_camera_builder *b, rtwo_camera *out);

@@ -327,3 +327,85 @@ def test_golden_renders_reproduce():
         if rows is not None:
             img = img[rows[0]:rows[1], cols[0]:cols[1]]
         assert np.array_equal(np.nan_to_num(img, nan=-7), np.nan_to_num(data[name], nan=-7)), name
+
+
+# ---- Quad + DiffuseLight (quadrilateral.rs, material.rs:490-514)
+
+QUAD = (0.0, 0.0, 0.0, 2.0, 0.0, 0.0, 0.0, 0.0, 3.0)      # Q, u, v: the y = 0 plane, 2 x 3
+
+
+def test_quad_new_aabb_pads_the_flat_axis():
+    """Quad::new: AABBox::from_points([q + (u+v)/2, q, q+v, q+u, q+u+v]), each
+    enclose padding axes thinner than 1e-4 by 1e-4 (aabox.rs:129-149)."""
+    lo, hi = O.quad_aabb(QUAD)
+    assert lo == (0.0, -1e-4, 0.0) and hi == (2.0, 1e-4, 3.0)
+
+
+def test_quad_hit_is_two_sided_with_uv_and_front_face():
+    # normal = u x v / |u x v| = (0, -1, 0); from above the ray is a back hit
+    t, a, b, n = O.quad_hit(QUAD, (1.0, 1.0, 1.0), (0.0, -1.0, 0.0))
+    assert (t, a, b) == (1.0, 0.5, 1.0 / 3.0) and n == (-0.0, 1.0, -0.0)
+    t, a, b, n = O.quad_hit(QUAD, (1.0, -2.0, 1.5), (0.0, 1.0, 0.0))
+    assert (t, a, b) == (2.0, 0.5, 0.5) and n == (0.0, -1.0, 0.0)
+
+
+def test_quad_hit_uv_range_inclusive_and_parallel_miss():
+    assert O.quad_hit(QUAD, (2.0, 1.0, 3.0), (0.0, -1.0, 0.0))[1:3] == (1.0, 1.0)   # corner
+    assert O.quad_hit(QUAD, (0.0, 1.0, 0.0), (0.0, -1.0, 0.0))[1:3] == (0.0, 0.0)
+    assert O.quad_hit(QUAD, (2.5, 1.0, 1.0), (0.0, -1.0, 0.0)) is None            # alpha > 1
+    assert O.quad_hit(QUAD, (1.0, 1.0, 1.0), (1.0, 0.0, 0.0)) is None             # |d.n| <= EPS
+    assert O.quad_hit(QUAD, (1.0, 1.0, 1.0), (0.0, -1.0, 0.0), tmax=0.5) is None  # t outside range
+
+
+def test_quad_pdf_is_distance_squared_over_cosine_area():
+    o, d = (0.0, 4.0, 0.0), (1.0, -2.0, 1.5)            # hits (2, 0, 3)... at t = 2 -> (2, 0, 3)
+    t, _, _, _ = O.quad_hit(QUAD, o, d, 0.0)
+    assert t == 2.0
+    d2 = t * t * (1 + 4 + 2.25)
+    cosine = abs(-2.0) / math.sqrt(1 + 4 + 2.25)
+    assert O.quad_pdf_value(QUAD, o, d) == pytest.approx(d2 / (cosine * 6.0), rel=1e-15)
+    assert O.quad_pdf_value(QUAD, o, (0.0, 1.0, 0.0)) == 0.0
+
+
+def test_quad_random_is_q_plus_open01_u_and_v():
+    r1, r2 = O.Rng(5, 6, 7), O.Rng(5, 6, 7)
+    o = (0.5, 1.0, -2.0)
+    x = O.quad_random(QUAD, o, r1)
+    a, b = r2.open01(), r2.open01()                      # u's draw first (quadrilateral.rs:115-116)
+    assert x == (2.0 * a - 0.5, -1.0, 3.0 * b + 2.0)
+
+
+def _quad_scene(light_rgb=(4.0, 2.0, 1.0)):
+    """A DiffuseLight quad facing a camera, nothing else."""
+    return O.Scene(np.zeros((0, 4)), np.zeros(0, np.uint32), np.zeros((0, 6)), np.zeros(0, np.uint32),
+                   np.array([4], np.uint32), np.array([[*light_rgb, 0.0, 0.0]]), np.zeros((0, 4)),
+                   quads=np.array([[-5.0, -5.0, -3.0, 10.0, 0.0, 0.0, 0.0, 10.0, 0.0]]),
+                   quad_mat=np.array([0], np.uint32))
+
+
+def test_diffuse_light_emits_its_colour_and_stops():
+    """scatter() is None for DiffuseLight: the sample is mult * emitted + res
+    with mult = 1 (camera.rs:484-486) -- exactly the light's colour."""
+    cam = O.camera_build(image_width=4, image_height=3, samples_per_pixel=5, max_depth=10,
+                         background=(0.0, 0.0, 0.0))
+    img, st = O.render(cam, _quad_scene(), 3)
+    np.testing.assert_array_equal(img, np.broadcast_to([20.0, 10.0, 5.0], img.shape))
+    assert st.segments == 4 * 3 * 5 and st.lambertian == 0
+
+
+def test_quad_world_bvh_variants_equal_brute_force():
+    """Quads join the BVH as a third type group; closest hit must not change."""
+    rng = np.random.default_rng(2)
+    quads = np.concatenate([rng.uniform(-3, 3, (20, 3)), rng.uniform(-1, 1, (20, 6))], axis=1)
+    sph = np.concatenate([rng.uniform(-3, 3, (30, 3)), rng.uniform(0.1, 0.5, (30, 1))], axis=1)
+    mats = np.array([0, 1, 2, 4], np.uint32)
+    mp = np.array([[0.6, 0.5, 0.4, 0, 0], [0.8, 0.8, 0.8, 0.2, 0], [1, 1, 1, 0, 1.5], [3, 3, 3, 0, 0]])
+    sc = O.Scene(sph, rng.integers(0, 4, 30).astype(np.uint32), np.zeros((0, 6)), np.zeros(0, np.uint32),
+                 mats, mp, np.array([[0.0, 4.0, 0.0, 1.0]]), quads=quads,
+                 quad_mat=rng.integers(0, 4, 20).astype(np.uint32),
+                 light_quads=quads[:2], light_kinds=np.array([1, 0, 1], np.uint32))
+    cam = O.camera_build(image_width=16, image_height=12, samples_per_pixel=3, max_depth=20,
+                         lookfrom=(0.0, 2.0, 9.0), lookat=(0.0, 0.0, 0.0), background=(0.5, 0.6, 0.7))
+    imgs = [O.render(cam, sc, 9, accel=a)[0] for a in (O.ACCEL_BRUTE, O.ACCEL_BVH_REF, O.ACCEL_BVH_CACHED)]
+    for im in imgs[1:]:
+        np.testing.assert_array_equal(np.nan_to_num(im, nan=-7), np.nan_to_num(imgs[0], nan=-7))
