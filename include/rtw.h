@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define RTW_ABI_VERSION 2
+#define RTW_ABI_VERSION 3
 
 /* error codes */
 #define RTW_OK 0
@@ -55,6 +55,7 @@ extern "C" {
 #define RTW_METAL 1              /* material.rs:378-421 */
 #define RTW_DIELECTRIC 2         /* material.rs:423-488 ("Dialectric") */
 #define RTW_INVISIBLE 3          /* material.rs:321-325 */
+#define RTW_DIFFUSE_LIGHT 4      /* material.rs:490-514: emits albedo, scatter() None */
 
 /* World acceleration used by the render kernel */
 #define RTW_ACCEL_AUTO 0         /* pick per scene */
@@ -95,10 +96,20 @@ typedef struct rtw_scene {
     const double *planes;         /* n_planes x {px, py, pz, nx, ny, nz}, unit normal */
     const uint32_t *plane_mat;
     uint32_t n_materials;
-    const uint32_t *mat_type;     /* RTW_LAMBERTIAN ... RTW_INVISIBLE */
+    const uint32_t *mat_type;     /* RTW_LAMBERTIAN ... RTW_DIFFUSE_LIGHT */
     const double *mat_params;     /* n_materials x {albedo r, g, b, fuzz, ior} */
     uint32_t n_lights;
-    const double *lights;         /* n_lights x {cx, cy, cz, radius} */
+    const double *lights;         /* n_lights x {cx, cy, cz, radius}: the light list's spheres */
+    /* Quads (quadrilateral.rs:21-56): Quad::new(Q, u, v, mat) */
+    uint32_t n_quads;
+    const double *quads;          /* n_quads x {Qx, Qy, Qz, ux, uy, uz, vx, vy, vz} */
+    const uint32_t *quad_mat;
+    uint32_t n_light_quads;
+    const double *light_quads;    /* the light list's quads, n x 9 as quads */
+    /* light-list order (HittableList insertion order, hittable_list.rs:408-419):
+     * n_lights + n_light_quads kinds, 0 = next sphere, 1 = next quad;
+     * NULL = all spheres, then all quads */
+    const uint32_t *light_kinds;
 } rtw_scene;
 
 typedef struct rtw_stats {

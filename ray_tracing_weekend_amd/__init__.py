@@ -22,7 +22,7 @@ import numpy as np
 
 from . import _capi
 from ._capi import (RTW_ACCEL_AUTO, RTW_ACCEL_BRUTE, RTW_ACCEL_BVH, RTW_DIELECTRIC, RTW_F32,
-                    RTW_F64, RTW_INVISIBLE, RTW_LAMBERTIAN, RTW_METAL)
+                    RTW_F64, RTW_INVISIBLE, RTW_LAMBERTIAN, RTW_METAL, RTW_DIFFUSE_LIGHT)
 
 __all__ = [
     "Material", "Lambertian", "Metal", "Dialectric", "INVISIBLE", "Sphere", "Plane",
@@ -63,6 +63,10 @@ def Dialectric(index_of_refraction):         # material.rs:423-455
 INVISIBLE = Material(RTW_INVISIBLE)          # material.rs:321-325
 
 
+def DiffuseLight(colour):                    # material.rs:490-514 (new_with_colour)
+    return Material(RTW_DIFFUSE_LIGHT, tuple(map(float, colour)))
+
+
 @dataclass(frozen=True)
 class Sphere:                                # entities/sphere.rs:24-47
     center: tuple
@@ -82,13 +86,23 @@ class Plane:                                 # entities/plane.rs:20-38 (normal n
         object.__setattr__(self, "normal", (n[0] / ln, n[1] / ln, n[2] / ln))
 
 
+@dataclass(frozen=True)
+class Quad:                                  # entities/quadrilateral.rs:21-56 (Quad::new(Q, u, v, mat))
+    q: tuple
+    u: tuple
+    v: tuple
+    mat: Material = INVISIBLE
+
+
 class HittableList:                          # hittable_collections/hittable_list.rs:247-294
     def __init__(self, objects=()):
-        self.objects = list(objects)
+        self.objects = []
+        for o in objects:
+            self.add(o)
 
     def add(self, obj):
-        if not isinstance(obj, (Sphere, Plane)):
-            raise TypeError("only Sphere and Plane are in this build's scope")
+        if not isinstance(obj, (Sphere, Plane, Quad)):
+            raise TypeError("only Sphere, Plane and Quad are in this build's scope")
         self.objects.append(obj)
 
     def __len__(self):
@@ -105,6 +119,10 @@ class SceneSoA:
     mat_type: np.ndarray = field(default_factory=lambda: np.zeros(0, np.uint32))
     mat_params: np.ndarray = field(default_factory=lambda: np.zeros((0, 5)))
     lights: np.ndarray = field(default_factory=lambda: np.zeros((0, 4)))
+    quads: np.ndarray = field(default_factory=lambda: np.zeros((0, 9)))
+    quad_mat: np.ndarray = field(default_factory=lambda: np.zeros(0, np.uint32))
+    light_quads: np.ndarray = field(default_factory=lambda: np.zeros((0, 9)))
+    light_kinds: np.ndarray = None          # list order: 0 sphere / 1 quad; None = spheres first
 
     def as_c(self):
         """(rtw_scene, keepalive) -- the struct points into these arrays."""
@@ -123,7 +141,10 @@ class SceneSoA:
         s = _capi.rtw_scene(len(self.sphere_mat), f(self.spheres, 4), u(self.sphere_mat),
                             len(self.plane_mat), f(self.planes, 6), u(self.plane_mat),
                             len(self.mat_type), u(self.mat_type), f(self.mat_params, 5),
-                            len(np.asarray(self.lights).reshape(-1, 4)), f(self.lights, 4))
+                            len(np.asarray(self.lights).reshape(-1, 4)), f(self.lights, 4),
+                            len(self.quad_mat), f(self.quads, 9), u(self.quad_mat),
+                            len(np.asarray(self.light_quads).reshape(-1, 9)), f(self.light_quads, 9),
+                            None if self.light_kinds is None else u(self.light_kinds))
         return s, keep
 
     @staticmethod
@@ -137,14 +158,18 @@ class SceneSoA:
         return SceneSoA(f(s.spheres, s.n_spheres, 4), u(s.sphere_mat, s.n_spheres),
                         f(s.planes, s.n_planes, 6), u(s.plane_mat, s.n_planes),
                         u(s.mat_type, s.n_materials), f(s.mat_params, s.n_materials, 5),
-                        f(s.lights, s.n_lights, 4))
+                        f(s.lights, s.n_lights, 4), f(s.quads, s.n_quads, 9), u(s.quad_mat, s.n_quads),
+                        f(s.light_quads, s.n_light_quads, 9),
+                        u(s.light_kinds, s.n_lights + s.n_light_quads) if s.light_kinds else None)
 
 
 def flatten(world, lights) -> SceneSoA:
-    """world: HittableList or SceneSoA; lights: HittableList of Spheres."""
+    """world: HittableList or SceneSoA; lights: HittableList of Spheres and
+    Quads (their list order is kept: it is the light pdf's sum order and the
+    uniform pick's index)."""
     if isinstance(world, SceneSoA):
         return world
-    mats, mtypes, sph, smat, pl, pmat = [], [], [], [], [], []
+    mats, mtypes, sph, smat, pl, pmat, qd, qmat = [], [], [], [], [], [], [], []
 
     def push(m: Material):
         mtypes.append(m.type)
@@ -156,18 +181,29 @@ def flatten(world, lights) -> SceneSoA:
             pl.append(list(o.point) + list(o.normal))
             pmat.append(push(o.mat))
     for o in world.objects:
+        if isinstance(o, Quad):
+            qd.append(list(o.q) + list(o.u) + list(o.v))
+            qmat.append(push(o.mat))
+    for o in world.objects:
         if isinstance(o, Sphere):
             sph.append(list(o.center) + [o.radius])
             smat.append(push(o.mat))
-    li = []
+    li, lq, kinds = [], [], []
     for o in lights.objects:
-        if not isinstance(o, Sphere):
-            raise RenderError(_capi.RTW_E_UNSUPPORTED, "only spheres can be lights in this build")
-        li.append(list(o.center) + [o.radius])
+        if isinstance(o, Sphere):
+            li.append(list(o.center) + [o.radius])
+            kinds.append(0)
+        elif isinstance(o, Quad):
+            lq.append(list(o.q) + list(o.u) + list(o.v))
+            kinds.append(1)
+        else:
+            raise RenderError(_capi.RTW_E_UNSUPPORTED, "lights must be spheres or quads in this build")
     return SceneSoA(np.array(sph, np.float64).reshape(-1, 4), np.array(smat, np.uint32),
                     np.array(pl, np.float64).reshape(-1, 6), np.array(pmat, np.uint32),
                     np.array(mtypes, np.uint32), np.array(mats, np.float64).reshape(-1, 5),
-                    np.array(li, np.float64).reshape(-1, 4))
+                    np.array(li, np.float64).reshape(-1, 4), np.array(qd, np.float64).reshape(-1, 9),
+                    np.array(qmat, np.uint32), np.array(lq, np.float64).reshape(-1, 9),
+                    np.array(kinds, np.uint32) if lq else None)
 
 
 # ---------------------------------------------------------------- camera

@@ -18,7 +18,7 @@ LIB_PATH = os.environ.get("RTW_LIB_OVERRIDE", LIB_PATH)
 RTW_OK = 0
 RTW_E_INVALID, RTW_E_DEVICE, RTW_E_NO_LIGHTS, RTW_E_NO_SCENE, RTW_E_UNSUPPORTED = -1, -2, -3, -4, -5
 RTW_F32, RTW_F64 = 0, 1
-RTW_LAMBERTIAN, RTW_METAL, RTW_DIELECTRIC, RTW_INVISIBLE = 0, 1, 2, 3
+RTW_LAMBERTIAN, RTW_METAL, RTW_DIELECTRIC, RTW_INVISIBLE, RTW_DIFFUSE_LIGHT = 0, 1, 2, 3, 4
 RTW_ACCEL_AUTO, RTW_ACCEL_BRUTE, RTW_ACCEL_BVH = 0, 1, 2
 
 _f64p = C.POINTER(C.c_double)
@@ -54,10 +54,12 @@ class rtw_scene(C.Structure):
         ("n_planes", C.c_uint32), ("planes", _f64p), ("plane_mat", _u32p),
         ("n_materials", C.c_uint32), ("mat_type", _u32p), ("mat_params", _f64p),
         ("n_lights", C.c_uint32), ("lights", _f64p),
+        ("n_quads", C.c_uint32), ("quads", _f64p), ("quad_mat", _u32p),
+        ("n_light_quads", C.c_uint32), ("light_quads", _f64p), ("light_kinds", _u32p),
     ]
 
 
-ABI_VERSION = 2     # RTW_ABI_VERSION of include/rtw.h
+ABI_VERSION = 3     # RTW_ABI_VERSION of include/rtw.h
 
 
 class rtw_stats(C.Structure):

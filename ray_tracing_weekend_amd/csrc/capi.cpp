@@ -82,6 +82,49 @@ int hip_fail(rtw_ctx* c, hipError_t e, const char* what) {
 
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
+// Quad::new (quadrilateral.rs:37-56) in f64, in the oracle's operation order
+// (rtw_oracle.c quad_new): out = {Q, u, v, w, normal, area, box lo, box hi}.
+void quad_derive(const double* p, double* out) {
+    const double q[3] = {p[0], p[1], p[2]}, u[3] = {p[3], p[4], p[5]}, v[3] = {p[6], p[7], p[8]};
+    // AABBox::from_points([q + (u + v) * 0.5, q, q + v, q + u, q + u + v]),
+    // each enclose followed by pad_to_minimum (aabox.rs:129-175)
+    double pts[5][3];
+    for (int a = 0; a < 3; ++a) {
+        pts[0][a] = q[a] + (u[a] + v[a]) * 0.5;
+        pts[1][a] = q[a];
+        pts[2][a] = q[a] + v[a];
+        pts[3][a] = q[a] + u[a];
+        pts[4][a] = (q[a] + u[a]) + v[a];
+    }
+    double mn[3], mx[3];
+    for (int a = 0; a < 3; ++a) mn[a] = mx[a] = pts[0][a];
+    for (int i = 1; i < 5; ++i) {
+        for (int a = 0; a < 3; ++a) {
+            mn[a] = fmin(mn[a], pts[i][a]);
+            mx[a] = fmax(mx[a], pts[i][a]);
+        }
+        for (int a = 0; a < 3; ++a)
+            if (mx[a] - mn[a] < 0.0001) {
+                mn[a] -= 0.0001;
+                mx[a] += 0.0001;
+            }
+    }
+    const double n[3] = {u[1] * v[2] - u[2] * v[1], u[2] * v[0] - u[0] * v[2], u[0] * v[1] - u[1] * v[0]};
+    const double n2 = n[0] * n[0] + n[1] * n[1] + n[2] * n[2];
+    const double area = sqrt(n2);
+    for (int a = 0; a < 3; ++a) {
+        out[a] = q[a];
+        out[3 + a] = u[a];
+        out[6 + a] = v[a];
+        out[9 + a] = n[a] / n2;
+        out[12 + a] = n[a] / area;
+        out[16 + a] = mn[a];
+        out[19 + a] = mx[a];
+    }
+    out[15] = area;
+    out[22] = out[23] = 0.0;
+}
+
 // Convert the caller's f64 SoA into the device layout of precision R, in one
 // host staging blob, and fill the DevScene pointers relative to `base`.
 template <typename R>
@@ -98,6 +141,11 @@ std::vector<unsigned char> stage_scene(const rtw_scene* s, rtw::DevScene<R>* ds,
     const size_t o_r = reserve(sizeof(R) * s->n_spheres);
     const size_t o_smat = reserve(sizeof(uint32_t) * s->n_spheres);
     const size_t o_pl = reserve(sizeof(R) * 12 * s->n_planes);
+    const size_t o_quads = reserve(sizeof(R) * rtw::kQuadR * s->n_quads);
+    const size_t o_qmat = reserve(sizeof(uint32_t) * s->n_quads);
+    const size_t o_lquads = reserve(sizeof(R) * rtw::kQuadR * s->n_light_quads);
+    const uint32_t n_list = s->n_lights + s->n_light_quads;
+    const size_t o_lref = reserve(sizeof(uint32_t) * n_list);
     const size_t o_pmat = reserve(sizeof(uint32_t) * s->n_planes);
     const size_t o_mt = reserve(sizeof(uint32_t) * s->n_materials);
     const size_t o_mp = reserve(sizeof(R4) * s->n_materials);
@@ -153,6 +201,32 @@ std::vector<unsigned char> stage_scene(const rtw_scene* s, rtw::DevScene<R>* ds,
         for (int q = 0; q < 6; ++q) dst[6 + q] = (R)box[q];
     }
     for (uint32_t k = 0; k < s->n_planes; ++k) reinterpret_cast<uint32_t*>(b + o_pmat)[k] = s->plane_mat[k];
+    // quads: derived in f64; the AABB is rounded outward into R (a cull only)
+    auto put_quad = [&](const double* src, R* dst) {
+        double q[rtw::kQuadR];
+        quad_derive(src, q);
+        for (uint32_t a = 0; a < rtw::kQuadR; ++a) dst[a] = (R)q[a];
+        for (int a = 0; a < 3; ++a) {
+            R lo = (R)q[16 + a], hi = (R)q[19 + a];
+            if ((double)lo > q[16 + a]) lo = std::nextafter(lo, (R)-INFINITY);
+            if ((double)hi < q[19 + a]) hi = std::nextafter(hi, (R)INFINITY);
+            dst[16 + a] = lo;
+            dst[19 + a] = hi;
+        }
+    };
+    for (uint32_t k = 0; k < s->n_quads; ++k) {
+        put_quad(s->quads + 9 * k, reinterpret_cast<R*>(b + o_quads) + rtw::kQuadR * k);
+        reinterpret_cast<uint32_t*>(b + o_qmat)[k] = s->quad_mat[k];
+    }
+    for (uint32_t k = 0; k < s->n_light_quads; ++k)
+        put_quad(s->light_quads + 9 * k, reinterpret_cast<R*>(b + o_lquads) + rtw::kQuadR * k);
+    {
+        uint32_t ns = 0, nq = 0;
+        for (uint32_t k = 0; k < n_list; ++k) {
+            const bool quad = s->light_kinds ? s->light_kinds[k] != 0 : k >= s->n_lights;
+            reinterpret_cast<uint32_t*>(b + o_lref)[k] = quad ? (0x80000000u | nq++) : ns++;
+        }
+    }
     for (uint32_t k = 0; k < s->n_materials; ++k) {
         const double* m = s->mat_params + 5 * k;
         const uint32_t t = s->mat_type[k];
@@ -172,6 +246,13 @@ std::vector<unsigned char> stage_scene(const rtw_scene* s, rtw::DevScene<R>* ds,
     ds->mat_type = reinterpret_cast<const uint32_t*>(base + o_mt);
     ds->mat_p = reinterpret_cast<const R4*>(base + o_mp);
     ds->lights = reinterpret_cast<const R4*>(base + o_li);
+    ds->quads = reinterpret_cast<const R*>(base + o_quads);
+    ds->quad_mat = reinterpret_cast<const uint32_t*>(base + o_qmat);
+    ds->lquads = reinterpret_cast<const R*>(base + o_lquads);
+    ds->lref = s->n_light_quads ? reinterpret_cast<const uint32_t*>(base + o_lref) : nullptr;
+    ds->n_quads = s->n_quads;
+    ds->n_lquads = s->n_light_quads;
+    ds->n_list = n_list;
     // round box bounds outward into precision R
     auto down = [](double x) {
         R r = (R)x;
@@ -265,18 +346,26 @@ std::vector<unsigned char> stage_scene(const rtw_scene* s, rtw::DevScene<R>* ds,
 int validate_scene(rtw_ctx* c, const rtw_scene* s) {
     if (!s) return fail(c, RTW_E_INVALID, "scene is NULL");
     if ((s->n_spheres && (!s->spheres || !s->sphere_mat)) || (s->n_planes && (!s->planes || !s->plane_mat)) ||
-        (s->n_materials && (!s->mat_type || !s->mat_params)) || (s->n_lights && !s->lights))
+        (s->n_materials && (!s->mat_type || !s->mat_params)) || (s->n_lights && !s->lights) ||
+        (s->n_quads && (!s->quads || !s->quad_mat)) || (s->n_light_quads && !s->light_quads))
         return fail(c, RTW_E_INVALID, "scene array pointer is NULL");
+    if (s->light_kinds) {
+        uint32_t nq = 0;
+        for (uint32_t k = 0; k < s->n_lights + s->n_light_quads; ++k) nq += s->light_kinds[k] ? 1 : 0;
+        if (nq != s->n_light_quads) return fail(c, RTW_E_INVALID, "light_kinds does not match the light counts");
+    }
     bool lambertian = false;
     for (uint32_t k = 0; k < s->n_materials; ++k) {
-        if (s->mat_type[k] > RTW_INVISIBLE) return fail(c, RTW_E_INVALID, "unknown material type");
+        if (s->mat_type[k] > RTW_DIFFUSE_LIGHT) return fail(c, RTW_E_INVALID, "unknown material type");
         lambertian |= s->mat_type[k] == RTW_LAMBERTIAN;
     }
     for (uint32_t k = 0; k < s->n_spheres; ++k)
         if (s->sphere_mat[k] >= s->n_materials) return fail(c, RTW_E_INVALID, "sphere material id out of range");
     for (uint32_t k = 0; k < s->n_planes; ++k)
         if (s->plane_mat[k] >= s->n_materials) return fail(c, RTW_E_INVALID, "plane material id out of range");
-    if (lambertian && s->n_lights == 0)
+    for (uint32_t k = 0; k < s->n_quads; ++k)
+        if (s->quad_mat[k] >= s->n_materials) return fail(c, RTW_E_INVALID, "quad material id out of range");
+    if (lambertian && s->n_lights + s->n_light_quads == 0)
         return fail(c, RTW_E_NO_LIGHTS, "Lambertian material with an empty light list "
                                         "(the reference panics: HittableList shouldn't be empty)");
     return RTW_OK;
@@ -386,7 +475,8 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
         // the light pdf goes through the light BVH (same per-lane stack) for
         // longer light lists
         const uint32_t light_stack = p.sc.lbvh_depth + 1;
-        p.light_bvh = (p.sc.n_lights >= c->light_bvh_min && light_stack <= rtw::kBvhStack) ? 1u : 0u;
+        p.light_bvh = (p.sc.n_lights >= c->light_bvh_min && light_stack <= rtw::kBvhStack &&
+                       p.sc.n_lquads == 0) ? 1u : 0u;
         const uint32_t min_stack = p.light_bvh ? light_stack : 1u;
         // binary traversal pushes at most one entry per inner level
         const uint32_t bin_stack = std::max(p.sc.bvh_depth + 1, min_stack);
@@ -646,8 +736,10 @@ int rtw_set_scene(rtw_ctx* c, const rtw_scene* s) {
         fix(ds.sph); fix(ds.sph_r); fix(ds.sph_mat); fix(ds.planes); fix(ds.plane_mat);
         fix(ds.mat_type); fix(ds.mat_p); fix(ds.lights); fix(ds.bvh); fix(ds.bsph); fix(ds.bid);
         fix(ds.bvh4); fix(ds.lbvh); fix(ds.lsph); fix(ds.lid);
+        fix(ds.quads); fix(ds.quad_mat); fix(ds.lquads);
+        if (ds.lref) fix(ds.lref);
     };
-    static_assert(offsetof(rtw::DevScene<float>, n_sph) == 15 * sizeof(void*),
+    static_assert(offsetof(rtw::DevScene<float>, n_sph) == 19 * sizeof(void*),
                   "DevScene gained a pointer: update rebase");
     if (c->precision == RTW_F32) {
         rebase(tmp32);

@@ -77,6 +77,12 @@ rtw_scene FlatScene::view() const {
     s.mat_params = mat_params.data();
     s.n_lights = (uint32_t)(lights.size() / 4);
     s.lights = lights.data();
+    s.n_quads = (uint32_t)quad_mat.size();
+    s.quads = quads.data();
+    s.quad_mat = quad_mat.data();
+    s.n_light_quads = (uint32_t)(light_quads.size() / 9);
+    s.light_quads = light_quads.data();
+    s.light_kinds = light_kinds.empty() ? nullptr : light_kinds.data();
     return s;
 }
 
@@ -96,10 +102,24 @@ FlatScene flatten(const HittableList& world, const HittableList& lights) {
         f.spheres.insert(f.spheres.end(), {s.center.x, s.center.y, s.center.z, s.radius});
         f.sphere_mat.push_back(push_mat(s.mat));
     }
+    for (const Quad& q : world.quads()) {
+        f.quads.insert(f.quads.end(), {q.q.x, q.q.y, q.q.z, q.u.x, q.u.y, q.u.z, q.v.x, q.v.y, q.v.z});
+        f.quad_mat.push_back(push_mat(q.mat));
+    }
     if (!lights.planes().empty())
         throw Error(RTW_E_UNSUPPORTED, "planes as lights are outside this build's scope");
-    for (const Sphere& s : lights.spheres())
-        f.lights.insert(f.lights.end(), {s.center.x, s.center.y, s.center.z, s.radius});
+    for (const auto& e : lights.order()) {
+        if (e.first == HittableList::kSphere) {
+            const Sphere& s = lights.spheres()[e.second];
+            f.lights.insert(f.lights.end(), {s.center.x, s.center.y, s.center.z, s.radius});
+            f.light_kinds.push_back(0);
+        } else {
+            const Quad& q = lights.quads()[e.second];
+            f.light_quads.insert(f.light_quads.end(),
+                                 {q.q.x, q.q.y, q.q.z, q.u.x, q.u.y, q.u.z, q.v.x, q.v.y, q.v.z});
+            f.light_kinds.push_back(1);
+        }
+    }
     return f;
 }
 

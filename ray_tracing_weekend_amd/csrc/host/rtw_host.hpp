@@ -20,6 +20,7 @@
 #include <stdexcept>
 #include <string>
 #include <tuple>
+#include <utility>
 #include <vector>
 
 #include "../../../include/rtw.h"
@@ -44,6 +45,7 @@ struct Material {
     static Material metal(Colour albedo, double fuzz) { return {RTW_METAL, albedo, fuzz, 0.0}; }
     static Material dialectric(double ior) { return {RTW_DIELECTRIC, {1, 1, 1}, 0.0, ior}; }
     static Material invisible() { return {RTW_INVISIBLE, {0, 0, 0}, 0.0, 0.0}; }
+    static Material diffuse_light(Colour emit) { return {RTW_DIFFUSE_LIGHT, emit, 0.0, 0.0}; }
 };
 
 struct Sphere {
@@ -59,31 +61,45 @@ struct Plane {
     Plane(Point3 p, Vec3 n, Material m);
 };
 
-// A world or light list.  Only the primitives of the reference's hot path
-// (Sphere, Plane) are representable; Quad/Triangle/Cuboid/Transformed are
-// outside this build's scope.
+// Quad::new(Q, u, v, mat), quadrilateral.rs:37-56
+struct Quad {
+    Point3 q;
+    Vec3 u, v;
+    Material mat;
+};
+
+// A world or light list.  The primitives this build renders: Sphere, Plane,
+// Quad (Triangle/Cuboid/Transformed are SURVEY.md §8f rank 4).  Insertion
+// order is kept: it is the light list's order (pdf sum, uniform pick).
 class HittableList {
    public:
-    void add(const Sphere& s) { spheres_.push_back(s); }
-    void add(const Plane& p) { planes_.push_back(p); }
-    size_t len() const { return spheres_.size() + planes_.size(); }
+    enum Kind : uint8_t { kSphere, kPlane, kQuad };
+    void add(const Sphere& s) { order_.push_back({kSphere, spheres_.size()}); spheres_.push_back(s); }
+    void add(const Plane& p) { order_.push_back({kPlane, planes_.size()}); planes_.push_back(p); }
+    void add(const Quad& q) { order_.push_back({kQuad, quads_.size()}); quads_.push_back(q); }
+    size_t len() const { return order_.size(); }
     bool is_empty() const { return len() == 0; }
     const std::vector<Sphere>& spheres() const { return spheres_; }
     const std::vector<Plane>& planes() const { return planes_; }
+    const std::vector<Quad>& quads() const { return quads_; }
+    const std::vector<std::pair<Kind, size_t>>& order() const { return order_; }
 
    private:
     std::vector<Sphere> spheres_;
     std::vector<Plane> planes_;
+    std::vector<Quad> quads_;
+    std::vector<std::pair<Kind, size_t>> order_;
 };
 
 // Flattened (SoA) world + lights; owns the arrays an rtw_scene points into.
 struct FlatScene {
-    std::vector<double> spheres, planes, mat_params, lights;
-    std::vector<uint32_t> sphere_mat, plane_mat, mat_type;
+    std::vector<double> spheres, planes, quads, mat_params, lights, light_quads;
+    std::vector<uint32_t> sphere_mat, plane_mat, quad_mat, mat_type, light_kinds;
     rtw_scene view() const;
 };
-// world's spheres/planes with one material record each; lights contribute
-// their sphere geometry only (their material is never consulted on the path).
+// world's spheres/planes/quads with one material record each; lights
+// contribute their geometry only, in list order (their material is never
+// consulted on the path).
 FlatScene flatten(const HittableList& world, const HittableList& lights);
 
 // SampledColour(sum, spp) -- colour.rs:136-148

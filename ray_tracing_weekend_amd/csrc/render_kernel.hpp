@@ -666,6 +666,25 @@ __device__ __forceinline__ double lights_pdf_bvh(const DevScene<double>& sc, V3<
     return acc;
 }
 
+// Light list with quads (DevScene::lref set): HittableList::pdf_value over
+// the mixed list in list order (hittable_list.rs:408-412), reference
+// arithmetic per entry; `li` = the sphere lights (LDS-staged or global).
+template <typename R>
+__device__ __forceinline__ R lights_pdf_mixed(const DevScene<R>& sc, const R4<R>* __restrict__ li, V3<R> o,
+                                              V3<R> d) {
+    R acc = (R)0;
+    for (uint32_t k = 0; k < sc.n_list; ++k) {
+        const uint32_t ref = sc.lref[k];
+        if (ref >> 31) {
+            acc = acc + quad_pdf_value(sc.lquads + kQuadR * (ref & 0x7fffffffu), o, d);
+        } else {
+            const R4<R> L = li[ref];
+            acc = acc + sphere_pdf_value(mk(L.x, L.y, L.z), L.w, o, d);
+        }
+    }
+    return acc;
+}
+
 // RTW_EXP (profiling builds only, tools/exp_cost.sh): repeat one part of the
 // per-segment work so that the time difference prices it.  1 = closest-hit
 // query, 2 = light pdf sum, 3 = stream seeding, 4 = Lambertian direction
@@ -746,6 +765,8 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? 5 : 1) render_kernel(
     const V3<R> zero = mk<R>(0, 0, 0);
     const R tmin = PR::kEps;
     const int32_t nplanes = (int32_t)p.sc.n_planes;
+    const int32_t nquads = (int32_t)p.sc.n_quads;
+    const int32_t sbase = nplanes + nquads;   // object ids: planes, quads, spheres
 
     // per-lane item state
     uint32_t q = lane;            // item index in the task's pool
@@ -848,22 +869,32 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? 5 : 1) render_kernel(
                     best = k;
                 }
             }
+            // quads, each behind its own AABB (bounded_hit, hittable.rs:190-196)
+            for (int32_t k = 0; k < nquads; ++k) {
+                R t;
+                const R* Q = p.sc.quads + kQuadR * k;
+                if (aabb_hit_ref(Q + 16, Q + 19, o, d, tmin) && quad_t_hit(Q, o, d, tmin, (R)INFINITY, t) &&
+                    (best < 0 || t < tb)) {
+                    tb = t;
+                    best = nplanes + k;
+                }
+            }
             if constexpr (kWorld >= kWorldBvh) {
 #if RTW_EXP == 1
                 {
                     R tb2 = tb;
                     int32_t best2 = best;
-                    bvh_closest<kWorld == kWorldBvhLds ? kWorldBvhWW : kWorld, kRobust>(scw, nplanes, o, d, tmin, tb2, best2,
+                    bvh_closest<kWorld == kWorldBvhLds ? kWorldBvhWW : kWorld, kRobust>(scw, sbase, o, d, tmin, tb2, best2,
                                         reinterpret_cast<int32_t*>(smem) + wave * p.stack * 64 + lane, nvis,
                                         ntest, self_s);
                     segs += best2 == -7 ? 1u : 0u;
                 }
 #endif
-                bvh_closest<kWorld == kWorldBvhLds ? kWorldBvhWW : kWorld, kRobust>(scw, nplanes, o, d, tmin, tb, best,
+                bvh_closest<kWorld == kWorldBvhLds ? kWorldBvhWW : kWorld, kRobust>(scw, sbase, o, d, tmin, tb, best,
                                     reinterpret_cast<int32_t*>(smem) + wave * p.stack * 64 + lane, nvis,
                                     ntest, self_s);
             } else {
-                sweep_spheres<kRobust>(sph, p.sc.n_sph, nplanes, o, d, tmin, tb, best);
+                sweep_spheres<kRobust>(sph, p.sc.n_sph, sbase, o, d, tmin, tb, best);
             }
             ++segs;
 
@@ -882,8 +913,12 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? 5 : 1) render_kernel(
                     const R* pl = p.sc.planes + 12 * best;
                     outward = mk(pl[3], pl[4], pl[5]);
                     m = p.sc.plane_mat[best];
+                } else if (best < sbase) {
+                    const R* Q = p.sc.quads + kQuadR * (best - nplanes);
+                    outward = q3(Q, 12);                           // quadrilateral.rs:97
+                    m = p.sc.quad_mat[best - nplanes];
                 } else {
-                    const uint32_t k = (uint32_t)(best - nplanes);
+                    const uint32_t k = (uint32_t)(best - sbase);
                     const R4<R> sk = p.sc.sph[k];
                     outward = PR::divs(pnt - mk(sk.x, sk.y, sk.z), p.sc.sph_r[k]);  // sphere.rs:82-83
                     const uint32_t mw = p.sc.sph_mat[k];
@@ -894,7 +929,9 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? 5 : 1) render_kernel(
                 const V3<R> nrm = front ? outward : -outward;
                 const uint32_t mtype = p.sc.mat_type[m];
                 const R4<R> mp = p.sc.mat_p[m];
-                const V3<R> emitted = zero;                            // material.rs:42-44
+                // Material::emitted: DiffuseLight's colour (material.rs:508-514),
+                // black for every other material (material.rs:42-44)
+                const V3<R> emitted = mtype == kMatDiffuseLight ? mk(mp.x, mp.y, mp.z) : zero;
                 if (mtype == kMatMetal) {
                     // Metal::scatter, material.rs:407-421
                     V3<R> refl = reflect(PR::normalize(d), nrm);
@@ -933,9 +970,19 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? 5 : 1) render_kernel(
                     V3<R> dir;
                     if (PR::u_std(g.next()) < (R)0.5) {
                         // HittableList::random (hittable_list.rs:414-419): a
-                        // uniform light (one gen_index draw), then Sphere::random
-                        const R4<R> L = li[g.index(p.sc.n_lights)];
-                        dir = sphere_random(mk(L.x, L.y, L.z), L.w, pnt, g);
+                        // uniform light (one gen_index draw), then its random()
+                        if (p.sc.lref) {
+                            const uint32_t ref = p.sc.lref[g.index(p.sc.n_list)];
+                            if (ref >> 31) {
+                                dir = quad_random(p.sc.lquads + kQuadR * (ref & 0x7fffffffu), pnt, g);
+                            } else {
+                                const R4<R> L = li[ref];
+                                dir = sphere_random(mk(L.x, L.y, L.z), L.w, pnt, g);
+                            }
+                        } else {
+                            const R4<R> L = li[g.index(p.sc.n_lights)];
+                            dir = sphere_random(mk(L.x, L.y, L.z), L.w, pnt, g);
+                        }
                     } else {
                         dir = uvw.transform(cosine_hemisphere<R>(g));
                     }
@@ -955,7 +1002,9 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? 5 : 1) render_kernel(
                     const V3<R> ndir = PR::normalize(dir);
                     const R cos_w = PR::over_pi(dot(ndir, uvw.w));
                     R acc;                                                // hittable_list.rs:408-412
-                    if constexpr (kLightBvh)
+                    if (p.sc.lref)
+                        acc = lights_pdf_mixed(p.sc, li, pnt, dir);
+                    else if constexpr (kLightBvh)
                         acc = lights_pdf_bvh<kRobust>(p.sc, pnt, dir,
                                                       reinterpret_cast<int32_t*>(smem) + wave * p.stack * 64 + lane);
                     else
@@ -963,7 +1012,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? 5 : 1) render_kernel(
 #if RTW_EXP == 2
                     segs += lights_pdf_sum<kRobust>(li, p.sc.n_lights, pnt, mk(dir.y, dir.z, dir.x)) == (R)-7 ? 1u : 0u;
 #endif
-                    const R lpdf = PR::div_(acc, (R)p.sc.n_lights);
+                    const R lpdf = PR::div_(acc, (R)p.sc.n_list);
                     const R pdf = lpdf * (R)0.5 + PR::max_(cos_w, (R)0) * (R)0.5;
                     const R spdf = PR::max_(PR::over_pi(dot(nrm, ndir)), (R)0);
                     const V3<R> w = PR::divs(att * spdf, pdf);

@@ -53,6 +53,7 @@ struct P<double> {
     static constexpr double kPi = 3.14159265358979323846;
     static constexpr double kTau = 2.0 * 3.14159265358979323846;
     static constexpr double kEps = 2.220446049250313080847e-16;  // f64::EPSILON
+    static constexpr double kEpsF64 = 2.220446049250313080847e-16;
     __device__ static __forceinline__ double sqrt_(double x) { return __builtin_sqrt(x); }
     __device__ static __forceinline__ double div_(double a, double b) { return a / b; }
     __device__ static __forceinline__ double over_pi(double a) { return a / kPi; }
@@ -132,6 +133,7 @@ struct P<float> {
     static constexpr float kPi = 3.14159265358979323846f;
     static constexpr float kInvPi = 0.318309886183790671538f;
     static constexpr float kEps = 2.220446049250313080847e-16f;  // same t_min as f64 (2^-52)
+    static constexpr float kEpsF64 = 2.220446049250313080847e-16f;
     __device__ static __forceinline__ float sqrt_(float x) { return __builtin_amdgcn_sqrtf(x); }
     __device__ static __forceinline__ float div_(float a, float b) { return a * __builtin_amdgcn_rcpf(b); }
     __device__ static __forceinline__ float over_pi(float a) { return a * kInvPi; }
@@ -341,6 +343,53 @@ __device__ __forceinline__ V3<R> sphere_random(V3<R> c, R radius, V3<R> o, Rng& 
         R y = s * P<R>::sqrt_((R)1 - z * z);
         return uvw.transform(mk(x, y, z));
     }
+}
+
+// ---------------------------------------------------------------------------
+// Quad (quadrilateral.rs), on the staged record Q (rtw_kernels.h kQuadR):
+// Q[0..2] q, [3..5] u, [6..8] v, [9..11] w, [12..14] unit normal, [15] area.
+// Operation order as the oracle's quad_new / quad_hit_t.
+// ---------------------------------------------------------------------------
+template <typename R>
+__device__ __forceinline__ V3<R> q3(const R* Q, int k) { return mk(Q[k], Q[k + 1], Q[k + 2]); }
+
+// Quad::hit, quadrilateral.rs:79-100: two-sided, t in [tmin, tmax], (alpha,
+// beta) = get_quad_uv in [0, 1] inclusive
+template <typename R>
+__device__ __forceinline__ bool quad_t_hit(const R* Q, V3<R> o, V3<R> d, R tmin, R tmax, R& t) {
+    const V3<R> n = q3(Q, 12);
+    const R denom = dot(d, n);
+    if (!(fabs(denom) > P<R>::kEpsF64)) return false;
+    const R tt = -P<R>::div_(dot(o - q3(Q, 0), n), denom);
+    if (!(tt >= tmin && tt <= tmax)) return false;
+    const V3<R> pq = (o + d * tt) - q3(Q, 0);
+    const V3<R> w = q3(Q, 9);
+    const R alpha = dot(cross(pq, q3(Q, 6)), w);
+    const R beta = dot(cross(q3(Q, 3), pq), w);
+    if (!(alpha >= (R)0 && alpha <= (R)1 && beta >= (R)0 && beta <= (R)1)) return false;
+    t = tt;
+    return true;
+}
+
+// Quad::pdf_value, quadrilateral.rs:102-112
+template <typename R>
+__device__ __forceinline__ R quad_pdf_value(const R* Q, V3<R> o, V3<R> d) {
+    R t;
+    if (!quad_t_hit(Q, o, d, (R)0, (R)INFINITY, t)) return (R)0;
+    const V3<R> n0 = q3(Q, 12);
+    const V3<R> n = dot(d, n0) < (R)0 ? n0 : -n0;               // HitRecord::new
+    const R distance_squared = t * t * dot(d, d);
+    const R cosine = fabs(P<R>::div_(dot(d, n), P<R>::sqrt_(dot(d, d))));
+    return P<R>::div_(distance_squared, cosine * Q[15]);
+}
+
+// Quad::random, quadrilateral.rs:114-118 (u's Open01 draw first)
+template <typename R>
+__device__ __forceinline__ V3<R> quad_random(const R* Q, V3<R> o, Rng& g) {
+    const R r1 = P<R>::u_open01(g.next());
+    const R r2 = P<R>::u_open01(g.next());
+    const V3<R> p = (q3(Q, 0) + q3(Q, 3) * r1) + q3(Q, 6) * r2;
+    return p - o;
 }
 
 // Dialectric::reflectance, material.rs:450-454; powi(5) = x * ((x*x)*(x*x))

@@ -24,7 +24,7 @@ enum WorldMode : int {
 };
 
 // material kinds (same codes as RTW_LAMBERTIAN.. in include/rtw.h)
-enum : uint32_t { kMatLambertian = 0, kMatMetal = 1, kMatDielectric = 2, kMatInvisible = 3 };
+enum : uint32_t { kMatLambertian = 0, kMatMetal = 1, kMatDielectric = 2, kMatInvisible = 3, kMatDiffuseLight = 4 };
 
 template <typename R>
 struct alignas(4 * sizeof(R)) R4 {
@@ -88,10 +88,21 @@ struct DevScene {
     const BvhNode<R>* lbvh;           // binary BVH over the light spheres
     const R4<R>* lsph;                // lights {cx, cy, cz, r} in light-BVH leaf order
     const uint32_t* lid;              // light-list index of lsph[k]
+    const R* quads;                   // n_quads x kQuadR (see quad layout below)
+    const uint32_t* quad_mat;
+    const R* lquads;                  // the light list's quads, n_lquads x kQuadR
+    const uint32_t* lref;             // light list in order: bit 31 = quad, low bits = index
+                                      // (null when the list is spheres only)
     uint32_t n_sph, n_planes, n_mat, n_lights, n_nodes, bvh_depth;
     uint32_t n_nodes4, bvh4_stack, n_lnodes, lbvh_depth;
     uint32_t robust;                  // f32: closest-approach sphere / light tests (far geometry)
+    uint32_t n_quads, n_lquads, n_list;   // world quads, light quads, light-list length
 };
+
+// Quad record (Quad::new's derived fields, quadrilateral.rs:37-56), kQuadR
+// values of precision R: Q[0..2], u[3..5], v[6..8], w = n/|n|^2 [9..11],
+// unit normal [12..14], area [15], AABB lo [16..18], hi [19..21], pad.
+constexpr uint32_t kQuadR = 24;
 
 constexpr uint32_t kBvhStack = 32;    // per-lane traversal stack entries (LDS)
 

@@ -413,3 +413,65 @@ def test_f32_sphere_test_forms_bvh_equals_brute(robust):
     brute, _, cb = _render_gpu(soa, cam, 19, rtw.RTW_F32, accel=rtw.RTW_ACCEL_BRUTE, tuning=t)
     bvh, _, cv = _render_gpu(soa, cam, 19, rtw.RTW_F32, accel=rtw.RTW_ACCEL_BVH, tuning=t)
     assert _same(brute, bvh) and cb == cv
+
+
+# ---- Quad + DiffuseLight
+
+def _cornell_quads(with_metal=True):
+    """scenes::cornell_box (scenes/src/lib.rs:292-395) without its rotated
+    Cuboid (rank 4): the five walls, the ceiling light and the glass sphere;
+    lights = [ceiling quad, glass sphere] in the reference's order."""
+    red, white, green = rtw.Lambertian((0.65, 0.05, 0.05)), rtw.Lambertian((0.73, 0.73, 0.73)), \
+        rtw.Lambertian((0.12, 0.45, 0.15))
+    light, glass = rtw.DiffuseLight((15.0, 15.0, 15.0)), rtw.Dialectric(1.5)
+    world = rtw.HittableList([
+        rtw.Quad((555, 0, 0), (0, 555, 0), (0, 0, 555), green),
+        rtw.Quad((0, 0, 0), (0, 555, 0), (0, 0, 555), red),
+        rtw.Quad((0, 0, 0), (555, 0, 0), (0, 0, 555), white),
+        rtw.Quad((555, 555, 555), (-555, 0, 0), (0, 0, -555), white),
+        rtw.Quad((0, 0, 555), (555, 0, 0), (0, 555, 0), white),
+        rtw.Quad((343, 554, 332), (-130, 0, 0), (0, 0, -105), light),
+        rtw.Sphere((190, 90, 190), 90, glass),
+    ])
+    if with_metal:
+        world.add(rtw.Sphere((400, 100, 350), 100, rtw.Metal((0.8, 0.85, 0.88), 0.05)))
+    lights = rtw.HittableList([rtw.Quad((343, 554, 332), (-130, 0, 0), (0, 0, -105)),
+                               rtw.Sphere((190, 90, 190), 90)])
+    cam = rtw.CameraBuilder().with_lookfrom((278, 278, -800)).with_lookat((278, 278, 0)) \
+        .with_vfov(40).with_background((0, 0, 0))
+    return rtw.flatten(world, lights), cam
+
+
+def test_quad_scene_f64_matches_oracle():
+    soa, b = _cornell_quads()
+    assert soa.light_kinds.tolist() == [1, 0]
+    cam = b.with_image_width(40).with_image_height(40).with_samples_per_pixel(6).with_max_depth(30).build()
+    for accel in (rtw.RTW_ACCEL_BRUTE, rtw.RTW_ACCEL_BVH):
+        gpu, chunk, (segs, lambs) = _render_gpu(soa, cam, 61, rtw.RTW_F64, accel=accel)
+        ref, st = _render_oracle(soa, cam, 61, chunk)
+        mae, exact = _compare_f64(gpu, ref, 6)
+        assert mae < F64_MAE_TOL and exact > 0.999, (accel, mae, exact)
+        assert segs == st.segments and lambs == st.lambertian
+
+
+def test_quad_scene_f32_bvh_equals_brute_and_tracks_f64():
+    soa, b = _cornell_quads()
+    cam = b.with_image_width(48).with_image_height(48).with_samples_per_pixel(16).with_max_depth(30).build()
+    brute, _, cb = _render_gpu(soa, cam, 67, rtw.RTW_F32, accel=rtw.RTW_ACCEL_BRUTE)
+    bvh, _, cv = _render_gpu(soa, cam, 67, rtw.RTW_F32, accel=rtw.RTW_ACCEL_BVH)
+    assert _same(brute, bvh) and cb == cv
+    ref, _ = _render_oracle(soa, cam, 67, 0)
+    ok = ~(np.isnan(bvh).any(-1) | np.isnan(ref).any(-1))
+    m32, m64 = bvh[ok].mean(), ref[ok].mean()
+    assert abs(m32 - m64) < 0.03 * m64, (m32, m64)
+
+
+def test_diffuse_light_quad_is_its_colour():
+    world = rtw.HittableList([rtw.Quad((-5, -5, -3), (10, 0, 0), (0, 10, 0), rtw.DiffuseLight((4, 2, 1)))])
+    soa = rtw.flatten(world, rtw.HittableList())
+    cam = rtw.CameraBuilder().with_image_width(8).with_image_height(6).with_samples_per_pixel(5) \
+        .with_max_depth(10).with_background((0, 0, 0)).build()
+    for prec in (rtw.RTW_F32, rtw.RTW_F64):
+        gpu, _, (segs, lambs) = _render_gpu(soa, cam, 3, prec)
+        np.testing.assert_array_equal(gpu, np.broadcast_to([20.0, 10.0, 5.0], gpu.shape))
+        assert segs == 8 * 6 * 5 and lambs == 0
