@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define RTW_ABI_VERSION 3
+#define RTW_ABI_VERSION 4
 
 /* error codes */
 #define RTW_OK 0
@@ -110,6 +110,12 @@ typedef struct rtw_scene {
      * n_lights + n_light_quads kinds, 0 = next sphere, 1 = next quad;
      * NULL = all spheres, then all quads */
     const uint32_t *light_kinds;
+    /* Transformed<Cuboid> (cuboid.rs:26-71, entities/transformations.rs:10-30):
+     * Cuboid::new(p, q, mat) under the composed Transformation (rotation R,
+     * translation T; Transformation::then order, geometry transformations.rs) */
+    uint32_t n_boxes;
+    const double *boxes;          /* n_boxes x {p xyz, q xyz, R[3][3] row-major, T xyz} = 18 */
+    const uint32_t *box_mat;
 } rtw_scene;
 
 typedef struct rtw_stats {
@@ -195,6 +201,9 @@ const rtw_scene *rtw_world_scene(const rtw_world *w);
 /* the camera builder scenes::simple returns (lib.rs:219-226) + main.rs's vfov */
 void rtw_world_camera_builder(const rtw_world *w, rtw_camera_builder *out);
 void rtw_world_free(rtw_world *w);
+/* a reference scene by its bin/src/main.rs name: "simple" (seeded, grid 11)
+ * or "cornell_box" (scenes/src/lib.rs:292-395); NULL for other names */
+rtw_world *rtw_scene_named(const char *name, uint64_t seed);
 
 /* ---- SampledColour / PPM (colour.rs:14-36; main.rs:89-104) ------------ */
 /* sums -> 8-bit RGB, rows flipped so that row 0 is the TOP row:

@@ -55,6 +55,7 @@ class _Scene(C.Structure):
         ("n_lights", C.c_uint32), ("lights", _f64p),
         ("n_quads", C.c_uint32), ("quads", _f64p), ("quad_mat", _u32p),
         ("n_light_quads", C.c_uint32), ("light_quads", _f64p), ("light_kinds", _u32p),
+        ("n_boxes", C.c_uint32), ("boxes", _f64p), ("box_mat", _u32p),
     ]
 
 
@@ -77,6 +78,8 @@ class Scene:
     quad_mat: np.ndarray = None      # (q,) uint32
     light_quads: np.ndarray = None   # (lq, 9)
     light_kinds: np.ndarray = None   # (l + lq,) 0 sphere / 1 quad, list order; None = spheres first
+    boxes: np.ndarray = None         # (b, 18) Cuboid p, q, rotation R (row-major), translation T
+    box_mat: np.ndarray = None       # (b,) uint32
 
 
 _lib = None
@@ -135,6 +138,13 @@ def lib():
         L.rtwo_quad_pdf_value.restype = C.c_double
         L.rtwo_quad_random.argtypes = [_f64p, _f64p, _u64p, _f64p]
         L.rtwo_quad_aabb.argtypes = [_f64p, _f64p]
+        L.rtwo_box_hit.argtypes = [_f64p, _f64p, _f64p, C.c_double, C.c_double, _f64p]
+        L.rtwo_box_aabb.argtypes = [_f64p, _f64p]
+        L.rtwo_trace_path.argtypes = [C.POINTER(Camera), C.POINTER(_Scene), C.c_uint64, C.c_uint32,
+                                      C.c_uint32, C.c_uint32, C.c_int, _f64p, C.POINTER(Stats), _f64p,
+                                      C.c_uint32]
+        L.rtwo_trace_path.restype = C.c_uint32
+        L.rtwo_world_hit.argtypes = [C.POINTER(_Scene), C.c_int, _f64p, _f64p, _f64p]
         _lib = L
     return _lib
 
@@ -243,7 +253,10 @@ def _scene_struct(sc: Scene):
                len(np.asarray(sc.lights).reshape(-1, 4)), f(sc.lights, 4),
                len(np.asarray(qmat).reshape(-1)), f(quads, 9), u(qmat),
                len(np.asarray(lq).reshape(-1, 9)), f(lq, 9),
-               None if sc.light_kinds is None else u(sc.light_kinds))
+               None if sc.light_kinds is None else u(sc.light_kinds),
+               0 if sc.box_mat is None else len(np.asarray(sc.box_mat).reshape(-1)),
+               f(np.zeros((0, 18)) if sc.boxes is None else sc.boxes, 18),
+               u(np.zeros(0, np.uint32) if sc.box_mat is None else sc.box_mat))
     return s, keep
 
 
@@ -276,6 +289,18 @@ def trace_sample(cam: Camera, sc: Scene, seed: int, i: int, j: int, s: int):
                             C.byref(st))
     del keep
     return rgb, st
+
+
+def trace_path(cam: Camera, sc: Scene, seed: int, i: int, j: int, s: int, accel=ACCEL_BRUTE, cap=64):
+    """(rgb, [segments x {o xyz, d xyz, id, t}]) of one sample (debugging / KATs)."""
+    st = Stats()
+    rgb = np.zeros(3)
+    path = np.zeros((cap, 8))
+    ss, keep = _scene_struct(sc)
+    n = lib().rtwo_trace_path(C.byref(cam), C.byref(ss), C.c_uint64(seed), i, j, s, accel,
+                              _p(rgb, _f64p), C.byref(st), _p(path, _f64p), cap)
+    del keep
+    return rgb, path[:min(n, cap)]
 
 
 def bvh_stats(sc: Scene):
@@ -330,3 +355,63 @@ def quad_aabb(quad):
     out = (C.c_double * 6)()
     lib().rtwo_quad_aabb(arr(quad, 9), out)
     return tuple(out[:3]), tuple(out[3:])
+
+
+# ---- Transformed<Cuboid> KAT entry points
+def box_hit(box, o, d, tmin=2.220446049250313e-16, tmax=float("inf")):
+    """(t, world point[3], object-space normal[3], front) or None."""
+    out = (C.c_double * 8)()
+    hit = lib().rtwo_box_hit(arr(box, 18), arr(o), arr(d), tmin, tmax, out)
+    return (out[0], tuple(out[1:4]), tuple(out[4:7]), bool(out[7])) if hit else None
+
+
+def box_aabb(box):
+    out = (C.c_double * 6)()
+    lib().rtwo_box_aabb(arr(box, 18), out)
+    return tuple(out[:3]), tuple(out[3:])
+
+
+def transform_compose(*steps):
+    """Transformation::then chain (geometry/src/transformations.rs:97-108):
+    steps are ('translate', (x, y, z)) or ('rotate', angle_deg, axis 0/1/2),
+    applied in order; returns (R 3x3 list, T 3-list) as the reference's
+    f64 arithmetic computes them."""
+    R = [[1.0, 0.0, 0.0], [0.0, 1.0, 0.0], [0.0, 0.0, 1.0]]
+    T = [0.0, 0.0, 0.0]
+    for st in steps:
+        if st[0] == "translate":
+            bR, bT = [[1.0, 0.0, 0.0], [0.0, 1.0, 0.0], [0.0, 0.0, 1.0]], list(map(float, st[1]))
+        else:
+            bR, bT = rotation_matrix(st[1], st[2]), [0.0, 0.0, 0.0]
+        # apply: rotation = b.R * self.R, translation = b.T + b.R * self.T
+        nR = [[_dot(bR[i], [R[0][j], R[1][j], R[2][j]]) for j in range(3)] for i in range(3)]
+        bRT = [_dot(bR[i], T) for i in range(3)]
+        T = [bT[i] + bRT[i] for i in range(3)]
+        R = nR
+    return R, T
+
+
+def _dot(a, b):
+    return (a[0] * b[0] + a[1] * b[1]) + a[2] * b[2]
+
+
+def rotation_matrix(angle_deg, axis):
+    """geometry::transformations::rotation (non-euclid), angle.to_radians()
+    = angle * (PI / 180) as Rust's f64::to_radians."""
+    import math
+    a = angle_deg * (math.pi / 180.0)
+    c, s = math.cos(a), math.sin(a)
+    if axis == 0:
+        return [[1.0, 0.0, 0.0], [0.0, c, -s], [0.0, s, c]]
+    if axis == 1:
+        return [[c, 0.0, s], [0.0, 1.0, 0.0], [-s, 0.0, c]]
+    return [[c, -s, 0.0], [s, c, 0.0], [0.0, 0.0, 1.0]]
+
+
+def world_hit(sc: Scene, o, d, accel=ACCEL_BRUTE):
+    """(object id, t, p, normal, front) of world.hit, or (-1, ...)."""
+    s, keep = _scene_struct(sc)
+    out = (C.c_double * 8)()
+    k = lib().rtwo_world_hit(C.byref(s), accel, arr(o), arr(d), out)
+    del keep
+    return k, out[0], tuple(out[1:4]), tuple(out[4:7]), bool(out[7])

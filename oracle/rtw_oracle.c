@@ -441,6 +441,130 @@ void rtwo_quad_aabb(const double quad[9], double box[6]) {
     memcpy(box + 3, Q.box.mx, 24);
 }
 
+/* ------------------------------------------------------------------------ */
+/* Transformed<Cuboid>                                                      */
+/* ------------------------------------------------------------------------ */
+typedef struct { double m[3][3]; } mat3;
+/* Mul<Vec3> for Matrix3 (matrix3.rs:94-105): each row . p */
+static inline v3 mat3_mul(const mat3 *M, v3 p) {
+    return mk(dot(ld(M->m[0]), p), dot(ld(M->m[1]), p), dot(ld(M->m[2]), p));
+}
+typedef struct {
+    rquad quads[6];             /* the cuboid's quads, object space */
+    mat3 R, Ri;                 /* Transformation.rotation and its inverse */
+    v3 T, Ti;                   /* translation, -(Ri T) */
+    int invertible;
+    aabb box;                   /* Transformed::get_aabbox, world space */
+} rbox;
+
+static rbox box_new(const double *b) {
+    rbox B;
+    /* Cuboid::new, cuboid.rs:26-47: the (padded) box of p and q */
+    aabb ab = {{b[0], b[1], b[2]}, {b[0], b[1], b[2]}};
+    aabb qb = {{b[3], b[4], b[5]}, {b[3], b[4], b[5]}};
+    aabb_enclose(&ab, &qb);
+    v3 mn = mk(ab.mn[0], ab.mn[1], ab.mn[2]), mx = mk(ab.mx[0], ab.mx[1], ab.mx[2]);
+    v3 delta = sub(mx, mn);
+    v3 dx = mk(delta.x, 0.0, 0.0), dy = mk(0.0, delta.y, 0.0), dz = mk(0.0, 0.0, delta.z);
+    v3 args[6][3] = {{mn, dx, dy}, {mn, dy, dz}, {mn, dx, dz},
+                     {mx, neg(dx), neg(dy)}, {mx, neg(dy), neg(dz)}, {mx, neg(dx), neg(dz)}};
+    for (int i = 0; i < 6; ++i) {
+        double q[9];
+        st3(q, args[i][0]);
+        st3(q + 3, args[i][1]);
+        st3(q + 6, args[i][2]);
+        B.quads[i] = quad_new(q);
+    }
+    /* Cuboid::get_aabbox (cuboid.rs:61-71): fold of the quads' boxes */
+    aabb cub = B.quads[0].box;
+    for (int i = 1; i < 6; ++i) aabb_enclose(&cub, &B.quads[i].box);
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) B.R.m[r][c] = b[6 + 3 * r + c];
+    B.T = ld(b + 15);
+    /* Transformed::get_aabbox: from_points(instance box corners (get_points
+     * order, aabox.rs:113-124) mapped through transform_point3d) */
+    const double *lo = cub.mn, *hi = cub.mx;
+    v3 corners[8] = {mk(lo[0], lo[1], lo[2]), mk(lo[0], hi[1], lo[2]), mk(lo[0], lo[1], hi[2]),
+                     mk(lo[0], hi[1], hi[2]), mk(hi[0], lo[1], lo[2]), mk(hi[0], hi[1], lo[2]),
+                     mk(hi[0], lo[1], hi[2]), mk(hi[0], hi[1], hi[2])};
+    for (int i = 0; i < 8; ++i) {
+        v3 w = add(mat3_mul(&B.R, corners[i]), B.T);
+        if (i == 0) {
+            B.box.mn[0] = B.box.mx[0] = w.x;
+            B.box.mn[1] = B.box.mx[1] = w.y;
+            B.box.mn[2] = B.box.mx[2] = w.z;
+        } else {
+            aabb pb = {{w.x, w.y, w.z}, {w.x, w.y, w.z}};
+            aabb_enclose(&B.box, &pb);
+        }
+    }
+    /* Matrix3::inverse (matrix3.rs:9-28) and Transformation::inverse */
+    const double a = B.R.m[0][0], bb = B.R.m[0][1], c = B.R.m[0][2];
+    const double d = B.R.m[1][0], e = B.R.m[1][1], f = B.R.m[1][2];
+    const double g = B.R.m[2][0], h = B.R.m[2][1], i = B.R.m[2][2];
+    const double det = a * (e * i - f * h) + bb * (f * g - d * i) + c * (d * h - e * g);
+    B.invertible = isnormal(det);
+    const double A = e * i - f * h, Bc = f * g - d * i, C = d * h - e * g;
+    const double D = c * h - bb * i, E = a * i - c * g, F = bb * g - a * h;
+    const double G = bb * f - c * e, H = c * d - a * f, I = a * e - bb * d;
+    B.Ri.m[0][0] = A / det; B.Ri.m[0][1] = D / det; B.Ri.m[0][2] = G / det;
+    B.Ri.m[1][0] = Bc / det; B.Ri.m[1][1] = E / det; B.Ri.m[1][2] = H / det;
+    B.Ri.m[2][0] = C / det; B.Ri.m[2][1] = F / det; B.Ri.m[2][2] = I / det;
+    B.Ti = neg(mat3_mul(&B.Ri, B.T));
+    return B;
+}
+
+/* Transformed<Cuboid>::hit (entities/transformations.rs:14-29 over
+ * Cuboid::hit, cuboid.rs:50-58).  The ray goes to object space through the
+ * inverse: origin by transform_point3d, direction by transform_vector3d --
+ * which in geometry/src/transformations.rs:112-114 also ADDS the translation
+ * (the reference's behaviour, kept).  Closest of the six quads (min_by: the
+ * first minimum), then only the hit point goes back to world space; the
+ * normal stays in object space. */
+static int box_hit(const rbox *B, v3 o, v3 d, double tmin, double tmax, double *t, v3 *pw, v3 *nrm,
+                   int *front) {
+    if (!B->invertible) return 0;
+    v3 o2 = add(mat3_mul(&B->Ri, o), B->Ti);
+    v3 d2 = add(mat3_mul(&B->Ri, d), B->Ti);
+    int best = -1;
+    double bt = INFINITY;
+    for (int k = 0; k < 6; ++k) {
+        double tt;
+        if (quad_hit_t(&B->quads[k], o2, d2, tmin, tmax, &tt) && (best < 0 || tt < bt)) {
+            bt = tt;
+            best = k;
+        }
+    }
+    if (best < 0) return 0;
+    *t = bt;
+    if (pw) {
+        v3 n = B->quads[best].normal;
+        *front = dot(d2, n) < 0.0;                               /* HitRecord::new */
+        *nrm = *front ? n : neg(n);
+        *pw = add(mat3_mul(&B->R, at(o2, d2, bt)), B->T);        /* transform_point3d */
+    }
+    return 1;
+}
+
+int rtwo_box_hit(const double box[18], const double o[3], const double d[3],
+                 double tmin, double tmax, double out[8]) {
+    rbox B = box_new(box);
+    double t;
+    v3 pw, n;
+    int front;
+    if (!box_hit(&B, ld(o), ld(d), tmin, tmax, &t, &pw, &n, &front)) return 0;
+    out[0] = t;
+    st3(out + 1, pw);
+    st3(out + 4, n);
+    out[7] = front;
+    return 1;
+}
+void rtwo_box_aabb(const double box[18], double aabb_out[6]) {
+    rbox B = box_new(box);
+    memcpy(aabb_out, B.box.mn, 24);
+    memcpy(aabb_out + 3, B.box.mx, 24);
+}
+
 /* Sphere::pdf_value, sphere.rs:101-111 */
 static inline double sphere_pdf_value(v3 c, double radius, v3 o, v3 d) {
     double t;
@@ -493,7 +617,7 @@ void rtwo_refract(const double v[3], const double n[3], double eta, double out[3
 /* ------------------------------------------------------------------------ */
 /* Object ids: planes, quads, spheres (three "type groups", as the          */
 /* TypeId-sorted RawHittableVecs of a HittableList).                        */
-#define NG 3
+#define NG 4
 typedef struct {
     int leaf;
     int left, right;            /* node children */
@@ -514,14 +638,19 @@ typedef struct {
     int max_depth;
 } bvh_t;
 
-/* object ids: [0, n_planes) planes, then n_quads quads, then the spheres */
-static inline int sphere_base(const rtwo_scene *sc) { return (int)(sc->n_planes + sc->n_quads); }
+/* object ids: [0, n_planes) planes, then n_quads quads, n_boxes boxes, then the spheres */
+static inline int box_base(const rtwo_scene *sc) { return (int)(sc->n_planes + sc->n_quads); }
+static inline int sphere_base(const rtwo_scene *sc) { return (int)(sc->n_planes + sc->n_quads + sc->n_boxes); }
 
 static aabb object_box(const rtwo_scene *sc, int id) {
     aabb b;
-    if (id >= (int)sc->n_planes && id < sphere_base(sc)) {
+    if (id >= (int)sc->n_planes && id < box_base(sc)) {
         rquad Q = quad_new(sc->quads + 9 * (id - (int)sc->n_planes));
         return Q.box;
+    }
+    if (id >= box_base(sc) && id < sphere_base(sc)) {
+        rbox B = box_new(sc->boxes + 18 * (id - box_base(sc)));
+        return B.box;
     }
     if (id < (int)sc->n_planes) {
         /* Plane::get_aabbox, plane.rs:218-242 */
@@ -554,7 +683,7 @@ static int new_node(bvh_t *t) {
  * ordered list of ids in the group's Vec order. */
 typedef struct { int *ids[NG]; int len[NG]; } hlist;
 
-static int hl_len(const hlist *h) { return h->len[0] + h->len[1] + h->len[2]; }
+static int hl_len(const hlist *h) { return h->len[0] + h->len[1] + h->len[2] + h->len[3]; }
 
 static aabb group_box(const bvh_t *t, const int *ids, int len) {
     /* Slice::get_aabbox: reduce(|acc, e| acc.enclose(e)) (utils.rs:152-158) */
@@ -675,14 +804,15 @@ static int build(bvh_t *t, hlist *h, int depth) {
 static void bvh_build(bvh_t *t, const rtwo_scene *sc) {
     memset(t, 0, sizeof(*t));
     t->sc = sc;
-    int n = (int)(sc->n_planes + sc->n_quads + sc->n_spheres);
+    int n = (int)(sc->n_planes + sc->n_quads + sc->n_boxes + sc->n_spheres);
     t->obj_box = (aabb *)malloc(sizeof(aabb) * (n ? n : 1));
     t->obj_ids = (int *)malloc(sizeof(int) * (n ? n : 1));
     for (int i = 0; i < n; ++i) t->obj_box[i] = object_box(sc, i);
     hlist h;
     h.len[0] = (int)sc->n_planes;
     h.len[1] = (int)sc->n_quads;
-    h.len[2] = (int)sc->n_spheres;
+    h.len[2] = (int)sc->n_boxes;
+    h.len[3] = (int)sc->n_spheres;
     int first = 0;
     for (int g = 0; g < NG; ++g) {
         h.ids[g] = (int *)malloc(sizeof(int) * (h.len[g] + 1));
@@ -714,9 +844,13 @@ static inline int object_hit_t(const rtwo_scene *sc, int id, v3 o, v3 d, double 
         const double *p = sc->planes + 6 * id;
         return plane_t(ld(p), ld(p + 3), o, d, tmin, tmax, t);
     }
-    if (id < sphere_base(sc)) {
+    if (id < box_base(sc)) {
         rquad Q = quad_new(sc->quads + 9 * (id - (int)sc->n_planes));
         return quad_hit_t(&Q, o, d, tmin, tmax, t);
+    }
+    if (id < sphere_base(sc)) {
+        rbox B = box_new(sc->boxes + 18 * (id - box_base(sc)));
+        return box_hit(&B, o, d, tmin, tmax, t, NULL, NULL, NULL);
     }
     const double *s = sc->spheres + 4 * (id - sphere_base(sc));
     return sphere_t(ld(s), s[3], o, d, tmin, tmax, t);
@@ -775,10 +909,12 @@ typedef struct {
     int accel;
     uint64_t seed;
     double u_scale;             /* Uniform::new_inclusive(-0.5, 0.5) scale */
+    double *path;               /* debugging: per-segment {o, d, id, t} or NULL */
+    uint32_t path_cap;
 } ctx_t;
 
 /* world.hit(&r, EPSILON..=INFINITY), closest over every primitive */
-static int world_hit(const ctx_t *cx, v3 o, v3 d, hitrec *rec) {
+static int world_hit_id(const ctx_t *cx, v3 o, v3 d, hitrec *rec, int *id_out) {
     const rtwo_scene *sc = cx->sc;
     const double tmin = DBL_EPSILON, tmax = INFINITY;
     int best = -1;
@@ -805,6 +941,12 @@ static int world_hit(const ctx_t *cx, v3 o, v3 d, hitrec *rec) {
             if (aabb_hit(&Q.box, o, d, tmin, tmax) && quad_hit_t(&Q, o, d, tmin, tmax, &t) &&
                 (best < 0 || t < bt)) { bt = t; best = (int)(sc->n_planes + k); }
         }
+        for (uint32_t k = 0; k < sc->n_boxes; ++k) {
+            rbox B = box_new(sc->boxes + 18 * k);
+            double t;
+            if (aabb_hit(&B.box, o, d, tmin, tmax) && box_hit(&B, o, d, tmin, tmax, &t, NULL, NULL, NULL) &&
+                (best < 0 || t < bt)) { bt = t; best = box_base(sc) + (int)k; }
+        }
         for (uint32_t k = 0; k < sc->n_spheres; ++k) {
             const double *s = sc->spheres + 4 * k;
             double t;
@@ -818,13 +960,21 @@ static int world_hit(const ctx_t *cx, v3 o, v3 d, hitrec *rec) {
         best = c.id;
         bt = c.t;
     }
+    if (id_out) *id_out = best;
     if (best < 0) return 0;
     if (best < (int)sc->n_planes) {
         make_record(o, d, bt, ld(sc->planes + 6 * best + 3), sc->plane_mat[best], rec);
-    } else if (best < sphere_base(sc)) {
+    } else if (best < box_base(sc)) {
         uint32_t k = (uint32_t)best - sc->n_planes;
         rquad Q = quad_new(sc->quads + 9 * k);
         make_record(o, d, bt, Q.normal, sc->quad_mat[k], rec);
+    } else if (best < sphere_base(sc)) {
+        uint32_t k = (uint32_t)(best - box_base(sc));
+        rbox B = box_new(sc->boxes + 18 * k);
+        double t2;
+        box_hit(&B, o, d, DBL_EPSILON, INFINITY, &t2, &rec->p, &rec->normal, &rec->front);
+        rec->t = bt;
+        rec->mat = sc->box_mat[k];
     } else {
         uint32_t k = (uint32_t)(best - sphere_base(sc));
         const double *s = sc->spheres + 4 * k;
@@ -848,6 +998,25 @@ static inline void light_entry(const rtwo_scene *sc, uint32_t k, int *is_quad, u
     }
     *is_quad = sc->light_kinds[k] != 0;
     *idx = *is_quad ? nq : ns;
+}
+
+/* world.hit for one ray (KATs / debugging): returns the object id (planes,
+ * quads, boxes, spheres numbering) or -1; out = {t, p xyz, normal xyz, front}. */
+int rtwo_world_hit(const rtwo_scene *sc, int accel, const double o[3], const double d[3], double out[8]) {
+    bvh_t bvh;
+    int use_bvh = accel != RTWO_ACCEL_BRUTE;
+    if (use_bvh) bvh_build(&bvh, sc);
+    ctx_t cx = {NULL, sc, use_bvh ? &bvh : NULL, accel, 0, 0.0, NULL, 0};
+    hitrec rec;
+    int id = -1;
+    if (world_hit_id(&cx, ld(o), ld(d), &rec, &id)) {
+        out[0] = rec.t;
+        st3(out + 1, rec.p);
+        st3(out + 4, rec.normal);
+        out[7] = rec.front;
+    }
+    if (use_bvh) bvh_free(&bvh);
+    return id;
 }
 
 /* HittableList::pdf_value, hittable_list.rs:408-412 */
@@ -918,8 +1087,17 @@ static v3 trace(const ctx_t *cx, uint32_t i, uint32_t j, uint32_t s, rtwo_stats 
     for (;;) {
         if (depth == 0) return add(zero, res);                     /* :470-472 */
         hitrec rec;
-        stats->segments++;
-        if (!world_hit(cx, o, d, &rec))
+        const uint64_t seg = stats->segments++;
+        int hid = -1;
+        const int hit = world_hit_id(cx, o, d, &rec, &hid);
+        if (cx->path && seg < cx->path_cap) {
+            double *e = cx->path + 8 * seg;
+            st3(e, o);
+            st3(e + 3, d);
+            e[6] = hid;
+            e[7] = hit ? rec.t : INFINITY;
+        }
+        if (!hit)
             return add(mulv(mult, ld(c->background)), res);        /* :473-475 */
         const uint32_t m = rec.mat;
         const double *mp = sc->mat_params + 5 * m;
@@ -978,9 +1156,19 @@ static v3 trace(const ctx_t *cx, uint32_t i, uint32_t j, uint32_t s, rtwo_stats 
 
 void rtwo_trace_sample(const rtwo_camera *cam, const rtwo_scene *sc, uint64_t seed,
                        uint32_t i, uint32_t j, uint32_t s, double out_rgb[3], rtwo_stats *stats) {
-    ctx_t cx = {cam, sc, NULL, RTWO_ACCEL_BRUTE, seed, uniform_incl_scale(-0.5, 0.5)};
+    rtwo_trace_path(cam, sc, seed, i, j, s, RTWO_ACCEL_BRUTE, out_rgb, stats, NULL, 0);
+}
+
+uint32_t rtwo_trace_path(const rtwo_camera *cam, const rtwo_scene *sc, uint64_t seed, uint32_t i, uint32_t j,
+                         uint32_t s, int accel, double out_rgb[3], rtwo_stats *stats, double *path,
+                         uint32_t path_cap) {
+    bvh_t bvh;
+    const int use_bvh = accel != RTWO_ACCEL_BRUTE;
+    if (use_bvh) bvh_build(&bvh, sc);
+    ctx_t cx = {cam, sc, use_bvh ? &bvh : NULL, accel, seed, uniform_incl_scale(-0.5, 0.5), path, path_cap};
     rtwo_stats local = {0, 0, 0, 0};
     v3 c = trace(&cx, i, j, s, &local);
+    if (use_bvh) bvh_free(&bvh);
     st3(out_rgb, c);
     if (stats) {
         stats->samples += 1;
@@ -988,6 +1176,7 @@ void rtwo_trace_sample(const rtwo_camera *cam, const rtwo_scene *sc, uint64_t se
         stats->lambertian += local.lambertian;
         stats->nan_samples += (c.x != c.x || c.y != c.y || c.z != c.z);
     }
+    return (uint32_t)local.segments;
 }
 
 typedef struct {
@@ -1051,7 +1240,7 @@ int rtwo_render(const rtwo_camera *cam, const rtwo_scene *sc, uint64_t seed,
     bvh_t bvh;
     int use_bvh = accel != RTWO_ACCEL_BRUTE;
     if (use_bvh) bvh_build(&bvh, sc);
-    ctx_t cx = {cam, sc, use_bvh ? &bvh : NULL, accel, seed, uniform_incl_scale(-0.5, 0.5)};
+    ctx_t cx = {cam, sc, use_bvh ? &bvh : NULL, accel, seed, uniform_incl_scale(-0.5, 0.5), NULL, 0};
     uint32_t n_rows = row_begin < row_end ? (row_end - row_begin + row_step - 1) / row_step : 0;
     volatile uint32_t next_row = 0;
     worker_t *ws = (worker_t *)calloc((size_t)nthreads, sizeof(worker_t));

@@ -81,6 +81,12 @@ typedef struct rtwo_scene {
     /* light-list order: n_lights + n_light_quads kinds (0 sphere, 1 quad),
      * each taking the next entry of its array; NULL = spheres then quads */
     const uint32_t *light_kinds;
+    /* Transformed<Cuboid> (cuboid.rs:26-59, entities/transformations.rs,
+     * geometry/src/transformations.rs): Cuboid::new(p, q, mat) under the
+     * composed Transformation {rotation R (row-major), translation T} */
+    uint32_t n_boxes;
+    const double *boxes;        /* n x {p xyz, q xyz, R[3][3], T xyz} = 18 */
+    const uint32_t *box_mat;
 } rtwo_scene;
 
 typedef struct rtwo_stats {
@@ -100,6 +106,19 @@ double rtwo_quad_pdf_value(const double quad[9], const double o[3], const double
 void rtwo_quad_random(const double quad[9], const double o[3], uint64_t st[4], double out[3]);
 /* Quad::new's AABBox::from_points (aabox.rs:199-211, padded per enclose) */
 void rtwo_quad_aabb(const double quad[9], double box[6]);
+
+/* Transformed<Cuboid>::hit for one box record (18 doubles, see rtwo_scene):
+ * out = {t, world point xyz, normal xyz (object space, front-face adjusted
+ * against the object-space ray -- the reference does not transform it back),
+ * front}.  Returns 1 on a hit. */
+int rtwo_box_hit(const double box[18], const double o[3], const double d[3],
+                 double tmin, double tmax, double out[8]);
+/* its world-space AABB (Transformed::get_aabbox) */
+void rtwo_box_aabb(const double box[18], double aabb_out[6]);
+
+/* world.hit(&r, EPSILON..=INFINITY) for one ray with the given accel:
+ * object id (planes, quads, boxes, spheres) or -1; out = {t, p, normal, front} */
+int rtwo_world_hit(const rtwo_scene *sc, int accel, const double o[3], const double d[3], double out[8]);
 
 /* CameraBuilder::build, camera.rs:114-218. Returns 0. */
 int rtwo_camera_build(const rtwo_camera_builder *b, rtwo_camera *out);
@@ -121,6 +140,11 @@ int rtwo_render(const rtwo_camera *cam, const rtwo_scene *sc, uint64_t seed,
 void rtwo_trace_sample(const rtwo_camera *cam, const rtwo_scene *sc, uint64_t seed,
                        uint32_t i, uint32_t j, uint32_t s, double out_rgb[3],
                        rtwo_stats *stats);
+/* rtwo_trace_sample with an accel and (debugging) the path: per segment
+ * {origin xyz, direction xyz, hit object id or -1, t}; returns segments */
+uint32_t rtwo_trace_path(const rtwo_camera *cam, const rtwo_scene *sc, uint64_t seed, uint32_t i, uint32_t j,
+                         uint32_t s, int accel, double out_rgb[3], rtwo_stats *stats, double *path,
+                         uint32_t path_cap);
 
 /* scenes::simple (scenes/src/lib.rs:155-233) driven by the build's seeded
  * RNG; grid a,b in [-n, n) (the reference uses n = 11).  Writes at most

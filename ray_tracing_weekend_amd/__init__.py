@@ -16,6 +16,7 @@ row j = 0 at the BOTTOM, like render_internal's Vec<Vec<Colour>>.
 from __future__ import annotations
 
 import ctypes as C
+import math
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -94,6 +95,48 @@ class Quad:                                  # entities/quadrilateral.rs:21-56 (
     mat: Material = INVISIBLE
 
 
+@dataclass(frozen=True)
+class Transformation:
+    """geometry::transformations::Transformation (non-euclid build): point ->
+    R p + T.  `then` composes like the reference (transformations.rs:97-108)."""
+    R: tuple = ((1.0, 0.0, 0.0), (0.0, 1.0, 0.0), (0.0, 0.0, 1.0))
+    T: tuple = (0.0, 0.0, 0.0)
+
+    def then(self, b: "Transformation") -> "Transformation":
+        def dot(u, v):
+            return (u[0] * v[0] + u[1] * v[1]) + u[2] * v[2]
+        cols = [[self.R[0][j], self.R[1][j], self.R[2][j]] for j in range(3)]
+        R = tuple(tuple(dot(b.R[i], cols[j]) for j in range(3)) for i in range(3))
+        bRT = [dot(b.R[i], self.T) for i in range(3)]
+        return Transformation(R, tuple(b.T[i] + bRT[i] for i in range(3)))
+
+
+def translation(v) -> Transformation:        # Translation3 = Vec3 -> Transformation (vec3.rs:11)
+    return Transformation(T=tuple(map(float, v)))
+
+
+def rotation(angle_deg: float, axis: int) -> Transformation:   # transformations.rs:37-58 (axis 0/1/2 = X/Y/Z)
+    a = float(angle_deg) * (math.pi / 180.0)                  # f64::to_radians
+    c, s = math.cos(a), math.sin(a)                           # libm, as f64::cos / f64::sin
+    R = [((1.0, 0.0, 0.0), (0.0, c, -s), (0.0, s, c)),
+         ((c, 0.0, s), (0.0, 1.0, 0.0), (-s, 0.0, c)),
+         ((c, -s, 0.0), (s, c, 0.0), (0.0, 0.0, 1.0))][axis]
+    return Transformation(R=R)
+
+
+@dataclass(frozen=True)
+class Cuboid:                                # entities/cuboid.rs:26-47, Cuboid::new(p, q, mat)
+    p: tuple
+    q: tuple
+    mat: Material = INVISIBLE
+    xform: Transformation = Transformation()
+
+    def transform(self, t: Transformation) -> "Cuboid":
+        """Transformable::transform (transformations.rs:187-211): the
+        transformations compose in call order."""
+        return Cuboid(self.p, self.q, self.mat, self.xform.then(t))
+
+
 class HittableList:                          # hittable_collections/hittable_list.rs:247-294
     def __init__(self, objects=()):
         self.objects = []
@@ -101,8 +144,8 @@ class HittableList:                          # hittable_collections/hittable_lis
             self.add(o)
 
     def add(self, obj):
-        if not isinstance(obj, (Sphere, Plane, Quad)):
-            raise TypeError("only Sphere, Plane and Quad are in this build's scope")
+        if not isinstance(obj, (Sphere, Plane, Quad, Cuboid)):
+            raise TypeError("only Sphere, Plane, Quad and (transformed) Cuboid are in this build's scope")
         self.objects.append(obj)
 
     def __len__(self):
@@ -123,6 +166,8 @@ class SceneSoA:
     quad_mat: np.ndarray = field(default_factory=lambda: np.zeros(0, np.uint32))
     light_quads: np.ndarray = field(default_factory=lambda: np.zeros((0, 9)))
     light_kinds: np.ndarray = None          # list order: 0 sphere / 1 quad; None = spheres first
+    boxes: np.ndarray = field(default_factory=lambda: np.zeros((0, 18)))
+    box_mat: np.ndarray = field(default_factory=lambda: np.zeros(0, np.uint32))
 
     def as_c(self):
         """(rtw_scene, keepalive) -- the struct points into these arrays."""
@@ -144,7 +189,8 @@ class SceneSoA:
                             len(np.asarray(self.lights).reshape(-1, 4)), f(self.lights, 4),
                             len(self.quad_mat), f(self.quads, 9), u(self.quad_mat),
                             len(np.asarray(self.light_quads).reshape(-1, 9)), f(self.light_quads, 9),
-                            None if self.light_kinds is None else u(self.light_kinds))
+                            None if self.light_kinds is None else u(self.light_kinds),
+                            len(self.box_mat), f(self.boxes, 18), u(self.box_mat))
         return s, keep
 
     @staticmethod
@@ -160,7 +206,8 @@ class SceneSoA:
                         u(s.mat_type, s.n_materials), f(s.mat_params, s.n_materials, 5),
                         f(s.lights, s.n_lights, 4), f(s.quads, s.n_quads, 9), u(s.quad_mat, s.n_quads),
                         f(s.light_quads, s.n_light_quads, 9),
-                        u(s.light_kinds, s.n_lights + s.n_light_quads) if s.light_kinds else None)
+                        u(s.light_kinds, s.n_lights + s.n_light_quads) if s.light_kinds else None,
+                        f(s.boxes, s.n_boxes, 18), u(s.box_mat, s.n_boxes))
 
 
 def flatten(world, lights) -> SceneSoA:
@@ -184,6 +231,11 @@ def flatten(world, lights) -> SceneSoA:
         if isinstance(o, Quad):
             qd.append(list(o.q) + list(o.u) + list(o.v))
             qmat.append(push(o.mat))
+    bx, bmat = [], []
+    for o in world.objects:
+        if isinstance(o, Cuboid):
+            bx.append(list(o.p) + list(o.q) + [v for row in o.xform.R for v in row] + list(o.xform.T))
+            bmat.append(push(o.mat))
     for o in world.objects:
         if isinstance(o, Sphere):
             sph.append(list(o.center) + [o.radius])
@@ -203,7 +255,8 @@ def flatten(world, lights) -> SceneSoA:
                     np.array(mtypes, np.uint32), np.array(mats, np.float64).reshape(-1, 5),
                     np.array(li, np.float64).reshape(-1, 4), np.array(qd, np.float64).reshape(-1, 9),
                     np.array(qmat, np.uint32), np.array(lq, np.float64).reshape(-1, 9),
-                    np.array(kinds, np.uint32) if lq else None)
+                    np.array(kinds, np.uint32) if lq else None,
+                    np.array(bx, np.float64).reshape(-1, 18), np.array(bmat, np.uint32))
 
 
 # ---------------------------------------------------------------- camera
@@ -389,6 +442,25 @@ class scenes:                                 # scenes/src/lib.rs
         finally:
             _lib.rtw_world_free(w)
         return soa, CameraBuilder(b)
+
+    @staticmethod
+    def named_soa(name: str, seed: int = 0x5EED0001):
+        """(SceneSoA, CameraBuilder) of a reference scene by its main.rs name
+        ("simple", "cornell_box")."""
+        w = _lib.rtw_scene_named(name.encode(), C.c_uint64(seed & 0xFFFFFFFFFFFFFFFF))
+        if not w:
+            raise RenderError(_capi.RTW_E_UNSUPPORTED, f"scene {name!r} is not in this build")
+        try:
+            soa = SceneSoA.from_c(_lib.rtw_world_scene(w).contents)
+            b = _capi.rtw_camera_builder()
+            _lib.rtw_world_camera_builder(w, C.byref(b))
+        finally:
+            _lib.rtw_world_free(w)
+        return soa, CameraBuilder(b)
+
+    @staticmethod
+    def cornell_box_soa():
+        return scenes.named_soa("cornell_box")
 
     @staticmethod
     def simple(seed: int = 0x5EED0001, n: int = 11):

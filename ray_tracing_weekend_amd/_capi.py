@@ -56,10 +56,11 @@ class rtw_scene(C.Structure):
         ("n_lights", C.c_uint32), ("lights", _f64p),
         ("n_quads", C.c_uint32), ("quads", _f64p), ("quad_mat", _u32p),
         ("n_light_quads", C.c_uint32), ("light_quads", _f64p), ("light_kinds", _u32p),
+        ("n_boxes", C.c_uint32), ("boxes", _f64p), ("box_mat", _u32p),
     ]
 
 
-ABI_VERSION = 3     # RTW_ABI_VERSION of include/rtw.h
+ABI_VERSION = 4     # RTW_ABI_VERSION of include/rtw.h
 
 
 class rtw_stats(C.Structure):
@@ -96,6 +97,7 @@ PROTOTYPES = [
     ("rtw_world_scene", C.POINTER(rtw_scene), [C.c_void_p]),
     ("rtw_world_camera_builder", None, [C.c_void_p, C.POINTER(rtw_camera_builder)]),
     ("rtw_world_free", None, [C.c_void_p]),
+    ("rtw_scene_named", C.c_void_p, [C.c_char_p, C.c_uint64]),
     ("rtw_encode_rgb8", C.c_int, [_f64p, C.c_uint32, C.c_uint32, C.c_uint32,
                                   C.POINTER(C.c_uint8)]),
     ("rtw_write_ppm", C.c_int, [C.c_char_p, _f64p, C.c_uint32, C.c_uint32, C.c_uint32]),

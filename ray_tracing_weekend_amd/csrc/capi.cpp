@@ -125,6 +125,93 @@ void quad_derive(const double* p, double* out) {
     out[22] = out[23] = 0.0;
 }
 
+// Transformed<Cuboid> derived record in f64, in the oracle's operation order
+// (rtw_oracle.c box_new); layout rtw_kernels.h kBoxR.
+void box_derive(const double* b, double* out) {
+    auto enclose_pad = [](double* mn, double* mx, const double* pmn, const double* pmx) {
+        for (int a = 0; a < 3; ++a) {
+            mn[a] = fmin(mn[a], pmn[a]);
+            mx[a] = fmax(mx[a], pmx[a]);
+        }
+        for (int a = 0; a < 3; ++a)
+            if (mx[a] - mn[a] < 0.0001) {
+                mn[a] -= 0.0001;
+                mx[a] += 0.0001;
+            }
+    };
+    // Cuboid::new: the padded box of p and q, then the six quads
+    double mn[3] = {b[0], b[1], b[2]}, mx[3] = {b[0], b[1], b[2]};
+    enclose_pad(mn, mx, b + 3, b + 3);
+    const double delta[3] = {mx[0] - mn[0], mx[1] - mn[1], mx[2] - mn[2]};
+    const double dx[3] = {delta[0], 0.0, 0.0}, dy[3] = {0.0, delta[1], 0.0}, dz[3] = {0.0, 0.0, delta[2]};
+    const double ndx[3] = {-dx[0], -dx[1], -dx[2]}, ndy[3] = {-dy[0], -dy[1], -dy[2]},
+                 ndz[3] = {-dz[0], -dz[1], -dz[2]};
+    const double* args[6][3] = {{mn, dx, dy}, {mn, dy, dz}, {mn, dx, dz}, {mx, ndx, ndy}, {mx, ndy, ndz}, {mx, ndx, ndz}};
+    double cmn[3] = {0, 0, 0}, cmx[3] = {0, 0, 0};
+    for (int i = 0; i < 6; ++i) {
+        double q[9];
+        for (int a = 0; a < 3; ++a) {
+            q[a] = args[i][0][a];
+            q[3 + a] = args[i][1][a];
+            q[6 + a] = args[i][2][a];
+        }
+        double* Q = out + rtw::kQuadR * i;
+        quad_derive(q, Q);
+        // Cuboid::get_aabbox: fold of the quads' boxes
+        if (i == 0) {
+            for (int a = 0; a < 3; ++a) {
+                cmn[a] = Q[16 + a];
+                cmx[a] = Q[19 + a];
+            }
+        } else {
+            enclose_pad(cmn, cmx, Q + 16, Q + 19);
+        }
+    }
+    double* Rm = out + rtw::kBoxRot;
+    for (int k = 0; k < 9; ++k) Rm[k] = b[6 + k];
+    for (int a = 0; a < 3; ++a) out[rtw::kBoxT + a] = b[15 + a];
+    auto mul = [&](const double* M, const double* p, double* o) {
+        for (int r = 0; r < 3; ++r) o[r] = M[3 * r] * p[0] + M[3 * r + 1] * p[1] + M[3 * r + 2] * p[2];
+    };
+    // world AABB: from_points of the cuboid box corners (get_points order) mapped by R p + T
+    const double* lo = cmn;
+    const double* hi = cmx;
+    const double corners[8][3] = {{lo[0], lo[1], lo[2]}, {lo[0], hi[1], lo[2]}, {lo[0], lo[1], hi[2]},
+                                  {lo[0], hi[1], hi[2]}, {hi[0], lo[1], lo[2]}, {hi[0], hi[1], lo[2]},
+                                  {hi[0], lo[1], hi[2]}, {hi[0], hi[1], hi[2]}};
+    double wmn[3], wmx[3];
+    for (int i = 0; i < 8; ++i) {
+        double w[3];
+        mul(Rm, corners[i], w);
+        for (int a = 0; a < 3; ++a) w[a] = w[a] + b[15 + a];
+        if (i == 0) {
+            for (int a = 0; a < 3; ++a) wmn[a] = wmx[a] = w[a];
+        } else {
+            enclose_pad(wmn, wmx, w, w);
+        }
+    }
+    for (int a = 0; a < 3; ++a) {
+        out[rtw::kBoxLo + a] = wmn[a];
+        out[rtw::kBoxHi + a] = wmx[a];
+    }
+    // Matrix3::inverse (matrix3.rs:9-28), Transformation::inverse
+    const double a = Rm[0], bb = Rm[1], c = Rm[2], d = Rm[3], e = Rm[4], f = Rm[5], g = Rm[6], h = Rm[7],
+                 i = Rm[8];
+    const double det = a * (e * i - f * h) + bb * (f * g - d * i) + c * (d * h - e * g);
+    out[rtw::kBoxOk] = std::isnormal(det) ? 1.0 : 0.0;
+    const double A = e * i - f * h, Bc = f * g - d * i, C = d * h - e * g;
+    const double D = c * h - bb * i, E = a * i - c * g, F = bb * g - a * h;
+    const double G = bb * f - c * e, H = c * d - a * f, I = a * e - bb * d;
+    double* Ri = out + rtw::kBoxInv;
+    Ri[0] = A / det; Ri[1] = D / det; Ri[2] = G / det;
+    Ri[3] = Bc / det; Ri[4] = E / det; Ri[5] = H / det;
+    Ri[6] = C / det; Ri[7] = F / det; Ri[8] = I / det;
+    double rt[3];
+    mul(Ri, b + 15, rt);
+    for (int a2 = 0; a2 < 3; ++a2) out[rtw::kBoxTi + a2] = -rt[a2];
+    out[rtw::kBoxOk + 1] = 0.0;
+}
+
 // Convert the caller's f64 SoA into the device layout of precision R, in one
 // host staging blob, and fill the DevScene pointers relative to `base`.
 template <typename R>
@@ -146,6 +233,8 @@ std::vector<unsigned char> stage_scene(const rtw_scene* s, rtw::DevScene<R>* ds,
     const size_t o_lquads = reserve(sizeof(R) * rtw::kQuadR * s->n_light_quads);
     const uint32_t n_list = s->n_lights + s->n_light_quads;
     const size_t o_lref = reserve(sizeof(uint32_t) * n_list);
+    const size_t o_boxes = reserve(sizeof(R) * rtw::kBoxR * s->n_boxes);
+    const size_t o_bmat = reserve(sizeof(uint32_t) * s->n_boxes);
     const size_t o_pmat = reserve(sizeof(uint32_t) * s->n_planes);
     const size_t o_mt = reserve(sizeof(uint32_t) * s->n_materials);
     const size_t o_mp = reserve(sizeof(R4) * s->n_materials);
@@ -220,6 +309,24 @@ std::vector<unsigned char> stage_scene(const rtw_scene* s, rtw::DevScene<R>* ds,
     }
     for (uint32_t k = 0; k < s->n_light_quads; ++k)
         put_quad(s->light_quads + 9 * k, reinterpret_cast<R*>(b + o_lquads) + rtw::kQuadR * k);
+    for (uint32_t k = 0; k < s->n_boxes; ++k) {
+        double bx[rtw::kBoxR];
+        box_derive(s->boxes + 18 * k, bx);
+        R* dst = reinterpret_cast<R*>(b + o_boxes) + rtw::kBoxR * k;
+        for (uint32_t a = 0; a < rtw::kBoxR; ++a) dst[a] = (R)bx[a];
+        auto outward = [&](uint32_t lo_at, uint32_t hi_at) {   // AABBs round outward (culls only)
+            for (int a = 0; a < 3; ++a) {
+                R lo = (R)bx[lo_at + a], hi = (R)bx[hi_at + a];
+                if ((double)lo > bx[lo_at + a]) lo = std::nextafter(lo, (R)-INFINITY);
+                if ((double)hi < bx[hi_at + a]) hi = std::nextafter(hi, (R)INFINITY);
+                dst[lo_at + a] = lo;
+                dst[hi_at + a] = hi;
+            }
+        };
+        outward(rtw::kBoxLo, rtw::kBoxHi);
+        for (uint32_t qd = 0; qd < 6; ++qd) outward(rtw::kQuadR * qd + 16, rtw::kQuadR * qd + 19);
+        reinterpret_cast<uint32_t*>(b + o_bmat)[k] = s->box_mat[k];
+    }
     {
         uint32_t ns = 0, nq = 0;
         for (uint32_t k = 0; k < n_list; ++k) {
@@ -253,6 +360,9 @@ std::vector<unsigned char> stage_scene(const rtw_scene* s, rtw::DevScene<R>* ds,
     ds->n_quads = s->n_quads;
     ds->n_lquads = s->n_light_quads;
     ds->n_list = n_list;
+    ds->boxes = reinterpret_cast<const R*>(base + o_boxes);
+    ds->box_mat = reinterpret_cast<const uint32_t*>(base + o_bmat);
+    ds->n_boxes = s->n_boxes;
     // round box bounds outward into precision R
     auto down = [](double x) {
         R r = (R)x;
@@ -347,7 +457,8 @@ int validate_scene(rtw_ctx* c, const rtw_scene* s) {
     if (!s) return fail(c, RTW_E_INVALID, "scene is NULL");
     if ((s->n_spheres && (!s->spheres || !s->sphere_mat)) || (s->n_planes && (!s->planes || !s->plane_mat)) ||
         (s->n_materials && (!s->mat_type || !s->mat_params)) || (s->n_lights && !s->lights) ||
-        (s->n_quads && (!s->quads || !s->quad_mat)) || (s->n_light_quads && !s->light_quads))
+        (s->n_quads && (!s->quads || !s->quad_mat)) || (s->n_light_quads && !s->light_quads) ||
+        (s->n_boxes && (!s->boxes || !s->box_mat)))
         return fail(c, RTW_E_INVALID, "scene array pointer is NULL");
     if (s->light_kinds) {
         uint32_t nq = 0;
@@ -365,6 +476,8 @@ int validate_scene(rtw_ctx* c, const rtw_scene* s) {
         if (s->plane_mat[k] >= s->n_materials) return fail(c, RTW_E_INVALID, "plane material id out of range");
     for (uint32_t k = 0; k < s->n_quads; ++k)
         if (s->quad_mat[k] >= s->n_materials) return fail(c, RTW_E_INVALID, "quad material id out of range");
+    for (uint32_t k = 0; k < s->n_boxes; ++k)
+        if (s->box_mat[k] >= s->n_materials) return fail(c, RTW_E_INVALID, "box material id out of range");
     if (lambertian && s->n_lights + s->n_light_quads == 0)
         return fail(c, RTW_E_NO_LIGHTS, "Lambertian material with an empty light list "
                                         "(the reference panics: HittableList shouldn't be empty)");
@@ -738,8 +851,9 @@ int rtw_set_scene(rtw_ctx* c, const rtw_scene* s) {
         fix(ds.bvh4); fix(ds.lbvh); fix(ds.lsph); fix(ds.lid);
         fix(ds.quads); fix(ds.quad_mat); fix(ds.lquads);
         if (ds.lref) fix(ds.lref);
+        fix(ds.boxes); fix(ds.box_mat);
     };
-    static_assert(offsetof(rtw::DevScene<float>, n_sph) == 19 * sizeof(void*),
+    static_assert(offsetof(rtw::DevScene<float>, n_sph) == 21 * sizeof(void*),
                   "DevScene gained a pointer: update rebase");
     if (c->precision == RTW_F32) {
         rebase(tmp32);
@@ -862,6 +976,24 @@ void rtw_world_camera_builder(const rtw_world* w, rtw_camera_builder* out) {
     if (w && out) *out = w->cam;
 }
 void rtw_world_free(rtw_world* w) { delete w; }
+
+rtw_world* rtw_scene_named(const char* name, uint64_t seed) {
+    if (!name) return nullptr;
+    const std::string n = name;
+    if (n == "simple") return rtw_scene_simple(seed, 11);
+    try {
+        if (n == "cornell_box") {
+            auto t = rtw::scenes::cornell_box();
+            rtw_world* w = new rtw_world();
+            w->flat = rtw::flatten(std::get<0>(t), std::get<1>(t));
+            w->view = w->flat.view();
+            w->cam = std::get<2>(t).raw();
+            return w;
+        }
+    } catch (...) {
+    }
+    return nullptr;
+}
 
 // ------------------------------------------------------------ output encoding
 static uint8_t to_u8(double x) {

@@ -5,7 +5,7 @@
 //
 //   rtw <scene> [--debug] [--seed N] [--f64] [--device N] [--config PATH] [--out PATH]
 //
-// Only the `simple` scene is in this build's scope; the other
+// The `simple` and `cornell_box` scenes are in this build's scope; the other
 // reference scenes need Quad/Cuboid/DiffuseLight/textures (§8f).
 #include <math.h>
 #include <stdio.h>
@@ -63,8 +63,9 @@ int main(int argc, char** argv) {
         else if (scene.empty()) scene = s;
         else { fprintf(stderr, "unexpected argument %s\n", s.c_str()); return 2; }
     }
-    if (scene != "simple") {
-        fprintf(stderr, "scene '%s' is not in this build's scope (supported: simple)\n", scene.c_str());
+    if (scene != "simple" && scene != "cornell_box") {
+        fprintf(stderr, "scene '%s' is not in this build's scope (supported: simple, cornell_box)\n",
+                scene.c_str());
         return 2;
     }
     std::map<std::string, std::string> kv;
@@ -87,7 +88,7 @@ int main(int argc, char** argv) {
     const uint32_t spp = (uint32_t)atol(kv["samples_per_pixel"].c_str());
     const uint32_t depth = (uint32_t)atol(kv["max_depth"].c_str());
 
-    auto [world, lights, builder] = rtw::scenes::simple(opt.seed);
+    auto [world, lights, builder] = scene == "cornell_box" ? rtw::scenes::cornell_box() : rtw::scenes::simple(opt.seed);
     try {
         rtw::Camera cam = builder.with_vfov(40.0)
                               .with_aspect_ratio(aspect)

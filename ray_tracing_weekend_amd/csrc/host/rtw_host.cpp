@@ -83,7 +83,40 @@ rtw_scene FlatScene::view() const {
     s.n_light_quads = (uint32_t)(light_quads.size() / 9);
     s.light_quads = light_quads.data();
     s.light_kinds = light_kinds.empty() ? nullptr : light_kinds.data();
+    s.n_boxes = (uint32_t)box_mat.size();
+    s.boxes = boxes.data();
+    s.box_mat = box_mat.data();
     return s;
+}
+
+// ---------------------------------------------------------------- Transformation
+Transformation Transformation::then(const Transformation& b) const {
+    // apply(b): rotation = b.R * R, translation = b.T + b.R * T
+    Transformation out;
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) out.R[i][j] = b.R[i][0] * R[0][j] + b.R[i][1] * R[1][j] + b.R[i][2] * R[2][j];
+    const double rt[3] = {b.R[0][0] * T.x + b.R[0][1] * T.y + b.R[0][2] * T.z,
+                          b.R[1][0] * T.x + b.R[1][1] * T.y + b.R[1][2] * T.z,
+                          b.R[2][0] * T.x + b.R[2][1] * T.y + b.R[2][2] * T.z};
+    out.T = {b.T.x + rt[0], b.T.y + rt[1], b.T.z + rt[2]};
+    return out;
+}
+Transformation Transformation::translation(Vec3 t) {
+    Transformation out;
+    out.T = t;
+    return out;
+}
+Transformation Transformation::rotation(double angle_deg, int axis) {
+    const double a = angle_deg * (3.14159265358979323846 / 180.0);   // f64::to_radians
+    const double c = cos(a), s = sin(a);
+    Transformation out;
+    const double X[3][3] = {{1, 0, 0}, {0, c, -s}, {0, s, c}};
+    const double Y[3][3] = {{c, 0, s}, {0, 1, 0}, {-s, 0, c}};
+    const double Z[3][3] = {{c, -s, 0}, {s, c, 0}, {0, 0, 1}};
+    const double(*M)[3] = axis == 0 ? X : (axis == 1 ? Y : Z);
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) out.R[i][j] = M[i][j];
+    return out;
 }
 
 FlatScene flatten(const HittableList& world, const HittableList& lights) {
@@ -106,8 +139,15 @@ FlatScene flatten(const HittableList& world, const HittableList& lights) {
         f.quads.insert(f.quads.end(), {q.q.x, q.q.y, q.q.z, q.u.x, q.u.y, q.u.z, q.v.x, q.v.y, q.v.z});
         f.quad_mat.push_back(push_mat(q.mat));
     }
-    if (!lights.planes().empty())
-        throw Error(RTW_E_UNSUPPORTED, "planes as lights are outside this build's scope");
+    for (const Cuboid& c : world.cuboids()) {
+        f.boxes.insert(f.boxes.end(), {c.p.x, c.p.y, c.p.z, c.q.x, c.q.y, c.q.z});
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j) f.boxes.push_back(c.xform.R[i][j]);
+        f.boxes.insert(f.boxes.end(), {c.xform.T.x, c.xform.T.y, c.xform.T.z});
+        f.box_mat.push_back(push_mat(c.mat));
+    }
+    if (!lights.planes().empty() || !lights.cuboids().empty())
+        throw Error(RTW_E_UNSUPPORTED, "planes and cuboids as lights are outside this build's scope");
     for (const auto& e : lights.order()) {
         if (e.first == HittableList::kSphere) {
             const Sphere& s = lights.spheres()[e.second];
@@ -219,6 +259,34 @@ std::tuple<HittableList, HittableList, CameraBuilder> simple(uint64_t seed, int 
         .with_focus_dist(sqrt(vdot(d, d)))
         .with_vfov(40.0)
         .with_background({1, 1, 1});
+    return {std::move(world), std::move(lights), cam};
+}
+
+std::tuple<HittableList, HittableList, CameraBuilder> cornell_box() {
+    // scenes/src/lib.rs:292-395
+    HittableList world, lights;
+    const Material red = Material::lambertian({0.65, 0.05, 0.05});
+    const Material white = Material::lambertian({0.73, 0.73, 0.73});
+    const Material green = Material::lambertian({0.12, 0.45, 0.15});
+    const Material light = Material::diffuse_light({15.0, 15.0, 15.0});
+    const Material glass = Material::dialectric(1.5);
+    world.add(Quad{{555, 0, 0}, {0, 555, 0}, {0, 0, 555}, green});
+    world.add(Quad{{0, 0, 0}, {0, 555, 0}, {0, 0, 555}, red});
+    world.add(Quad{{0, 0, 0}, {555, 0, 0}, {0, 0, 555}, white});
+    world.add(Quad{{0, 555, 0}, {555, 0, 0}, {0, 0, 555}, white});
+    world.add(Quad{{0, 0, 555}, {0, 555, 0}, {555, 0, 0}, white});
+    world.add(Cuboid{{0, 0, 0}, {165, 330, 165}, white}
+                  .transform(Transformation::translation({265, 0, 295}))
+                  .transform(Transformation::rotation(15.0, 1)));
+    world.add(Sphere{{190, 90, 190}, 90.0, glass});
+    world.add(Quad{{343, 554, 332}, {-130, 0, 0}, {0, 0, -105}, light});
+    lights.add(Quad{{343, 554, 332}, {-130, 0, 0}, {0, 0, -105}, light});
+    lights.add(Sphere{{190, 90, 190}, 90.0, glass});
+    const Point3 lookfrom{277.5, 277.5, -800.0}, lookat{277.5, 277.5, 0.0};
+    const Vec3 d{lookfrom.x - lookat.x, lookfrom.y - lookat.y, lookfrom.z - lookat.z};
+    CameraBuilder cam;
+    cam.with_lookfrom(lookfrom).with_lookat(lookat).with_vfov(40.0).with_defocus_angle(0.0).with_focus_dist(
+        sqrt(vdot(d, d)));
     return {std::move(world), std::move(lights), cam};
 }
 }  // namespace scenes

@@ -68,15 +68,39 @@ struct Quad {
     Material mat;
 };
 
+// geometry::transformations::Transformation (non-euclid build): p -> R p + T;
+// then() composes in call order (transformations.rs:97-108).
+struct Transformation {
+    double R[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}};
+    Vec3 T{};
+    Transformation then(const Transformation& b) const;
+    static Transformation translation(Vec3 t);
+    static Transformation rotation(double angle_deg, int axis);   // axis 0/1/2 = X/Y/Z
+};
+
+// Cuboid::new(p, q, mat) (cuboid.rs:26-47), optionally .transform()ed
+struct Cuboid {
+    Point3 p, q;
+    Material mat;
+    Transformation xform{};
+    Cuboid transform(const Transformation& t) const {
+        Cuboid c = *this;
+        c.xform = xform.then(t);
+        return c;
+    }
+};
+
 // A world or light list.  The primitives this build renders: Sphere, Plane,
-// Quad (Triangle/Cuboid/Transformed are SURVEY.md §8f rank 4).  Insertion
-// order is kept: it is the light list's order (pdf sum, uniform pick).
+// Quad, (transformed) Cuboid; Triangle is outside it.  Insertion order is
+// kept: it is the light list's order (pdf sum, uniform pick).
 class HittableList {
    public:
-    enum Kind : uint8_t { kSphere, kPlane, kQuad };
+    enum Kind : uint8_t { kSphere, kPlane, kQuad, kCuboid };
     void add(const Sphere& s) { order_.push_back({kSphere, spheres_.size()}); spheres_.push_back(s); }
     void add(const Plane& p) { order_.push_back({kPlane, planes_.size()}); planes_.push_back(p); }
     void add(const Quad& q) { order_.push_back({kQuad, quads_.size()}); quads_.push_back(q); }
+    void add(const Cuboid& c) { order_.push_back({kCuboid, cuboids_.size()}); cuboids_.push_back(c); }
+    const std::vector<Cuboid>& cuboids() const { return cuboids_; }
     size_t len() const { return order_.size(); }
     bool is_empty() const { return len() == 0; }
     const std::vector<Sphere>& spheres() const { return spheres_; }
@@ -88,13 +112,14 @@ class HittableList {
     std::vector<Sphere> spheres_;
     std::vector<Plane> planes_;
     std::vector<Quad> quads_;
+    std::vector<Cuboid> cuboids_;
     std::vector<std::pair<Kind, size_t>> order_;
 };
 
 // Flattened (SoA) world + lights; owns the arrays an rtw_scene points into.
 struct FlatScene {
-    std::vector<double> spheres, planes, quads, mat_params, lights, light_quads;
-    std::vector<uint32_t> sphere_mat, plane_mat, quad_mat, mat_type, light_kinds;
+    std::vector<double> spheres, planes, quads, mat_params, lights, light_quads, boxes;
+    std::vector<uint32_t> sphere_mat, plane_mat, quad_mat, mat_type, light_kinds, box_mat;
     rtw_scene view() const;
 };
 // world's spheres/planes/quads with one material record each; lights
@@ -166,6 +191,8 @@ class Camera {
 namespace scenes {
 // scenes::simple restated with the build's seeded RNG; grid a, b in [-n, n).
 std::tuple<HittableList, HittableList, CameraBuilder> simple(uint64_t seed, int n = 11);
+// scenes::cornell_box (scenes/src/lib.rs:292-395)
+std::tuple<HittableList, HittableList, CameraBuilder> cornell_box();
 }  // namespace scenes
 
 // host RNG used by the scene generator (the same xoshiro256++/splitmix64 and

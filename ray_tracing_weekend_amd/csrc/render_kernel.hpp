@@ -69,6 +69,36 @@ __device__ __forceinline__ bool aabb_hit_ref(const R* lo, const R* hi, V3<R> o, 
     return P<R>::max_(rs, tmin) <= P<R>::min_((R)INFINITY, tmax);
 }
 
+// Transformed<Cuboid>::hit (entities/transformations.rs:14-29, cuboid.rs:50-58)
+// on the staged record B (rtw_kernels.h kBoxR), as the oracle's box_hit: the
+// ray into object space through the inverse (the direction ALSO gets the
+// translation, geometry/src/transformations.rs:112-114 -- the reference's
+// behaviour), the closest of the six quads (first minimum wins).
+template <typename R>
+__device__ __forceinline__ V3<R> mat3_mul(const R* M, V3<R> p) {   // Mul<Vec3> for Matrix3
+    return mk(dot(q3(M, 0), p), dot(q3(M, 3), p), dot(q3(M, 6), p));
+}
+template <typename R>
+__device__ __forceinline__ bool box_t_hit(const R* B, V3<R> o, V3<R> d, R tmin, R tmax, R& t, int& quad,
+                                          V3<R>& o2, V3<R>& d2) {
+    if (B[kBoxOk] == (R)0) return false;
+    o2 = mat3_mul(B + kBoxInv, o) + q3(B, kBoxTi);
+    d2 = mat3_mul(B + kBoxInv, d) + q3(B, kBoxTi);
+    int best = -1;
+    R bt = (R)INFINITY;
+    for (int k = 0; k < 6; ++k) {
+        R tt;
+        if (quad_t_hit(B + kQuadR * k, o2, d2, tmin, tmax, tt) && (best < 0 || tt < bt)) {
+            bt = tt;
+            best = k;
+        }
+    }
+    if (best < 0) return false;
+    t = bt;
+    quad = best;
+    return true;
+}
+
 // Closest sphere of a contiguous list [0, n), ids base + k.  Semantics of the
 // reference's closest hit: t = near root if it lies in [tmin, inf], else the
 // far root (sphere.rs:71-80); the smallest t wins, the lowest id on ties.
@@ -766,7 +796,8 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? 5 : 1) render_kernel(
     const R tmin = PR::kEps;
     const int32_t nplanes = (int32_t)p.sc.n_planes;
     const int32_t nquads = (int32_t)p.sc.n_quads;
-    const int32_t sbase = nplanes + nquads;   // object ids: planes, quads, spheres
+    const int32_t bbase = nplanes + nquads;                  // object ids: planes, quads,
+    const int32_t sbase = bbase + (int32_t)p.sc.n_boxes;     // boxes, spheres
 
     // per-lane item state
     uint32_t q = lane;            // item index in the task's pool
@@ -879,6 +910,18 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? 5 : 1) render_kernel(
                     best = nplanes + k;
                 }
             }
+            // transformed cuboids, each behind its world AABB
+            for (int32_t k = 0; k < (int32_t)p.sc.n_boxes; ++k) {
+                R t;
+                int qd;
+                V3<R> o2, d2;
+                const R* B = p.sc.boxes + kBoxR * k;
+                if (aabb_hit_ref(B + kBoxLo, B + kBoxHi, o, d, tmin) &&
+                    box_t_hit(B, o, d, tmin, (R)INFINITY, t, qd, o2, d2) && (best < 0 || t < tb)) {
+                    tb = t;
+                    best = bbase + k;
+                }
+            }
             if constexpr (kWorld >= kWorldBvh) {
 #if RTW_EXP == 1
                 {
@@ -909,11 +952,28 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? 5 : 1) render_kernel(
                 V3<R> outward;
                 uint32_t m;
                 int32_t next_self = -1;
-                if (best < nplanes) {
+                bool box_hit = false;
+                bool box_front = false;
+                if (best >= bbase && best < sbase) {
+                    // Transformed<Cuboid>: the record of the object-space hit,
+                    // its point mapped back (transform_point3d); the normal and
+                    // front face stay in object space (transformations.rs:14-29)
+                    const R* B = p.sc.boxes + kBoxR * (best - bbase);
+                    R t2;
+                    int qd = 0;
+                    V3<R> o2, d2;
+                    box_t_hit(B, o, d, tmin, (R)INFINITY, t2, qd, o2, d2);
+                    const V3<R> n = q3(B + kQuadR * qd, 12);
+                    box_front = dot(d2, n) < (R)0;
+                    outward = n;
+                    pnt = mat3_mul(B + kBoxRot, o2 + d2 * t2) + q3(B, kBoxT);
+                    m = p.sc.box_mat[best - bbase];
+                    box_hit = true;
+                } else if (best < nplanes) {
                     const R* pl = p.sc.planes + 12 * best;
                     outward = mk(pl[3], pl[4], pl[5]);
                     m = p.sc.plane_mat[best];
-                } else if (best < sbase) {
+                } else if (best < bbase) {
                     const R* Q = p.sc.quads + kQuadR * (best - nplanes);
                     outward = q3(Q, 12);                           // quadrilateral.rs:97
                     m = p.sc.quad_mat[best - nplanes];
@@ -925,7 +985,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? 5 : 1) render_kernel(
                     m = mw & 0x7fffffffu;
                     next_self = (mw >> 31) ? (int32_t)k : -1;   // bit 31: isolated sphere
                 }
-                const bool front = dot(d, outward) < (R)0;
+                const bool front = box_hit ? box_front : dot(d, outward) < (R)0;
                 const V3<R> nrm = front ? outward : -outward;
                 const uint32_t mtype = p.sc.mat_type[m];
                 const R4<R> mp = p.sc.mat_p[m];

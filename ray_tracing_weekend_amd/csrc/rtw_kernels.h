@@ -93,16 +93,27 @@ struct DevScene {
     const R* lquads;                  // the light list's quads, n_lquads x kQuadR
     const uint32_t* lref;             // light list in order: bit 31 = quad, low bits = index
                                       // (null when the list is spheres only)
+    const R* boxes;                   // n_boxes x kBoxR (transformed cuboids, layout below)
+    const uint32_t* box_mat;
     uint32_t n_sph, n_planes, n_mat, n_lights, n_nodes, bvh_depth;
     uint32_t n_nodes4, bvh4_stack, n_lnodes, lbvh_depth;
     uint32_t robust;                  // f32: closest-approach sphere / light tests (far geometry)
     uint32_t n_quads, n_lquads, n_list;   // world quads, light quads, light-list length
+    uint32_t n_boxes;
 };
 
 // Quad record (Quad::new's derived fields, quadrilateral.rs:37-56), kQuadR
 // values of precision R: Q[0..2], u[3..5], v[6..8], w = n/|n|^2 [9..11],
 // unit normal [12..14], area [15], AABB lo [16..18], hi [19..21], pad.
 constexpr uint32_t kQuadR = 24;
+
+// Transformed<Cuboid> record, kBoxR values of precision R: the six object-
+// space quads (6 x kQuadR), rotation R [144..152] and its inverse [153..161]
+// (row-major), translation T [162..164], -(R^-1 T) [165..167], world AABB lo
+// [168..170] hi [171..173], invertible flag [174], pad.
+constexpr uint32_t kBoxR = 176;
+constexpr uint32_t kBoxRot = 144, kBoxInv = 153, kBoxT = 162, kBoxTi = 165, kBoxLo = 168, kBoxHi = 171,
+                   kBoxOk = 174;
 
 constexpr uint32_t kBvhStack = 32;    // per-lane traversal stack entries (LDS)
 

@@ -50,11 +50,12 @@ def _render_gpu(soa, cam, seed, precision, chunk=0, accel=rtw.RTW_ACCEL_AUTO, bv
         return img, r.stats.chunk, (r.stats.segments, r.stats.lambertian)
 
 
-def _render_oracle(soa, cam, seed, chunk):
+def _render_oracle(soa, cam, seed, chunk, accel=None):
     ocam = O.Camera()
     for name, _ in O.Camera._fields_:
         setattr(ocam, name, getattr(cam.raw, name))
-    img, st = O.render(ocam, O.Scene(**soa.__dict__), seed, chunk=chunk, accel=O.ACCEL_BVH_CACHED)
+    img, st = O.render(ocam, O.Scene(**soa.__dict__), seed, chunk=chunk,
+                       accel=O.ACCEL_BVH_CACHED if accel is None else accel)
     return img, st
 
 
@@ -475,3 +476,32 @@ def test_diffuse_light_quad_is_its_colour():
         gpu, _, (segs, lambs) = _render_gpu(soa, cam, 3, prec)
         np.testing.assert_array_equal(gpu, np.broadcast_to([20.0, 10.0, 5.0], gpu.shape))
         assert segs == 8 * 6 * 5 and lambs == 0
+
+
+def test_cornell_box_f64_matches_oracle():
+    """scenes::cornell_box (scenes/src/lib.rs:292-395) in full: walls, light,
+    glass sphere and the translated + rotated Cuboid (Transformed<Cuboid>
+    with the reference's direction-translation behaviour).  The reference
+    world is a flat HittableList (lib.rs:297, :392), so the oracle runs brute
+    force: coplanar ties (floor vs the cuboid's bottom face) go to the first
+    type group, as HittableList::hit's min_by does (hittable_list.rs:395-406)."""
+    soa, b = rtw.scenes.cornell_box_soa()
+    assert len(soa.box_mat) == 1 and soa.light_kinds.tolist() == [1, 0]
+    cam = b.with_image_width(40).with_image_height(40).with_samples_per_pixel(4).with_max_depth(20).build()
+    for accel in (rtw.RTW_ACCEL_BRUTE, rtw.RTW_ACCEL_BVH):
+        gpu, chunk, (segs, lambs) = _render_gpu(soa, cam, 71, rtw.RTW_F64, accel=accel)
+        ref, st = _render_oracle(soa, cam, 71, chunk, O.ACCEL_BRUTE)
+        mae, exact = _compare_f64(gpu, ref, 4)
+        assert mae < F64_MAE_TOL and exact > 0.999, (accel, mae, exact)
+        assert segs == st.segments and lambs == st.lambertian
+
+
+def test_cornell_box_f32_tracks_f64():
+    soa, b = rtw.scenes.cornell_box_soa()
+    cam = b.with_image_width(48).with_image_height(48).with_samples_per_pixel(32).with_max_depth(20).build()
+    brute, _, cb = _render_gpu(soa, cam, 73, rtw.RTW_F32, accel=rtw.RTW_ACCEL_BRUTE)
+    bvh, _, cv = _render_gpu(soa, cam, 73, rtw.RTW_F32, accel=rtw.RTW_ACCEL_BVH)
+    assert _same(brute, bvh) and cb == cv
+    ref, _ = _render_oracle(soa, cam, 73, 0, O.ACCEL_BRUTE)
+    ok = ~(np.isnan(bvh).any(-1) | np.isnan(ref).any(-1))
+    assert abs(bvh[ok].mean() - ref[ok].mean()) < 0.03 * ref[ok].mean()

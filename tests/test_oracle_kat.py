@@ -409,3 +409,69 @@ def test_quad_world_bvh_variants_equal_brute_force():
     imgs = [O.render(cam, sc, 9, accel=a)[0] for a in (O.ACCEL_BRUTE, O.ACCEL_BVH_REF, O.ACCEL_BVH_CACHED)]
     for im in imgs[1:]:
         np.testing.assert_array_equal(np.nan_to_num(im, nan=-7), np.nan_to_num(imgs[0], nan=-7))
+
+
+# ---- Transformed<Cuboid> (cuboid.rs, entities/transformations.rs, geometry transformations.rs)
+
+def _box(p, q, R=((1, 0, 0), (0, 1, 0), (0, 0, 1)), T=(0, 0, 0)):
+    return list(p) + list(q) + [float(v) for row in R for v in row] + list(map(float, T))
+
+
+def test_identity_box_is_the_cuboid_six_quads():
+    b = _box((0, 0, 0), (2, 3, 4))
+    t, p, n, front = O.box_hit(b, (1.0, 1.0, -5.0), (0.0, 0.0, 1.0))
+    # the min-z face is Quad(min_p, dx, dy): its normal dx x dy points +z, i.e.
+    # INTO the cuboid, so this outside hit is a back face (cuboid.rs:38-45)
+    assert t == 5.0 and p == (1.0, 1.0, 0.0) and not front and n == (0.0, 0.0, -1.0)
+    # the quads' t from Quad::hit directly: the nearer face wins
+    q0 = O.quad_hit((0, 0, 0, 2, 0, 0, 0, 3, 0), (1.0, 1.0, -5.0), (0.0, 0.0, 1.0))
+    assert q0[0] == t
+
+
+def test_translated_box_aabb_and_the_direction_translation():
+    """Transformation::transform_vector3d ADDS the translation
+    (geometry/src/transformations.rs:112-114): the inverse maps a direction d
+    to R^-1 d - R^-1 T.  With a pure translation T the object-space ray is
+    (o - T, d - T); its hit point goes back by + T."""
+    T = (10.0, 0.0, 0.0)
+    b = _box((0, 0, 0), (2, 2, 2), T=T)
+    lo, hi = O.box_aabb(b)
+    # AABBox::from_points pads after EVERY enclose: the first two corners
+    # differ only in y, so x and z get 1e-4 twice at the low end
+    assert all(a < b for a, b in zip(lo, (10.0, 0.0, 0.0))) and all(a > b for a, b in zip(hi, (12.0, 2.0, 2.0)))
+    assert all(b - a < 5e-4 for a, b in zip(lo, (10.0, 0.0, 0.0)))
+    o, d = (11.0, 1.0, -5.0), (10.0, 0.0, 1.0)          # object space: o' = (1, 1, -5), d' = (0, 0, 1)
+    t, p, n, front = O.box_hit(b, o, d)
+    assert t == 5.0 and p == (11.0, 1.0, 0.0) and n == (0.0, 0.0, -1.0) and not front
+
+
+def test_singular_transformation_is_never_hit():
+    b = _box((0, 0, 0), (1, 1, 1), R=((1, 0, 0), (0, 0, 0), (0, 0, 1)))   # det 0: inverse() is None
+    assert O.box_hit(b, (0.5, 0.5, -3.0), (0.0, 0.0, 1.0)) is None
+
+
+def test_transform_composition_matches_the_reference_order():
+    """translate then rotate(15 deg, Y) = {R, R T} (apply: b.R * a.R, b.T + b.R * a.T)."""
+    R, T = O.transform_compose(("translate", (265, 0, 295)), ("rotate", 15, 1))
+    c, s = math.cos(15 * (math.pi / 180)), math.sin(15 * (math.pi / 180))
+    assert R == [[c, 0.0, s], [0.0, 1.0, 0.0], [-s, 0.0, c]]
+    assert T == [c * 265 + 0.0 * 0 + s * 295 + 0.0, 0.0, (-s * 265 + 0.0 * 0) + c * 295 + 0.0]
+
+
+def test_cornell_coplanar_tie_goes_to_the_first_type_group():
+    """The cuboid's bottom face lies in the floor's plane (y = 0): a ray
+    reaching the floor under the box gets the same t from both.  The reference
+    world is a flat HittableList whose hit is min_by over type groups in
+    first-insertion order, Quad before Transformed<Cuboid>
+    (hittable_list.rs:395-406; lib.rs:306-343), and min_by keeps the first
+    minimum: the floor quad (object 2) wins."""
+    import ray_tracing_weekend_amd as rtw
+    soa, _ = rtw.scenes.cornell_box_soa()
+    sc = O.Scene(**soa.__dict__)
+    o = (404.1316009481821, 0.010599100747201926, 367.9403068786761)
+    d = (-0.6518441571396578, -0.41416419117277475, 0.6352694054911589)
+    k, t, p, n, front = O.world_hit(sc, o, d)
+    assert k == 2 and p[1] == 0.0 and n == (-0.0, 1.0, -0.0) and not front
+    # the box reports the same t for its own bottom face
+    box = soa.boxes[0].tolist()
+    assert O.box_hit(box, o, d)[0] == t
