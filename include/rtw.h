@@ -34,16 +34,18 @@
 extern "C" {
 #endif
 
-#define RTW_ABI_VERSION 4
+#define RTW_ABI_VERSION 5
 
 /* error codes */
 #define RTW_OK 0
 #define RTW_E_INVALID (-1)       /* bad argument / inconsistent scene */
 #define RTW_E_DEVICE (-2)        /* HIP runtime error (message in rtw_last_error) */
-#define RTW_E_NO_LIGHTS (-3)     /* Lambertian present, empty light list:
-                                    hittable_list.rs:417 panics there */
+#define RTW_E_NO_LIGHTS (-3)     /* a Lambertian bounce drew a light sample from an empty
+                                    light list: hittable_list.rs:417 panics there */
 #define RTW_E_NO_SCENE (-4)      /* render before a scene was set */
 #define RTW_E_UNSUPPORTED (-5)   /* scene/feature outside this build's scope */
+#define RTW_E_PANIC (-6)         /* the render reached a point where the reference panics:
+                                    a non-finite plane UV (plane.rs:66-69) */
 
 /* precision of the device arithmetic */
 #define RTW_F32 0                /* speed mode: f32 + FMA + native sqrt/rcp/sin/cos */
@@ -56,6 +58,21 @@ extern "C" {
 #define RTW_DIELECTRIC 2         /* material.rs:423-488 ("Dialectric") */
 #define RTW_INVISIBLE 3          /* material.rs:321-325 */
 #define RTW_DIFFUSE_LIGHT 4      /* material.rs:490-514: emits albedo, scatter() None */
+
+/* texture kinds (shared/src/texture.rs) */
+#define RTW_TEX_SOLID 0          /* SolidColour, texture.rs:15-22 */
+#define RTW_TEX_CHECKER 1        /* CheckerTexture, texture.rs:24-55 */
+#define RTW_TEX_NOISE 2          /* NoiseTexture over a Perlin table, texture.rs:57-102, perlin.rs */
+
+/* light-list entry kinds (rtw_scene.light_kinds) */
+#define RTW_LIGHT_SPHERE 0       /* Sphere::pdf_value / random, sphere.rs:101-127 */
+#define RTW_LIGHT_QUAD 1         /* Quad::pdf_value / random, quadrilateral.rs:100-118 */
+#define RTW_LIGHT_DEFAULT 2      /* a hittable without its own pdf (Plane, Transformed<Cuboid>):
+                                    the trait defaults pdf_value = 0, random = (1, 0, 0),
+                                    hittable.rs:175-181 */
+/* rtw_scene.light_flags */
+#define RTW_LIGHTS_BVH_LEAF 1    /* the light list is a BoundedVolumeHierarchy of <= 5 entries
+                                    (a leaf): pdf_value = (sum / n * n) / n, bvh.rs:67-76,191-194 */
 
 /* World acceleration used by the render kernel */
 #define RTW_ACCEL_AUTO 0         /* pick per scene */
@@ -107,7 +124,8 @@ typedef struct rtw_scene {
     uint32_t n_light_quads;
     const double *light_quads;    /* the light list's quads, n x 9 as quads */
     /* light-list order (HittableList insertion order, hittable_list.rs:408-419):
-     * n_lights + n_light_quads kinds, 0 = next sphere, 1 = next quad;
+     * n_lights + n_light_quads + n_light_other RTW_LIGHT_* kinds, each taking
+     * the next entry of its array (RTW_LIGHT_DEFAULT has no data);
      * NULL = all spheres, then all quads */
     const uint32_t *light_kinds;
     /* Transformed<Cuboid> (cuboid.rs:26-71, entities/transformations.rs:10-30):
@@ -116,6 +134,25 @@ typedef struct rtw_scene {
     uint32_t n_boxes;
     const double *boxes;          /* n_boxes x {p xyz, q xyz, R[3][3] row-major, T xyz} = 18 */
     const uint32_t *box_mat;
+    /* Textures (texture.rs, perlin.rs).  mat_tex == NULL: every material's
+     * colour is the SolidColour albedo in mat_params.  Otherwise mat_tex[m] is
+     * the texture of material m (Lambertian attenuation, DiffuseLight emission),
+     * evaluated at the hit's (u, v, p) (sphere.rs:49-54, plane.rs:40-54,
+     * quadrilateral.rs:58-63):
+     *   RTW_TEX_SOLID    tex_params {r, g, b, -}
+     *   RTW_TEX_CHECKER  tex_params {-, -, -, inv_scale = 1 / scale}, tex_refs {even, odd} texture ids
+     *   RTW_TEX_NOISE    tex_params {-, -, -, scale}, tex_refs {Perlin table id, -} */
+    const uint32_t *mat_tex;
+    uint32_t n_textures;
+    const uint32_t *tex_type;
+    const double *tex_params;     /* n_textures x 4 */
+    const uint32_t *tex_refs;     /* n_textures x 2 */
+    uint32_t n_perlin;
+    const double *perlin_vec;     /* n_perlin x 256 x 3: Perlin::rand_vec */
+    const uint32_t *perlin_perm;  /* n_perlin x 3 x 256: perm_x, perm_y, perm_z (0..255) */
+    /* light-list entries of kind RTW_LIGHT_DEFAULT (light_kinds == 2) */
+    uint32_t n_light_other;
+    uint32_t light_flags;         /* RTW_LIGHTS_BVH_LEAF */
 } rtw_scene;
 
 typedef struct rtw_stats {
@@ -131,6 +168,11 @@ typedef struct rtw_stats {
     uint32_t kernel;              /* render-kernel variant: 0 brute/L2, 1 brute/LDS, 2 BVH one
                                      loop, 3 BVH while-while, 4 BVH 4-wide, 5 BVH while-while
                                      with the tree in LDS */
+    /* samples that reached a reference panic (the render then returns an
+     * error): a non-finite plane UV (plane.rs:66-69) -> RTW_E_PANIC;
+     * HittableList::random on an empty light list (hittable_list.rs:417)
+     * -> RTW_E_NO_LIGHTS */
+    uint64_t panic_plane_uv, panic_no_lights;
 } rtw_stats;
 
 typedef struct rtw_ctx rtw_ctx;
@@ -185,7 +227,9 @@ int rtw_render_device(rtw_ctx *ctx, const rtw_camera *cam, uint64_t seed,
                       void *stream);
 uint32_t rtw_tile_rows(void);                        /* rows per tile row (8) */
 uint32_t rtw_rows_for_rank(uint32_t image_height, uint32_t rank, uint32_t nranks);
-/* Counters of the last render (waits for it to finish). */
+/* Counters of the last render (waits for it to finish).  Returns
+ * RTW_E_NO_LIGHTS / RTW_E_PANIC (stats still filled) when a sample reached a
+ * reference panic. */
 int rtw_get_stats(rtw_ctx *ctx, rtw_stats *stats);
 /* Device times (HIP events) of the last min(max, 64) renders, oldest first:
  * render_ms = the render kernel alone, total_ms = render + chunk reduction.
@@ -201,9 +245,18 @@ const rtw_scene *rtw_world_scene(const rtw_world *w);
 /* the camera builder scenes::simple returns (lib.rs:219-226) + main.rs's vfov */
 void rtw_world_camera_builder(const rtw_world *w, rtw_camera_builder *out);
 void rtw_world_free(rtw_world *w);
-/* a reference scene by its bin/src/main.rs name: "simple" (seeded, grid 11)
- * or "cornell_box" (scenes/src/lib.rs:292-395); NULL for other names */
+/* a reference scene by its bin/src/main.rs name (scenes/src/lib.rs):
+ * "simple" (seeded, grid 11), "cornell_box", "debug", "checkered_spheres",
+ * "perlin_spheres", "plane", "simple_light", "simple_transform"; the seed
+ * drives simple's generator and the Perlin tables.  NULL for other names. */
 rtw_world *rtw_scene_named(const char *name, uint64_t seed);
+
+/* ---- Perlin::new (perlin.rs:46-58) ------------------------------------- */
+/* The reference fills the tables from thread_rng; here from the build's
+ * seeded xoshiro256++: rand_vec = 256 UnitSphere samples, then perm_x, perm_y,
+ * perm_z, each the identity shuffled by j = Uniform::new(i, 256) for i < 255.
+ * rand_vec: 768 doubles; perm: 768 values (perm_x, perm_y, perm_z). */
+int rtw_perlin_generate(uint64_t seed, double *rand_vec, uint32_t *perm);
 
 /* ---- SampledColour / PPM (colour.rs:14-36; main.rs:89-104) ------------ */
 /* sums -> 8-bit RGB, rows flipped so that row 0 is the TOP row:

@@ -17,7 +17,17 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "liboracle.so")
 
-LAMBERTIAN, METAL, DIELECTRIC, INVISIBLE = 0, 1, 2, 3
+LAMBERTIAN, METAL, DIELECTRIC, INVISIBLE, DIFFUSE_LIGHT = 0, 1, 2, 3, 4
+TEX_SOLID, TEX_CHECKER, TEX_NOISE = 0, 1, 2
+LIGHTS_BVH_LEAF = 1
+
+
+class ReferencePanic(RuntimeError):
+    """The render reached a point where the reference panics (stats.panic_*)."""
+
+    def __init__(self, msg, stats):
+        super().__init__(msg)
+        self.stats = stats
 ACCEL_BRUTE, ACCEL_BVH_REF, ACCEL_BVH_CACHED = 0, 1, 2
 
 _u32p = C.POINTER(C.c_uint32)
@@ -56,12 +66,16 @@ class _Scene(C.Structure):
         ("n_quads", C.c_uint32), ("quads", _f64p), ("quad_mat", _u32p),
         ("n_light_quads", C.c_uint32), ("light_quads", _f64p), ("light_kinds", _u32p),
         ("n_boxes", C.c_uint32), ("boxes", _f64p), ("box_mat", _u32p),
+        ("mat_tex", _u32p), ("n_textures", C.c_uint32), ("tex_type", _u32p), ("tex_params", _f64p),
+        ("tex_refs", _u32p), ("n_perlin", C.c_uint32), ("perlin_vec", _f64p), ("perlin_perm", _u32p),
+        ("n_light_other", C.c_uint32), ("light_flags", C.c_uint32),
     ]
 
 
 class Stats(C.Structure):
     _fields_ = [("samples", C.c_uint64), ("segments", C.c_uint64),
-                ("lambertian", C.c_uint64), ("nan_samples", C.c_uint64)]
+                ("lambertian", C.c_uint64), ("nan_samples", C.c_uint64),
+                ("panic_plane_uv", C.c_uint64), ("panic_no_lights", C.c_uint64)]
 
 
 @dataclass
@@ -77,9 +91,18 @@ class Scene:
     quads: np.ndarray = None         # (q, 9) Q, u, v
     quad_mat: np.ndarray = None      # (q,) uint32
     light_quads: np.ndarray = None   # (lq, 9)
-    light_kinds: np.ndarray = None   # (l + lq,) 0 sphere / 1 quad, list order; None = spheres first
+    light_kinds: np.ndarray = None   # (l + lq + lo,) 0 sphere / 1 quad / 2 Hittable defaults, list order;
+                                     # None = spheres first
     boxes: np.ndarray = None         # (b, 18) Cuboid p, q, rotation R (row-major), translation T
     box_mat: np.ndarray = None       # (b,) uint32
+    mat_tex: np.ndarray = None       # (k,) texture id per material; None = SolidColour albedos
+    tex_type: np.ndarray = None      # (t,) TEX_SOLID / TEX_CHECKER / TEX_NOISE
+    tex_params: np.ndarray = None    # (t, 4) solid rgb | checker inv_scale [3] | noise scale [3]
+    tex_refs: np.ndarray = None      # (t, 2) checker even/odd ids | noise perlin id
+    perlin_vec: np.ndarray = None    # (p, 256, 3) Perlin::rand_vec
+    perlin_perm: np.ndarray = None   # (p, 3, 256) perm_x, perm_y, perm_z
+    n_light_other: int = 0
+    light_flags: int = 0             # LIGHTS_BVH_LEAF
 
 
 _lib = None
@@ -145,6 +168,15 @@ def lib():
                                       C.c_uint32]
         L.rtwo_trace_path.restype = C.c_uint32
         L.rtwo_world_hit.argtypes = [C.POINTER(_Scene), C.c_int, _f64p, _f64p, _f64p]
+        L.rtwo_sin.argtypes = [C.c_double]
+        L.rtwo_sin.restype = C.c_double
+        L.rtwo_sphere_uv.argtypes = [_f64p, _f64p]
+        L.rtwo_plane_uv.argtypes = [_f64p, _f64p, _f64p]
+        L.rtwo_perlin_noise.argtypes = [_f64p, _u32p, _f64p]
+        L.rtwo_perlin_noise.restype = C.c_double
+        L.rtwo_perlin_turb.argtypes = [_f64p, _u32p, _f64p, C.c_int]
+        L.rtwo_perlin_turb.restype = C.c_double
+        L.rtwo_texture_colour.argtypes = [C.POINTER(_Scene), C.c_uint32, C.c_double, C.c_double, _f64p, _f64p]
         _lib = L
     return _lib
 
@@ -256,12 +288,21 @@ def _scene_struct(sc: Scene):
                None if sc.light_kinds is None else u(sc.light_kinds),
                0 if sc.box_mat is None else len(np.asarray(sc.box_mat).reshape(-1)),
                f(np.zeros((0, 18)) if sc.boxes is None else sc.boxes, 18),
-               u(np.zeros(0, np.uint32) if sc.box_mat is None else sc.box_mat))
+               u(np.zeros(0, np.uint32) if sc.box_mat is None else sc.box_mat),
+               None if sc.mat_tex is None else u(sc.mat_tex),
+               0 if sc.tex_type is None else len(np.asarray(sc.tex_type).reshape(-1)),
+               u(np.zeros(0) if sc.tex_type is None else sc.tex_type),
+               f(np.zeros((0, 4)) if sc.tex_params is None else sc.tex_params, 4),
+               u(np.zeros(0) if sc.tex_refs is None else sc.tex_refs),
+               0 if sc.perlin_vec is None else len(np.asarray(sc.perlin_vec).reshape(-1, 768)),
+               f(np.zeros((0, 768)) if sc.perlin_vec is None else sc.perlin_vec, 768),
+               u(np.zeros(0) if sc.perlin_perm is None else sc.perlin_perm),
+               int(sc.n_light_other), int(sc.light_flags))
     return s, keep
 
 
 def render(cam: Camera, sc: Scene, seed: int, *, chunk: int = 0, accel: int = ACCEL_BRUTE,
-           threads: int = 0, rows=None, cols=None, out=None):
+           threads: int = 0, rows=None, cols=None, out=None, allow_panic: bool = False):
     """Camera::render restated.  Returns (sums[H, W, 3] float64, Stats).
     rows = (begin, end, step); cols = (begin, end)."""
     H, W = cam.image_height, cam.image_width
@@ -275,9 +316,12 @@ def render(cam: Camera, sc: Scene, seed: int, *, chunk: int = 0, accel: int = AC
     st = Stats()
     rc = lib().rtwo_render(C.byref(cam), C.byref(s), C.c_uint64(seed & 0xFFFFFFFFFFFFFFFF), chunk,
                            accel, threads, rb, re, rs, cb, ce, _p(out, _f64p), C.byref(st))
-    if rc != 0:
-        raise ValueError("oracle render rejected the scene (e.g. Lambertian with no lights)")
     del keep
+    if rc == -2 and not allow_panic:
+        raise ReferencePanic(f"the reference panics on this render (plane UV: {st.panic_plane_uv}, "
+                             f"empty light list: {st.panic_no_lights} samples)", st)
+    if rc not in (0, -2):
+        raise ValueError("oracle render rejected the scene")
     return out, st
 
 
@@ -415,3 +459,40 @@ def world_hit(sc: Scene, o, d, accel=ACCEL_BRUTE):
     k = lib().rtwo_world_hit(C.byref(s), accel, arr(o), arr(d), out)
     del keep
     return k, out[0], tuple(out[1:4]), tuple(out[4:7]), bool(out[7])
+
+
+# ---- texture KAT entry points
+def sin(x):
+    return lib().rtwo_sin(float(x))
+
+
+def sphere_uv(n):
+    out = (C.c_double * 2)()
+    lib().rtwo_sphere_uv(arr(n), out)
+    return out[0], out[1]
+
+
+def plane_uv(plane, p):
+    out = (C.c_double * 2)()
+    lib().rtwo_plane_uv(arr(plane, 6), arr(p), out)
+    return out[0], out[1]
+
+
+def perlin_noise(vec, perm, p):
+    v, vp = dptr(np.asarray(vec).reshape(-1))
+    pm = np.ascontiguousarray(np.asarray(perm, np.uint32).reshape(-1))
+    return lib().rtwo_perlin_noise(vp, _p(pm, _u32p), arr(p))
+
+
+def perlin_turb(vec, perm, p, depth=7):
+    v, vp = dptr(np.asarray(vec).reshape(-1))
+    pm = np.ascontiguousarray(np.asarray(perm, np.uint32).reshape(-1))
+    return lib().rtwo_perlin_turb(vp, _p(pm, _u32p), arr(p), depth)
+
+
+def texture_colour(sc: Scene, tid, u, v, p):
+    s, keep = _scene_struct(sc)
+    out = (C.c_double * 3)()
+    lib().rtwo_texture_colour(C.byref(s), tid, u, v, arr(p), out)
+    del keep
+    return tuple(out)

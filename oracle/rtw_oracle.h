@@ -87,13 +87,40 @@ typedef struct rtwo_scene {
     uint32_t n_boxes;
     const double *boxes;        /* n x {p xyz, q xyz, R[3][3], T xyz} = 18 */
     const uint32_t *box_mat;
+    /* Textures (texture.rs, perlin.rs).  mat_tex NULL: every material's colour
+     * is its SolidColour albedo from mat_params.  Otherwise mat_tex[m] is the
+     * texture of material m (Lambertian attenuation, DiffuseLight emission):
+     *   RTWO_TEX_SOLID   params {r, g, b, -}
+     *   RTWO_TEX_CHECKER params {-, -, -, inv_scale}, refs {even, odd} texture ids
+     *   RTWO_TEX_NOISE   params {-, -, -, scale},     refs {perlin table id, -} */
+    const uint32_t *mat_tex;
+    uint32_t n_textures;
+    const uint32_t *tex_type;
+    const double *tex_params;   /* n x 4 */
+    const uint32_t *tex_refs;   /* n x 2 */
+    uint32_t n_perlin;
+    const double *perlin_vec;   /* n x 256 x 3: Perlin::rand_vec */
+    const uint32_t *perlin_perm;/* n x 3 x 256: perm_x, perm_y, perm_z */
+    /* light-list entries with the Hittable trait defaults (hittable.rs:175-181:
+     * pdf_value 0, random (1, 0, 0)), e.g. a Transformed<Cuboid>: light_kinds 2 */
+    uint32_t n_light_other;
+    uint32_t light_flags;       /* RTWO_LIGHTS_BVH_LEAF */
 } rtwo_scene;
+
+enum { RTWO_TEX_SOLID = 0, RTWO_TEX_CHECKER = 1, RTWO_TEX_NOISE = 2 };
+/* the light list is a BoundedVolumeHierarchy leaf (<= 5 entries): pdf_value =
+ * (HittableList::pdf_value * len) / len (bvh.rs:67-76, 191-194) */
+enum { RTWO_LIGHTS_BVH_LEAF = 1 };
 
 typedef struct rtwo_stats {
     uint64_t samples;
     uint64_t segments;          /* world.hit calls (one per bounce) */
     uint64_t lambertian;        /* Scatter-branch bounces (light-list pdf loop) */
     uint64_t nan_samples;
+    /* samples on which the reference panics: a non-finite plane UV
+     * (plane.rs:66-69), or HittableList::random on an empty light list
+     * (hittable_list.rs:414-419) */
+    uint64_t panic_plane_uv, panic_no_lights;
 } rtwo_stats;
 
 /* Quad::hit (quadrilateral.rs:79-100) with Quad::new's derived fields
@@ -128,8 +155,10 @@ int rtwo_camera_build(const rtwo_camera_builder *b, rtwo_camera *out);
  * chunk: samples are summed in chunks of `chunk` (chunk >= spp = the
  * reference's single fold, camera.rs:323-335); the per-pixel sum is
  * ((0 + chunk_0) + chunk_1) + ..., each chunk ((0 + s_a) + s_a+1) + ...
- * Returns 0 on success, -1 on invalid input (e.g. Lambertian with an empty
- * light list: hittable_list.rs:417 panics there). */
+ * Returns 0 on success, -1 on invalid input, -2 when a sample hit a point
+ * where the reference panics (stats->panic_*: a non-finite plane UV,
+ * plane.rs:66-69; HittableList::random on an empty light list,
+ * hittable_list.rs:417) -- the image is still written. */
 int rtwo_render(const rtwo_camera *cam, const rtwo_scene *sc, uint64_t seed,
                 uint32_t chunk, int accel, int nthreads,
                 uint32_t row_begin, uint32_t row_end, uint32_t row_step,
@@ -186,6 +215,21 @@ void rtwo_cosine_hemisphere(uint64_t st[4], double out[3]);
 void rtwo_sphere_random(const double sph[4], const double o[3], uint64_t st[4], double out[3]);
 /* Number of BVH nodes/leaves built for a scene (tests of the BVH restatement). */
 int rtwo_bvh_stats(const rtwo_scene *sc, uint32_t *nodes, uint32_t *leaves, uint32_t *depth);
+
+/* ---- texture KATs ---- */
+/* sin(x) as the build evaluates it on CPU and GPU (fdlibm: medium-size
+ * Cody-Waite reduction by pi/2 + __kernel_sin/__kernel_cos) */
+double rtwo_sin(double x);
+/* Sphere::get_sphere_uv (sphere.rs:49-54) of an outward unit normal */
+void rtwo_sphere_uv(const double n[3], double uv[2]);
+/* Plane::get_plane_uv (plane.rs:40-54); plane = {p, unit normal} */
+void rtwo_plane_uv(const double pl[6], const double p[3], double uv[2]);
+/* Perlin::noise / Perlin::turb (perlin.rs:59-94) over one table */
+double rtwo_perlin_noise(const double *vec, const uint32_t *perm, const double p[3]);
+double rtwo_perlin_turb(const double *vec, const uint32_t *perm, const double p[3], int depth);
+/* Texture::get_colour (texture.rs) of texture `tid` of the scene */
+void rtwo_texture_colour(const rtwo_scene *sc, uint32_t tid, double u, double v, const double p[3],
+                         double out[3]);
 
 #ifdef __cplusplus
 }

@@ -23,12 +23,16 @@ import numpy as np
 
 from . import _capi
 from ._capi import (RTW_ACCEL_AUTO, RTW_ACCEL_BRUTE, RTW_ACCEL_BVH, RTW_DIELECTRIC, RTW_F32,
-                    RTW_F64, RTW_INVISIBLE, RTW_LAMBERTIAN, RTW_METAL, RTW_DIFFUSE_LIGHT)
+                    RTW_F64, RTW_INVISIBLE, RTW_LAMBERTIAN, RTW_METAL, RTW_DIFFUSE_LIGHT, RTW_TEX_SOLID,
+                    RTW_TEX_CHECKER, RTW_TEX_NOISE, RTW_LIGHT_SPHERE, RTW_LIGHT_QUAD, RTW_LIGHT_DEFAULT,
+                    RTW_LIGHTS_BVH_LEAF)
 
 __all__ = [
-    "Material", "Lambertian", "Metal", "Dialectric", "INVISIBLE", "Sphere", "Plane",
-    "HittableList", "SceneSoA", "flatten", "CameraBuilder", "Camera", "Renderer", "scenes",
-    "encode_rgb8", "write_ppm", "RenderError", "RTW_F32", "RTW_F64",
+    "Material", "Lambertian", "Metal", "Dialectric", "DiffuseLight", "INVISIBLE", "Sphere", "Plane",
+    "Quad", "Cuboid", "Transformation", "translation", "rotation", "SolidColour", "CheckerTexture",
+    "NoiseTexture", "Perlin", "HittableList", "BoundedVolumeHierarchy", "SceneSoA", "flatten",
+    "CameraBuilder", "Camera", "Renderer", "scenes", "encode_rgb8", "write_ppm", "RenderError",
+    "RTW_F32", "RTW_F64",
 ]
 
 _lib = _capi.load()   # raises if librtw.so is missing: there is no CPU fallback
@@ -40,6 +44,54 @@ class RenderError(RuntimeError):
         self.code = code
 
 
+# ---------------------------------------------------------------- textures
+class Perlin:                                # perlin.rs:13-58
+    """Perlin::new with the build's seeded RNG (the reference draws the
+    tables from thread_rng): rand_vec (256 x 3) and perm (3 x 256)."""
+
+    def __init__(self, seed: int = 0x5EED0001):
+        self.rand_vec = np.zeros((256, 3), np.float64)
+        self.perm = np.zeros((3, 256), np.uint32)
+        rc = _lib.rtw_perlin_generate(C.c_uint64(seed & 0xFFFFFFFFFFFFFFFF),
+                                      self.rand_vec.ctypes.data_as(_capi._f64p),
+                                      self.perm.ctypes.data_as(_capi._u32p))
+        if rc != 0:
+            raise RenderError(rc, "rtw_perlin_generate failed")
+
+
+@dataclass(frozen=True, eq=False)
+class SolidColour:                           # texture.rs:15-22
+    colour: tuple
+
+
+@dataclass(frozen=True, eq=False)
+class CheckerTexture:                        # texture.rs:24-55
+    even: object
+    odd: object
+    inv_scale: float
+
+    @staticmethod
+    def new(even, odd, scale: float) -> "CheckerTexture":
+        return CheckerTexture(even, odd, 1.0 / float(scale))          # scale.recip()
+
+    @staticmethod
+    def new_with_colours(even, odd, scale: float) -> "CheckerTexture":
+        return CheckerTexture.new(SolidColour(tuple(map(float, even))), SolidColour(tuple(map(float, odd))), scale)
+
+
+@dataclass(frozen=True, eq=False)
+class NoiseTexture:                          # texture.rs:57-102
+    scale: float
+    noise: Perlin
+
+    @staticmethod
+    def new(scale: float, seed: int = 0x5EED0001) -> "NoiseTexture":
+        return NoiseTexture(float(scale), Perlin(seed))
+
+
+_TEXTURES = (SolidColour, CheckerTexture, NoiseTexture)
+
+
 # ---------------------------------------------------------------- materials
 @dataclass(frozen=True)
 class Material:
@@ -47,9 +99,12 @@ class Material:
     albedo: tuple = (0.0, 0.0, 0.0)
     fuzz: float = 0.0
     ior: float = 0.0
+    texture: object = None                   # Lambertian / DiffuseLight texture; None = SolidColour(albedo)
 
 
-def Lambertian(albedo):                      # material.rs:327-355 (new_with_colour)
+def Lambertian(albedo):                      # material.rs:347-355 (new / new_with_colour)
+    if isinstance(albedo, _TEXTURES):
+        return Material(RTW_LAMBERTIAN, texture=albedo)
     return Material(RTW_LAMBERTIAN, tuple(map(float, albedo)))
 
 
@@ -64,7 +119,9 @@ def Dialectric(index_of_refraction):         # material.rs:423-455
 INVISIBLE = Material(RTW_INVISIBLE)          # material.rs:321-325
 
 
-def DiffuseLight(colour):                    # material.rs:490-514 (new_with_colour)
+def DiffuseLight(colour):                    # material.rs:490-514 (new / new_with_colour)
+    if isinstance(colour, _TEXTURES):
+        return Material(RTW_DIFFUSE_LIGHT, texture=colour)
     return Material(RTW_DIFFUSE_LIGHT, tuple(map(float, colour)))
 
 
@@ -152,6 +209,17 @@ class HittableList:                          # hittable_collections/hittable_lis
         return len(self.objects)
 
 
+class BoundedVolumeHierarchy(HittableList):  # hittable_collections/bvh.rs:106-143 (::from(list))
+    """The reference's BVH over a list: as the world it gives the list's
+    closest hit (the device builds its own tree); as a light list its
+    pdf_value is (sum / n * n) / n for a leaf of <= 5 entries (bvh.rs:67-76,
+    191-194).  Deeper BVH light lists are outside this build (their
+    aux_random indexing, bvh.rs:78-92, is inconsistent)."""
+
+    def __init__(self, lst=()):
+        super().__init__(lst.objects if isinstance(lst, HittableList) else lst)
+
+
 @dataclass
 class SceneSoA:
     """Flattened world + lights in the C-ABI's struct-of-arrays layout."""
@@ -168,6 +236,14 @@ class SceneSoA:
     light_kinds: np.ndarray = None          # list order: 0 sphere / 1 quad; None = spheres first
     boxes: np.ndarray = field(default_factory=lambda: np.zeros((0, 18)))
     box_mat: np.ndarray = field(default_factory=lambda: np.zeros(0, np.uint32))
+    mat_tex: np.ndarray = None              # texture id per material; None = SolidColour albedos
+    tex_type: np.ndarray = field(default_factory=lambda: np.zeros(0, np.uint32))
+    tex_params: np.ndarray = field(default_factory=lambda: np.zeros((0, 4)))
+    tex_refs: np.ndarray = field(default_factory=lambda: np.zeros((0, 2), np.uint32))
+    perlin_vec: np.ndarray = field(default_factory=lambda: np.zeros((0, 256, 3)))
+    perlin_perm: np.ndarray = field(default_factory=lambda: np.zeros((0, 3, 256), np.uint32))
+    n_light_other: int = 0
+    light_flags: int = 0
 
     def as_c(self):
         """(rtw_scene, keepalive) -- the struct points into these arrays."""
@@ -190,7 +266,12 @@ class SceneSoA:
                             len(self.quad_mat), f(self.quads, 9), u(self.quad_mat),
                             len(np.asarray(self.light_quads).reshape(-1, 9)), f(self.light_quads, 9),
                             None if self.light_kinds is None else u(self.light_kinds),
-                            len(self.box_mat), f(self.boxes, 18), u(self.box_mat))
+                            len(self.box_mat), f(self.boxes, 18), u(self.box_mat),
+                            None if self.mat_tex is None else u(self.mat_tex),
+                            len(np.asarray(self.tex_type).reshape(-1)), u(self.tex_type), f(self.tex_params, 4),
+                            u(self.tex_refs), len(np.asarray(self.perlin_vec).reshape(-1, 768)),
+                            f(self.perlin_vec, 768), u(self.perlin_perm),
+                            int(self.n_light_other), int(self.light_flags))
         return s, keep
 
     @staticmethod
@@ -206,27 +287,73 @@ class SceneSoA:
                         u(s.mat_type, s.n_materials), f(s.mat_params, s.n_materials, 5),
                         f(s.lights, s.n_lights, 4), f(s.quads, s.n_quads, 9), u(s.quad_mat, s.n_quads),
                         f(s.light_quads, s.n_light_quads, 9),
-                        u(s.light_kinds, s.n_lights + s.n_light_quads) if s.light_kinds else None,
-                        f(s.boxes, s.n_boxes, 18), u(s.box_mat, s.n_boxes))
+                        u(s.light_kinds, s.n_lights + s.n_light_quads + s.n_light_other) if s.light_kinds else None,
+                        f(s.boxes, s.n_boxes, 18), u(s.box_mat, s.n_boxes),
+                        u(s.mat_tex, s.n_materials) if s.mat_tex else None,
+                        u(s.tex_type, s.n_textures), f(s.tex_params, s.n_textures, 4),
+                        u(s.tex_refs, 2 * s.n_textures).reshape(-1, 2),
+                        f(s.perlin_vec, s.n_perlin, 768).reshape(-1, 256, 3),
+                        u(s.perlin_perm, 768 * s.n_perlin).reshape(-1, 3, 256),
+                        int(s.n_light_other), int(s.light_flags))
 
 
 def flatten(world, lights) -> SceneSoA:
-    """world: HittableList or SceneSoA; lights: HittableList of Spheres and
-    Quads (their list order is kept: it is the light pdf's sum order and the
-    uniform pick's index)."""
+    """world: HittableList (or BoundedVolumeHierarchy) or SceneSoA; lights:
+    a HittableList / BoundedVolumeHierarchy.  The light list's order is kept:
+    it is the light pdf's sum order and the uniform pick's index.  Spheres
+    and Quads sample themselves; Planes and Cuboids in a light list have the
+    Hittable defaults (pdf 0, random (1, 0, 0); hittable.rs:175-181)."""
     if isinstance(world, SceneSoA):
         return world
     mats, mtypes, sph, smat, pl, pmat, qd, qmat = [], [], [], [], [], [], [], []
+    textured = any(o.mat.texture is not None and o.mat.type in (RTW_LAMBERTIAN, RTW_DIFFUSE_LIGHT)
+                   for o in world.objects)
+    mtex, ttype, tpar, trefs, pvec, pperm = [], [], [], [], [], []
+    tex_ids, perlin_ids = {}, {}
+
+    def push_tex(t):
+        if id(t) in tex_ids:
+            return tex_ids[id(t)][0]
+        k = len(ttype)
+        tex_ids[id(t)] = (k, t)                       # keep t alive while its id() is a key
+        if isinstance(t, SolidColour):
+            ttype.append(RTW_TEX_SOLID)
+            tpar.append(list(map(float, t.colour)) + [0.0])
+            trefs.append([0, 0])
+        elif isinstance(t, CheckerTexture):
+            ttype.append(RTW_TEX_CHECKER)
+            tpar.append([0.0, 0.0, 0.0, t.inv_scale])
+            trefs.append([0, 0])
+            trefs[k] = [push_tex(t.even), push_tex(t.odd)]
+        else:
+            ttype.append(RTW_TEX_NOISE)
+            tpar.append([0.0, 0.0, 0.0, t.scale])
+            if id(t.noise) not in perlin_ids:
+                perlin_ids[id(t.noise)] = (len(pvec), t.noise)
+                pvec.append(t.noise.rand_vec)
+                pperm.append(t.noise.perm)
+            trefs.append([perlin_ids[id(t.noise)][0], 0])
+        return k
 
     def push(m: Material):
         mtypes.append(m.type)
         mats.append(list(m.albedo) + [m.fuzz, m.ior])
+        if textured:
+            if m.texture is not None and m.type in (RTW_LAMBERTIAN, RTW_DIFFUSE_LIGHT):
+                mtex.append(push_tex(m.texture))
+            else:
+                mtex.append(push_tex(SolidColour(m.albedo)))
         return len(mtypes) - 1
 
+    # materials numbered planes, spheres, quads, cuboids (as the C++ flatten)
     for o in world.objects:
         if isinstance(o, Plane):
             pl.append(list(o.point) + list(o.normal))
             pmat.append(push(o.mat))
+    for o in world.objects:
+        if isinstance(o, Sphere):
+            sph.append(list(o.center) + [o.radius])
+            smat.append(push(o.mat))
     for o in world.objects:
         if isinstance(o, Quad):
             qd.append(list(o.q) + list(o.u) + list(o.v))
@@ -236,27 +363,33 @@ def flatten(world, lights) -> SceneSoA:
         if isinstance(o, Cuboid):
             bx.append(list(o.p) + list(o.q) + [v for row in o.xform.R for v in row] + list(o.xform.T))
             bmat.append(push(o.mat))
-    for o in world.objects:
-        if isinstance(o, Sphere):
-            sph.append(list(o.center) + [o.radius])
-            smat.append(push(o.mat))
     li, lq, kinds = [], [], []
     for o in lights.objects:
         if isinstance(o, Sphere):
             li.append(list(o.center) + [o.radius])
-            kinds.append(0)
+            kinds.append(RTW_LIGHT_SPHERE)
         elif isinstance(o, Quad):
             lq.append(list(o.q) + list(o.u) + list(o.v))
-            kinds.append(1)
+            kinds.append(RTW_LIGHT_QUAD)
         else:
-            raise RenderError(_capi.RTW_E_UNSUPPORTED, "lights must be spheres or quads in this build")
+            kinds.append(RTW_LIGHT_DEFAULT)
+    n_other = kinds.count(RTW_LIGHT_DEFAULT)
+    flags = 0
+    if isinstance(lights, BoundedVolumeHierarchy):
+        if len(lights) > 5:
+            raise RenderError(_capi.RTW_E_UNSUPPORTED, "a BVH light list of more than 5 entries (bvh.rs:78-92)")
+        flags |= RTW_LIGHTS_BVH_LEAF
     return SceneSoA(np.array(sph, np.float64).reshape(-1, 4), np.array(smat, np.uint32),
                     np.array(pl, np.float64).reshape(-1, 6), np.array(pmat, np.uint32),
                     np.array(mtypes, np.uint32), np.array(mats, np.float64).reshape(-1, 5),
                     np.array(li, np.float64).reshape(-1, 4), np.array(qd, np.float64).reshape(-1, 9),
                     np.array(qmat, np.uint32), np.array(lq, np.float64).reshape(-1, 9),
-                    np.array(kinds, np.uint32) if lq else None,
-                    np.array(bx, np.float64).reshape(-1, 18), np.array(bmat, np.uint32))
+                    np.array(kinds, np.uint32) if (lq or n_other) else None,
+                    np.array(bx, np.float64).reshape(-1, 18), np.array(bmat, np.uint32),
+                    np.array(mtex, np.uint32) if textured else None, np.array(ttype, np.uint32),
+                    np.array(tpar, np.float64).reshape(-1, 4), np.array(trefs, np.uint32).reshape(-1, 2),
+                    np.array(pvec, np.float64).reshape(-1, 256, 3), np.array(pperm, np.uint32).reshape(-1, 3, 256),
+                    n_other, flags)
 
 
 # ---------------------------------------------------------------- camera
@@ -443,10 +576,13 @@ class scenes:                                 # scenes/src/lib.rs
             _lib.rtw_world_free(w)
         return soa, CameraBuilder(b)
 
+    NAMES = ("cornell_box", "debug", "checkered_spheres", "perlin_spheres", "plane", "simple",
+             "simple_light", "simple_transform")      # bin/src/main.rs:29-38
+
     @staticmethod
     def named_soa(name: str, seed: int = 0x5EED0001):
         """(SceneSoA, CameraBuilder) of a reference scene by its main.rs name
-        ("simple", "cornell_box")."""
+        (scenes.NAMES); `seed` drives simple's generator and the Perlin tables."""
         w = _lib.rtw_scene_named(name.encode(), C.c_uint64(seed & 0xFFFFFFFFFFFFFFFF))
         if not w:
             raise RenderError(_capi.RTW_E_UNSUPPORTED, f"scene {name!r} is not in this build")

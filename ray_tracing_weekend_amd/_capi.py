@@ -16,10 +16,13 @@ LIB_PATH = os.path.join(LIB_DIR, "librtw.so")
 LIB_PATH = os.environ.get("RTW_LIB_OVERRIDE", LIB_PATH)
 
 RTW_OK = 0
-RTW_E_INVALID, RTW_E_DEVICE, RTW_E_NO_LIGHTS, RTW_E_NO_SCENE, RTW_E_UNSUPPORTED = -1, -2, -3, -4, -5
+RTW_E_INVALID, RTW_E_DEVICE, RTW_E_NO_LIGHTS, RTW_E_NO_SCENE, RTW_E_UNSUPPORTED, RTW_E_PANIC = -1, -2, -3, -4, -5, -6
 RTW_F32, RTW_F64 = 0, 1
 RTW_LAMBERTIAN, RTW_METAL, RTW_DIELECTRIC, RTW_INVISIBLE, RTW_DIFFUSE_LIGHT = 0, 1, 2, 3, 4
 RTW_ACCEL_AUTO, RTW_ACCEL_BRUTE, RTW_ACCEL_BVH = 0, 1, 2
+RTW_TEX_SOLID, RTW_TEX_CHECKER, RTW_TEX_NOISE = 0, 1, 2
+RTW_LIGHT_SPHERE, RTW_LIGHT_QUAD, RTW_LIGHT_DEFAULT = 0, 1, 2
+RTW_LIGHTS_BVH_LEAF = 1
 
 _f64p = C.POINTER(C.c_double)
 _u32p = C.POINTER(C.c_uint32)
@@ -57,10 +60,13 @@ class rtw_scene(C.Structure):
         ("n_quads", C.c_uint32), ("quads", _f64p), ("quad_mat", _u32p),
         ("n_light_quads", C.c_uint32), ("light_quads", _f64p), ("light_kinds", _u32p),
         ("n_boxes", C.c_uint32), ("boxes", _f64p), ("box_mat", _u32p),
+        ("mat_tex", _u32p), ("n_textures", C.c_uint32), ("tex_type", _u32p), ("tex_params", _f64p),
+        ("tex_refs", _u32p), ("n_perlin", C.c_uint32), ("perlin_vec", _f64p), ("perlin_perm", _u32p),
+        ("n_light_other", C.c_uint32), ("light_flags", C.c_uint32),
     ]
 
 
-ABI_VERSION = 4     # RTW_ABI_VERSION of include/rtw.h
+ABI_VERSION = 5     # RTW_ABI_VERSION of include/rtw.h
 
 
 class rtw_stats(C.Structure):
@@ -69,6 +75,7 @@ class rtw_stats(C.Structure):
         ("kernel_ms", C.c_double), ("accel", C.c_uint32), ("chunk", C.c_uint32),
         ("node_visits", C.c_uint64), ("sphere_tests", C.c_uint64),
         ("bvh_width", C.c_uint32), ("kernel", C.c_uint32),
+        ("panic_plane_uv", C.c_uint64), ("panic_no_lights", C.c_uint64),
     ]
 
 
@@ -98,6 +105,7 @@ PROTOTYPES = [
     ("rtw_world_camera_builder", None, [C.c_void_p, C.POINTER(rtw_camera_builder)]),
     ("rtw_world_free", None, [C.c_void_p]),
     ("rtw_scene_named", C.c_void_p, [C.c_char_p, C.c_uint64]),
+    ("rtw_perlin_generate", C.c_int, [C.c_uint64, _f64p, _u32p]),
     ("rtw_encode_rgb8", C.c_int, [_f64p, C.c_uint32, C.c_uint32, C.c_uint32,
                                   C.POINTER(C.c_uint8)]),
     ("rtw_write_ppm", C.c_int, [C.c_char_p, _f64p, C.c_uint32, C.c_uint32, C.c_uint32]),

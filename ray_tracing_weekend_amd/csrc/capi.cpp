@@ -56,6 +56,7 @@ struct rtw_ctx {
     size_t partial_cap = 0;
     void* d_out = nullptr;
     size_t out_cap = 0;
+    static constexpr int kCounters = 6;   // rtw_kernels.h KParams::counters
     unsigned long long* d_counters = nullptr;
     std::vector<unsigned char> h_out;
     rtw_stats last{};
@@ -227,11 +228,11 @@ std::vector<unsigned char> stage_scene(const rtw_scene* s, rtw::DevScene<R>* ds,
     const size_t o_sph = reserve(sizeof(R4) * s->n_spheres);
     const size_t o_r = reserve(sizeof(R) * s->n_spheres);
     const size_t o_smat = reserve(sizeof(uint32_t) * s->n_spheres);
-    const size_t o_pl = reserve(sizeof(R) * 12 * s->n_planes);
+    const size_t o_pl = reserve(sizeof(R) * rtw::kPlaneR * s->n_planes);
     const size_t o_quads = reserve(sizeof(R) * rtw::kQuadR * s->n_quads);
     const size_t o_qmat = reserve(sizeof(uint32_t) * s->n_quads);
     const size_t o_lquads = reserve(sizeof(R) * rtw::kQuadR * s->n_light_quads);
-    const uint32_t n_list = s->n_lights + s->n_light_quads;
+    const uint32_t n_list = s->n_lights + s->n_light_quads + s->n_light_other;
     const size_t o_lref = reserve(sizeof(uint32_t) * n_list);
     const size_t o_boxes = reserve(sizeof(R) * rtw::kBoxR * s->n_boxes);
     const size_t o_bmat = reserve(sizeof(uint32_t) * s->n_boxes);
@@ -239,6 +240,13 @@ std::vector<unsigned char> stage_scene(const rtw_scene* s, rtw::DevScene<R>* ds,
     const size_t o_mt = reserve(sizeof(uint32_t) * s->n_materials);
     const size_t o_mp = reserve(sizeof(R4) * s->n_materials);
     const size_t o_li = reserve(sizeof(R4) * s->n_lights);
+    const bool tex = s->mat_tex != nullptr;
+    const size_t o_mtex = reserve(sizeof(uint32_t) * (tex ? s->n_materials : 0));
+    const size_t o_ttype = reserve(sizeof(uint32_t) * (tex ? s->n_textures : 0));
+    const size_t o_tp = reserve(sizeof(R4) * (tex ? s->n_textures : 0));
+    const size_t o_trefs = reserve(sizeof(uint32_t) * 2 * (tex ? s->n_textures : 0));
+    const size_t o_pvec = reserve(sizeof(R4) * 256 * (tex ? s->n_perlin : 0));
+    const size_t o_pperm = reserve(sizeof(uint32_t) * 768 * (tex ? s->n_perlin : 0));
     // BVH over the spheres; boxes padded outward by a margin that absorbs the
     // rounding of the slab test in precision R (it only ever culls)
     const rtw::BvhBuild bb = rtw::build_bvh(s->spheres, s->n_spheres,
@@ -285,9 +293,21 @@ std::vector<unsigned char> stage_scene(const rtw_scene* s, rtw::DevScene<R>* ds,
                    fz = fabs(pl[3]) < e && fabs(pl[4]) < e;
         const double box[6] = {fx ? 0.0 : -INFINITY, fy ? 0.0 : -INFINITY, fz ? 0.0 : -INFINITY,
                                fx ? 0.0 : INFINITY, fy ? 0.0 : INFINITY, fz ? 0.0 : INFINITY};
-        R* dst = reinterpret_cast<R*>(b + o_pl) + 12 * k;
+        R* dst = reinterpret_cast<R*>(b + o_pl) + rtw::kPlaneR * k;
         for (int q = 0; q < 6; ++q) dst[q] = (R)pl[q];
         for (int q = 0; q < 6; ++q) dst[6 + q] = (R)box[q];
+        // Plane::get_plane_uv's constants (plane.rs:40-54), computed as the
+        // oracle's plane_uv does: theta = atan2(|n x V|, n . V), V = (0, 1, 0)
+        const double c[3] = {pl[4] * 0.0 - pl[5] * 1.0, pl[5] * 0.0 - pl[3] * 0.0, pl[3] * 1.0 - pl[4] * 0.0};
+        const double clen = sqrt(c[0] * c[0] + c[1] * c[1] + c[2] * c[2]);
+        const double theta = atan2(clen, pl[3] * 0.0 + pl[4] * 1.0 + pl[5] * 0.0);
+        const double kv[3] = {c[0] / clen, c[1] / clen, c[2] / clen};
+        const bool kfin = std::isfinite(kv[0]) && std::isfinite(kv[1]) && std::isfinite(kv[2]);
+        dst[12] = theta <= e ? (R)0 : (kfin ? (R)1 : (R)2);
+        dst[13] = (R)cos(theta);
+        dst[14] = (R)sin(theta);
+        for (int q = 0; q < 3; ++q) dst[15 + q] = kfin ? (R)kv[q] : (R)0;
+        dst[18] = dst[19] = (R)0;
     }
     for (uint32_t k = 0; k < s->n_planes; ++k) reinterpret_cast<uint32_t*>(b + o_pmat)[k] = s->plane_mat[k];
     // quads: derived in f64; the AABB is rounded outward into R (a cull only)
@@ -330,10 +350,34 @@ std::vector<unsigned char> stage_scene(const rtw_scene* s, rtw::DevScene<R>* ds,
     {
         uint32_t ns = 0, nq = 0;
         for (uint32_t k = 0; k < n_list; ++k) {
-            const bool quad = s->light_kinds ? s->light_kinds[k] != 0 : k >= s->n_lights;
-            reinterpret_cast<uint32_t*>(b + o_lref)[k] = quad ? (0x80000000u | nq++) : ns++;
+            const uint32_t kind = s->light_kinds ? s->light_kinds[k] : (k >= s->n_lights ? 1u : 0u);
+            reinterpret_cast<uint32_t*>(b + o_lref)[k] =
+                kind == RTW_LIGHT_QUAD ? (rtw::kLrefQuad | nq++) : (kind == RTW_LIGHT_DEFAULT ? rtw::kLrefDefault : ns++);
         }
     }
+    if (tex) {
+        for (uint32_t k = 0; k < s->n_materials; ++k) reinterpret_cast<uint32_t*>(b + o_mtex)[k] = s->mat_tex[k];
+        for (uint32_t k = 0; k < s->n_textures; ++k) {
+            const double* tp = s->tex_params + 4 * k;
+            reinterpret_cast<uint32_t*>(b + o_ttype)[k] = s->tex_type[k];
+            reinterpret_cast<R4*>(b + o_tp)[k] = R4{(R)tp[0], (R)tp[1], (R)tp[2], (R)tp[3]};
+            reinterpret_cast<uint32_t*>(b + o_trefs)[2 * k] = s->tex_refs[2 * k];
+            reinterpret_cast<uint32_t*>(b + o_trefs)[2 * k + 1] = s->tex_refs[2 * k + 1];
+        }
+        for (uint32_t k = 0; k < 256 * s->n_perlin; ++k) {
+            const double* v = s->perlin_vec + 3 * k;
+            reinterpret_cast<R4*>(b + o_pvec)[k] = R4{(R)v[0], (R)v[1], (R)v[2], (R)0};
+        }
+        for (uint32_t k = 0; k < 768 * s->n_perlin; ++k)
+            reinterpret_cast<uint32_t*>(b + o_pperm)[k] = s->perlin_perm[k];
+    }
+    ds->mat_tex = tex ? reinterpret_cast<const uint32_t*>(base + o_mtex) : nullptr;
+    ds->tex_type = reinterpret_cast<const uint32_t*>(base + o_ttype);
+    ds->tex_p = reinterpret_cast<const R4*>(base + o_tp);
+    ds->tex_refs = reinterpret_cast<const uint32_t*>(base + o_trefs);
+    ds->perlin_vec = reinterpret_cast<const R4*>(base + o_pvec);
+    ds->perlin_perm = reinterpret_cast<const uint32_t*>(base + o_pperm);
+    ds->light_flags = s->light_flags;
     for (uint32_t k = 0; k < s->n_materials; ++k) {
         const double* m = s->mat_params + 5 * k;
         const uint32_t t = s->mat_type[k];
@@ -356,7 +400,7 @@ std::vector<unsigned char> stage_scene(const rtw_scene* s, rtw::DevScene<R>* ds,
     ds->quads = reinterpret_cast<const R*>(base + o_quads);
     ds->quad_mat = reinterpret_cast<const uint32_t*>(base + o_qmat);
     ds->lquads = reinterpret_cast<const R*>(base + o_lquads);
-    ds->lref = s->n_light_quads ? reinterpret_cast<const uint32_t*>(base + o_lref) : nullptr;
+    ds->lref = (s->n_light_quads || s->n_light_other) ? reinterpret_cast<const uint32_t*>(base + o_lref) : nullptr;
     ds->n_quads = s->n_quads;
     ds->n_lquads = s->n_light_quads;
     ds->n_list = n_list;
@@ -460,15 +504,54 @@ int validate_scene(rtw_ctx* c, const rtw_scene* s) {
         (s->n_quads && (!s->quads || !s->quad_mat)) || (s->n_light_quads && !s->light_quads) ||
         (s->n_boxes && (!s->boxes || !s->box_mat)))
         return fail(c, RTW_E_INVALID, "scene array pointer is NULL");
+    const uint32_t n_list = s->n_lights + s->n_light_quads + s->n_light_other;
     if (s->light_kinds) {
-        uint32_t nq = 0;
-        for (uint32_t k = 0; k < s->n_lights + s->n_light_quads; ++k) nq += s->light_kinds[k] ? 1 : 0;
-        if (nq != s->n_light_quads) return fail(c, RTW_E_INVALID, "light_kinds does not match the light counts");
+        uint32_t cnt[3] = {0, 0, 0};
+        for (uint32_t k = 0; k < n_list; ++k) {
+            if (s->light_kinds[k] > RTW_LIGHT_DEFAULT) return fail(c, RTW_E_INVALID, "unknown light kind");
+            ++cnt[s->light_kinds[k]];
+        }
+        if (cnt[0] != s->n_lights || cnt[1] != s->n_light_quads || cnt[2] != s->n_light_other)
+            return fail(c, RTW_E_INVALID, "light_kinds does not match the light counts");
+    } else if (s->n_light_other) {
+        return fail(c, RTW_E_INVALID, "n_light_other needs light_kinds");
     }
-    bool lambertian = false;
-    for (uint32_t k = 0; k < s->n_materials; ++k) {
+    if (s->light_flags & ~(uint32_t)RTW_LIGHTS_BVH_LEAF) return fail(c, RTW_E_INVALID, "unknown light_flags");
+    if ((s->light_flags & RTW_LIGHTS_BVH_LEAF) && n_list > 5)
+        return fail(c, RTW_E_UNSUPPORTED, "a BVH light list of more than 5 entries is not a leaf: the reference's "
+                                          "BVH aux_random indexes it inconsistently (bvh.rs:78-92)");
+    for (uint32_t k = 0; k < s->n_materials; ++k)
         if (s->mat_type[k] > RTW_DIFFUSE_LIGHT) return fail(c, RTW_E_INVALID, "unknown material type");
-        lambertian |= s->mat_type[k] == RTW_LAMBERTIAN;
+    if (s->mat_tex) {
+        if ((s->n_textures && (!s->tex_type || !s->tex_params || !s->tex_refs)) ||
+            (s->n_perlin && (!s->perlin_vec || !s->perlin_perm)))
+            return fail(c, RTW_E_INVALID, "texture array pointer is NULL");
+        for (uint32_t k = 0; k < s->n_materials; ++k)
+            if (s->mat_tex[k] >= s->n_textures) return fail(c, RTW_E_INVALID, "material texture id out of range");
+        for (uint32_t k = 0; k < s->n_textures; ++k) {
+            const uint32_t t = s->tex_type[k];
+            if (t > RTW_TEX_NOISE) return fail(c, RTW_E_INVALID, "unknown texture type");
+            if (t == RTW_TEX_CHECKER && (s->tex_refs[2 * k] >= s->n_textures || s->tex_refs[2 * k + 1] >= s->n_textures))
+                return fail(c, RTW_E_INVALID, "checker texture id out of range");
+            if (t == RTW_TEX_NOISE && s->tex_refs[2 * k] >= s->n_perlin)
+                return fail(c, RTW_E_INVALID, "noise texture Perlin table id out of range");
+        }
+        // nested checkers must bottom out (the reference's Arc<dyn Texture> tree)
+        for (uint32_t k = 0; k < s->n_textures; ++k) {
+            std::vector<uint32_t> stack{k};
+            uint32_t steps = 0;
+            while (!stack.empty()) {
+                const uint32_t t = stack.back();
+                stack.pop_back();
+                if (++steps > 4096) return fail(c, RTW_E_INVALID, "checker textures form a cycle or are too deep");
+                if (s->tex_type[t] == RTW_TEX_CHECKER) {
+                    stack.push_back(s->tex_refs[2 * t]);
+                    stack.push_back(s->tex_refs[2 * t + 1]);
+                }
+            }
+        }
+        for (uint32_t k = 0; k < 768 * s->n_perlin; ++k)
+            if (s->perlin_perm[k] > 255) return fail(c, RTW_E_INVALID, "Perlin permutation entry > 255");
     }
     for (uint32_t k = 0; k < s->n_spheres; ++k)
         if (s->sphere_mat[k] >= s->n_materials) return fail(c, RTW_E_INVALID, "sphere material id out of range");
@@ -478,9 +561,6 @@ int validate_scene(rtw_ctx* c, const rtw_scene* s) {
         if (s->quad_mat[k] >= s->n_materials) return fail(c, RTW_E_INVALID, "quad material id out of range");
     for (uint32_t k = 0; k < s->n_boxes; ++k)
         if (s->box_mat[k] >= s->n_materials) return fail(c, RTW_E_INVALID, "box material id out of range");
-    if (lambertian && s->n_lights + s->n_light_quads == 0)
-        return fail(c, RTW_E_NO_LIGHTS, "Lambertian material with an empty light list "
-                                        "(the reference panics: HittableList shouldn't be empty)");
     return RTW_OK;
 }
 
@@ -564,7 +644,7 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
     p.partial = reinterpret_cast<R*>(c->d_partial);
     p.counters = c->d_counters;
     if (!stream) stream = c->stream;
-    HIP_TRY(c, hipMemsetAsync(c->d_counters, 0, 4 * sizeof(unsigned long long), stream));
+    HIP_TRY(c, hipMemsetAsync(c->d_counters, 0, rtw_ctx::kCounters * sizeof(unsigned long long), stream));
     const size_t lds = (size_t)(p.sc.n_sph + p.sc.n_lights) * sizeof(rtw::R4<R>);
     int accel = c->accel == RTW_ACCEL_AUTO ? c->auto_accel : c->accel;
     if (accel == RTW_ACCEL_AUTO) accel = p.sc.n_sph >= 64 ? RTW_ACCEL_BVH : RTW_ACCEL_BRUTE;
@@ -616,6 +696,13 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
             return fail(c, RTW_E_UNSUPPORTED, "BVH deeper than the kernel's traversal stack");
         }
     }
+    // textured scenes have kernels for the brute-force and binary while-while worlds only
+    if (p.sc.mat_tex && (world == rtw::kWorldBvh4 || world == rtw::kWorldBvh)) {
+        world = rtw::kWorldBvhWW;
+        bvh_width = 2;
+        p.stack = std::max(p.sc.bvh_depth + 1, p.light_bvh ? p.sc.lbvh_depth + 1 : 1u);
+        if (p.stack > rtw::kBvhStack) return fail(c, RTW_E_UNSUPPORTED, "BVH deeper than the kernel's traversal stack");
+    }
     hipEvent_t* ev = c->ring[c->n_renders % rtw_ctx::kRing];
     HIP_TRY(c, hipEventRecord(c->ev0, stream));
     HIP_TRY(c, hipEventRecord(ev[0], stream));
@@ -657,7 +744,7 @@ rtw_ctx* rtw_create(int device, int precision) {
     c->precision = precision;
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
-        hipMalloc(reinterpret_cast<void**>(&c->d_counters), 4 * sizeof(unsigned long long)) != hipSuccess) {
+        hipMalloc(reinterpret_cast<void**>(&c->d_counters), rtw_ctx::kCounters * sizeof(unsigned long long)) != hipSuccess) {
         rtw_destroy(c);
         return nullptr;
     }
@@ -852,8 +939,10 @@ int rtw_set_scene(rtw_ctx* c, const rtw_scene* s) {
         fix(ds.quads); fix(ds.quad_mat); fix(ds.lquads);
         if (ds.lref) fix(ds.lref);
         fix(ds.boxes); fix(ds.box_mat);
+        if (ds.mat_tex) fix(ds.mat_tex);
+        fix(ds.tex_type); fix(ds.tex_p); fix(ds.tex_refs); fix(ds.perlin_vec); fix(ds.perlin_perm);
     };
-    static_assert(offsetof(rtw::DevScene<float>, n_sph) == 21 * sizeof(void*),
+    static_assert(offsetof(rtw::DevScene<float>, n_sph) == 27 * sizeof(void*),
                   "DevScene gained a pointer: update rebase");
     if (c->precision == RTW_F32) {
         rebase(tmp32);
@@ -891,7 +980,7 @@ int rtw_get_stats(rtw_ctx* c, rtw_stats* out) {
     if (!c || !out) return RTW_E_INVALID;
     HIP_TRY(c, hipSetDevice(c->device));
     HIP_TRY(c, hipEventSynchronize(c->ev1));
-    unsigned long long h[4] = {0, 0, 0, 0};
+    unsigned long long h[rtw_ctx::kCounters] = {};
     HIP_TRY(c, hipMemcpy(h, c->d_counters, sizeof h, hipMemcpyDeviceToHost));
     float ms = 0.f;
     HIP_TRY(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
@@ -901,7 +990,15 @@ int rtw_get_stats(rtw_ctx* c, rtw_stats* out) {
     // the brute-force sweep tests every sphere on every segment
     c->last.sphere_tests = c->last.accel == RTW_ACCEL_BVH ? h[3] : h[0] * (uint64_t)c->last_n_sph;
     c->last.kernel_ms = ms;
+    c->last.panic_plane_uv = h[4];
+    c->last.panic_no_lights = h[5];
     *out = c->last;
+    if (h[5])
+        return fail(c, RTW_E_NO_LIGHTS, std::to_string(h[5]) + " samples drew a light from an empty light list "
+                                        "(the reference panics: HittableList shouldn't be empty, hittable_list.rs:417)");
+    if (h[4])
+        return fail(c, RTW_E_PANIC, std::to_string(h[4]) + " plane tests produced a non-finite UV "
+                                    "(the reference panics in Plane::hit, plane.rs:66-69)");
     return RTW_OK;
 }
 
@@ -946,9 +1043,8 @@ int rtw_render(rtw_ctx* c, const rtw_camera* cam, const rtw_scene* scene, uint64
     }
     rtw_stats st{};
     rc = rtw_get_stats(c, &st);
-    if (rc) return rc;
     if (stats) *stats = st;
-    return RTW_OK;
+    return rc;
 }
 
 // ------------------------------------------------------------ scenes::simple
@@ -982,17 +1078,31 @@ rtw_world* rtw_scene_named(const char* name, uint64_t seed) {
     const std::string n = name;
     if (n == "simple") return rtw_scene_simple(seed, 11);
     try {
-        if (n == "cornell_box") {
-            auto t = rtw::scenes::cornell_box();
-            rtw_world* w = new rtw_world();
-            w->flat = rtw::flatten(std::get<0>(t), std::get<1>(t));
-            w->view = w->flat.view();
-            w->cam = std::get<2>(t).raw();
-            return w;
-        }
+        std::tuple<rtw::HittableList, rtw::HittableList, rtw::CameraBuilder> t;
+        if (n == "cornell_box") t = rtw::scenes::cornell_box();
+        else if (n == "debug") t = rtw::scenes::debugging_scene(seed);
+        else if (n == "checkered_spheres") t = rtw::scenes::checkered_spheres();
+        else if (n == "perlin_spheres") t = rtw::scenes::perlin_spheres(seed);
+        else if (n == "plane") t = rtw::scenes::plane();
+        else if (n == "simple_light") t = rtw::scenes::simple_light(seed);
+        else if (n == "simple_transform") t = rtw::scenes::simple_transform(seed);
+        else return nullptr;
+        rtw_world* w = new rtw_world();
+        w->flat = rtw::flatten(std::get<0>(t), std::get<1>(t));
+        w->view = w->flat.view();
+        w->cam = std::get<2>(t).raw();
+        return w;
     } catch (...) {
     }
     return nullptr;
+}
+
+int rtw_perlin_generate(uint64_t seed, double* rand_vec, uint32_t* perm) {
+    if (!rand_vec || !perm) return RTW_E_INVALID;
+    auto p = rtw::Perlin::generate(seed);
+    memcpy(rand_vec, p->rand_vec.data(), sizeof(double) * 768);
+    memcpy(perm, p->perm.data(), sizeof(uint32_t) * 768);
+    return RTW_OK;
 }
 
 // ------------------------------------------------------------ output encoding

@@ -5,6 +5,8 @@
 #include <string.h>
 
 #include <cstdio>
+#include <functional>
+#include <unordered_map>
 
 namespace rtw {
 
@@ -62,6 +64,70 @@ double HostRng::uniform_incl(double low, double high) {
     double v01 = unit12(next()) - 1.0;
     return v01 * scale + low;
 }
+uint64_t HostRng::uniform_u64(uint64_t low, uint64_t high) {
+    // rand 0.8.6 UniformInt<usize>::new(low, high) = new_inclusive(low, high - 1):
+    // range = high - low, zone = u64::MAX - (2^64 - range) % range; sample:
+    // (hi, lo) = next_u64 * range, accept lo <= zone, return low + hi
+    const uint64_t range = high - low;
+    const uint64_t reject = (0 - range) % range;   // (u64::MAX - range + 1) % range
+    const uint64_t zone = ~0ULL - reject;
+    for (;;) {
+        const unsigned __int128 m = (unsigned __int128)next() * range;
+        if ((uint64_t)m <= zone) return low + (uint64_t)(m >> 64);
+    }
+}
+Vec3 HostRng::unit_sphere() {
+    for (;;) {
+        const double a = 2.0 * standard() - 1.0, b = 2.0 * standard() - 1.0, c = 2.0 * standard() - 1.0;
+        if (a * a + b * b + c * c < 1.0) return {a, b, c};
+    }
+}
+
+// ---------------------------------------------------------------- textures
+std::shared_ptr<const Perlin> Perlin::generate(uint64_t seed) {
+    auto p = std::make_shared<Perlin>();
+    HostRng rng(seed);
+    for (int i = 0; i < 256; ++i) {            // perlin.rs:47-51
+        const Vec3 v = rng.unit_sphere();
+        p->rand_vec[3 * i] = v.x;
+        p->rand_vec[3 * i + 1] = v.y;
+        p->rand_vec[3 * i + 2] = v.z;
+    }
+    for (int axis = 0; axis < 3; ++axis) {     // perlin_generate_perm, perlin.rs:30-44
+        uint32_t* perm = p->perm.data() + 256 * axis;
+        for (uint32_t i = 0; i < 256; ++i) perm[i] = i;
+        for (uint64_t i = 0; i < 255; ++i) {
+            const uint64_t j = rng.uniform_u64(i, 256);
+            std::swap(perm[i], perm[j]);
+        }
+    }
+    return p;
+}
+std::shared_ptr<const Texture> Texture::solid(Colour c) {
+    auto t = std::make_shared<Texture>();
+    t->kind = RTW_TEX_SOLID;
+    t->colour = c;
+    return t;
+}
+std::shared_ptr<const Texture> Texture::checker(std::shared_ptr<const Texture> even,
+                                                std::shared_ptr<const Texture> odd, double scale) {
+    auto t = std::make_shared<Texture>();
+    t->kind = RTW_TEX_CHECKER;
+    t->scale = 1.0 / scale;                    // inv_scale: scale.recip(), texture.rs:32-38
+    t->even = std::move(even);
+    t->odd = std::move(odd);
+    return t;
+}
+std::shared_ptr<const Texture> Texture::checker(Colour even, Colour odd, double scale) {
+    return checker(solid(even), solid(odd), scale);
+}
+std::shared_ptr<const Texture> Texture::noise(double scale, uint64_t perlin_seed) {
+    auto t = std::make_shared<Texture>();
+    t->kind = RTW_TEX_NOISE;
+    t->scale = scale;
+    t->perlin = Perlin::generate(perlin_seed);
+    return t;
+}
 
 // ---------------------------------------------------------------- flatten
 rtw_scene FlatScene::view() const {
@@ -86,6 +152,16 @@ rtw_scene FlatScene::view() const {
     s.n_boxes = (uint32_t)box_mat.size();
     s.boxes = boxes.data();
     s.box_mat = box_mat.data();
+    s.mat_tex = textured ? mat_tex.data() : nullptr;
+    s.n_textures = (uint32_t)tex_type.size();
+    s.tex_type = tex_type.data();
+    s.tex_params = tex_params.data();
+    s.tex_refs = tex_refs.data();
+    s.n_perlin = (uint32_t)(perlin_perm.size() / 768);
+    s.perlin_vec = perlin_vec.data();
+    s.perlin_perm = perlin_perm.data();
+    s.n_light_other = n_light_other;
+    s.light_flags = light_flags;
     return s;
 }
 
@@ -121,9 +197,55 @@ Transformation Transformation::rotation(double angle_deg, int axis) {
 
 FlatScene flatten(const HittableList& world, const HittableList& lights) {
     FlatScene f;
+    // textures and Perlin tables, each shared object once (Arc identity)
+    std::unordered_map<const Texture*, uint32_t> tex_ids;
+    std::vector<const Perlin*> perlin_ids;
+    std::function<uint32_t(const std::shared_ptr<const Texture>&)> push_tex =
+        [&](const std::shared_ptr<const Texture>& t) -> uint32_t {
+        auto it = tex_ids.find(t.get());
+        if (it != tex_ids.end()) return it->second;
+        const uint32_t id = (uint32_t)f.tex_type.size();
+        tex_ids.emplace(t.get(), id);
+        f.tex_type.push_back(t->kind);
+        f.tex_params.insert(f.tex_params.end(), {t->colour.x, t->colour.y, t->colour.z, t->scale});
+        f.tex_refs.insert(f.tex_refs.end(), {0u, 0u});
+        if (t->kind == RTW_TEX_CHECKER) {
+            const uint32_t e = push_tex(t->even), o = push_tex(t->odd);
+            f.tex_refs[2 * id] = e;
+            f.tex_refs[2 * id + 1] = o;
+        } else if (t->kind == RTW_TEX_NOISE) {
+            uint32_t q = 0;
+            while (q < perlin_ids.size() && perlin_ids[q] != t->perlin.get()) ++q;
+            if (q == perlin_ids.size()) {
+                perlin_ids.push_back(t->perlin.get());
+                f.perlin_vec.insert(f.perlin_vec.end(), t->perlin->rand_vec.begin(), t->perlin->rand_vec.end());
+                f.perlin_perm.insert(f.perlin_perm.end(), t->perlin->perm.begin(), t->perlin->perm.end());
+            }
+            f.tex_refs[2 * id] = q;
+        }
+        return id;
+    };
+    auto textured = [](const Material& m) {
+        return m.texture && (m.type == RTW_LAMBERTIAN || m.type == RTW_DIFFUSE_LIGHT);
+    };
+    for (const Plane& o : world.planes()) f.textured |= textured(o.mat);
+    for (const Sphere& o : world.spheres()) f.textured |= textured(o.mat);
+    for (const Quad& o : world.quads()) f.textured |= textured(o.mat);
+    for (const Cuboid& o : world.cuboids()) f.textured |= textured(o.mat);
     auto push_mat = [&](const Material& m) {
         f.mat_type.push_back(m.type);
         f.mat_params.insert(f.mat_params.end(), {m.albedo.x, m.albedo.y, m.albedo.z, m.fuzz, m.ior});
+        if (f.textured) {
+            // a material without a texture gets its SolidColour as one
+            if (textured(m)) {
+                f.mat_tex.push_back(push_tex(m.texture));
+            } else {
+                f.mat_tex.push_back((uint32_t)f.tex_type.size());
+                f.tex_type.push_back(RTW_TEX_SOLID);
+                f.tex_params.insert(f.tex_params.end(), {m.albedo.x, m.albedo.y, m.albedo.z, 0.0});
+                f.tex_refs.insert(f.tex_refs.end(), {0u, 0u});
+            }
+        }
         return (uint32_t)(f.mat_type.size() - 1);
     };
     for (const Plane& p : world.planes()) {
@@ -146,19 +268,27 @@ FlatScene flatten(const HittableList& world, const HittableList& lights) {
         f.boxes.insert(f.boxes.end(), {c.xform.T.x, c.xform.T.y, c.xform.T.z});
         f.box_mat.push_back(push_mat(c.mat));
     }
-    if (!lights.planes().empty() || !lights.cuboids().empty())
-        throw Error(RTW_E_UNSUPPORTED, "planes and cuboids as lights are outside this build's scope");
+    // Planes and Transformed<Cuboid>s have no pdf_value / random of their own:
+    // in a light list they are RTW_LIGHT_DEFAULT entries (hittable.rs:175-181)
     for (const auto& e : lights.order()) {
         if (e.first == HittableList::kSphere) {
             const Sphere& s = lights.spheres()[e.second];
             f.lights.insert(f.lights.end(), {s.center.x, s.center.y, s.center.z, s.radius});
-            f.light_kinds.push_back(0);
-        } else {
+            f.light_kinds.push_back(RTW_LIGHT_SPHERE);
+        } else if (e.first == HittableList::kQuad) {
             const Quad& q = lights.quads()[e.second];
             f.light_quads.insert(f.light_quads.end(),
                                  {q.q.x, q.q.y, q.q.z, q.u.x, q.u.y, q.u.z, q.v.x, q.v.y, q.v.z});
-            f.light_kinds.push_back(1);
+            f.light_kinds.push_back(RTW_LIGHT_QUAD);
+        } else {
+            f.light_kinds.push_back(RTW_LIGHT_DEFAULT);
+            ++f.n_light_other;
         }
+    }
+    if (lights.is_bvh()) {
+        if (lights.len() > 5)
+            throw Error(RTW_E_UNSUPPORTED, "a BVH light list of more than 5 entries (bvh.rs:78-92)");
+        f.light_flags |= RTW_LIGHTS_BVH_LEAF;
     }
     return f;
 }
@@ -288,6 +418,119 @@ std::tuple<HittableList, HittableList, CameraBuilder> cornell_box() {
     cam.with_lookfrom(lookfrom).with_lookat(lookat).with_vfov(40.0).with_defocus_angle(0.0).with_focus_dist(
         sqrt(vdot(d, d)));
     return {std::move(world), std::move(lights), cam};
+}
+
+namespace {
+double dist(Point3 a, Point3 b) {   // (lookfrom - lookat).length()
+    const Vec3 d{a.x - b.x, a.y - b.y, a.z - b.z};
+    return sqrt(vdot(d, d));
+}
+// the eight wall quads of debugging_scene / simple_transform (lib.rs:416-466, :549-599)
+void add_walls(HittableList& world, const Material& white) {
+    const double c[4][2] = {{6, 6}, {-6, 6}, {-6, -6}, {6, -6}};
+    for (const auto& xz : c) {
+        const double sx = xz[0] > 0 ? -2.0 : 2.0, sz = xz[1] > 0 ? -2.0 : 2.0;
+        world.add(Quad{{xz[0], 0, xz[1]}, {0, 2, 0}, {sx, 0, 0}, white});
+        world.add(Quad{{xz[0], 0, xz[1]}, {0, 2, 0}, {0, 0, sz}, white});
+    }
+}
+}  // namespace
+
+std::tuple<HittableList, HittableList, CameraBuilder> perlin_spheres(uint64_t seed) {
+    HittableList world, lights;
+    const Material pertext = Material::lambertian_tex(Texture::noise(4.0, seed));
+    world.add(Plane({0, 0, 0}, {0, 1, 0}, pertext));
+    world.add(Sphere{{0, 2, 0}, 2.0, pertext});
+    world.add(Sphere{{-5, 1, 5}, 1.0, Material::lambertian({1, 0, 0})});
+    world.add(Sphere{{-5, 1, -5}, 1.0, Material::lambertian({0, 1, 0})});
+    world.add(Sphere{{5, 1, -5}, 1.0, Material::lambertian({0, 0, 1})});
+    world.add(Sphere{{5, 1, 5}, 1.0, Material::lambertian({0.5, 0, 0.5})});
+    const Point3 lookfrom{0, 30, 0}, lookat{0, 0, 0};
+    CameraBuilder cam;
+    cam.with_lookfrom(lookfrom).with_lookat(lookat).with_focus_dist(dist(lookfrom, lookat)).with_vfov(40.0)
+        .with_background({1, 1, 1});
+    return {std::move(world), std::move(lights), cam};
+}
+
+std::tuple<HittableList, HittableList, CameraBuilder> plane() {
+    HittableList world, lights;
+    world.add(Plane({0, 0, 0}, {0, 1, 0},
+                    Material::lambertian_tex(Texture::checker(Colour{0.2, 0.3, 0.1}, Colour{0.9, 0.9, 0.9}, 0.32))));
+    const Point3 lookfrom{0, 30, 0}, lookat{0, 0, 0};
+    CameraBuilder cam;
+    cam.with_lookfrom(lookfrom).with_lookat(lookat).with_focus_dist(dist(lookfrom, lookat)).with_vfov(40.0)
+        .with_background({1, 1, 1});
+    return {std::move(world), std::move(lights), cam};
+}
+
+std::tuple<HittableList, HittableList, CameraBuilder> checkered_spheres() {
+    HittableList world, lights;
+    const Material checker =
+        Material::lambertian_tex(Texture::checker(Colour{0.2, 0.3, 0.1}, Colour{0.9, 0.9, 0.9}, 0.01));
+    world.add(Sphere{{0, -10, 0}, 10.0, checker});
+    world.add(Sphere{{0, 10, 0}, 10.0, checker});
+    lights.add(Sphere{{0, 0, 0}, 0.1, checker});
+    const Point3 lookfrom{40, 1, 0}, lookat{0, 0, 0};
+    CameraBuilder cam;
+    cam.with_lookfrom(lookfrom).with_lookat(lookat).with_focus_dist(dist(lookfrom, lookat)).with_vfov(40.0)
+        .with_background({1, 1, 1});
+    return {std::move(world), std::move(lights), cam};
+}
+
+std::tuple<HittableList, HittableList, CameraBuilder> simple_light(uint64_t seed) {
+    HittableList world, lights;
+    const Material pertext = Material::lambertian_tex(Texture::noise(4.0, seed));
+    const Material difflight = Material::diffuse_light({4, 4, 4});
+    world.add(Plane({0, 0, 0}, {0, 1, 0}, pertext));
+    world.add(Sphere{{0, 2, 0}, 2.0, pertext});
+    world.add(Quad{{3, 1, -2}, {2, 0, 0}, {0, 2, 0}, difflight});
+    lights.add(Quad{{3, 1, -2}, {2, 0, 0}, {0, 2, 0}, difflight});
+    const Point3 lookfrom{26, 3, 6}, lookat{0, 2, 0};
+    CameraBuilder cam;
+    cam.with_lookfrom(lookfrom).with_lookat(lookat).with_focus_dist(dist(lookfrom, lookat)).with_vfov(40.0);
+    return {std::move(world), std::move(lights), cam};
+}
+
+std::tuple<HittableList, HittableList, CameraBuilder> debugging_scene(uint64_t seed) {
+    HittableList world, lights;
+    const Material pertext = Material::lambertian_tex(Texture::noise(4.0, seed));
+    world.add(Plane({0, 0, 0}, {0, 1, 0}, pertext));
+    world.add(Sphere{{0, 2, 0}, 2.0, pertext});
+    add_walls(world, Material::lambertian({0.75, 0.75, 0.75}));
+    const Sphere ls[4] = {{{5, 1, 5}, 1.0, Material::diffuse_light({0.5, 0, 0.5})},
+                          {{-5, 1, 5}, 1.0, Material::diffuse_light({1, 0, 0})},
+                          {{-5, 1, -5}, 1.0, Material::diffuse_light({0, 1, 0})},
+                          {{5, 1, -5}, 1.0, Material::diffuse_light({0, 0, 1})}};
+    for (const Sphere& s : ls) {
+        world.add(s);
+        lights.add(s);
+    }
+    const Point3 lookfrom{0, 20, 0}, lookat{0, 0, 0};
+    CameraBuilder cam;
+    cam.with_image_width(3).with_image_height(2).with_samples_per_pixel(10).with_max_depth(5)
+        .with_lookfrom(lookfrom).with_lookat(lookat).with_focus_dist(4.0);
+    return {world.into_bvh(), lights.into_bvh(), cam};
+}
+
+std::tuple<HittableList, HittableList, CameraBuilder> simple_transform(uint64_t seed) {
+    HittableList world, lights;
+    const Material pertext = Material::lambertian_tex(Texture::noise(4.0, seed));
+    world.add(Plane({0, 0, 0}, {0, 1, 0}, pertext));
+    add_walls(world, Material::lambertian({0.75, 0.75, 0.75}));
+    const Cuboid original{{0, 0, 0}, {1, 1, 1}, Material::diffuse_light({1, 0, 0})};
+    const Cuboid boxes[3] = {
+        original.transform(Transformation::translation({-0.5, 0, -0.5})),
+        original.transform(Transformation::translation({2, 0, 2})),
+        original.transform(Transformation::translation({-3, 0, -3})).transform(Transformation::rotation(45.0, 1))};
+    for (const Cuboid& c : boxes) {
+        world.add(c);
+        lights.add(c);
+    }
+    const Point3 lookfrom{0, 20, 0}, lookat{0, 0, 0};
+    CameraBuilder cam;
+    cam.with_image_width(3).with_image_height(2).with_samples_per_pixel(10).with_max_depth(5)
+        .with_lookfrom(lookfrom).with_lookat(lookat).with_focus_dist(4.0);
+    return {world.into_bvh(), lights.into_bvh(), cam};
 }
 }  // namespace scenes
 

@@ -10,7 +10,10 @@
 //   Sphere / Plane                shared/src/entities/sphere.rs:24-47, plane.rs:20-38
 //   Lambertian/Metal/Dialectric/Invisible   shared/src/material.rs:321-488
 //   SampledColour (+ Display)     shared/src/colour.rs:14-36, 136-148
-//   scenes::simple                scenes/src/lib.rs:155-233
+//   SolidColour / CheckerTexture / NoiseTexture   shared/src/texture.rs:15-102
+//   Perlin::new                   shared/src/perlin.rs:27-58
+//   BoundedVolumeHierarchy::from  shared/src/hittable_collections/bvh.rs:106-143 (as a list flag)
+//   the scene generators          scenes/src/lib.rs:40-653
 #pragma once
 
 #include <stdint.h>
@@ -33,19 +36,47 @@ struct Vec3 {
 using Point3 = Vec3;
 using Colour = Vec3;
 
+// Perlin::new (perlin.rs:46-58) from the build's seeded RNG (the reference
+// draws the tables from thread_rng): rand_vec = 256 UnitSphere samples, then
+// perm_x, perm_y, perm_z, each the identity shuffled by j = Uniform::new(i, 256).
+struct Perlin {
+    std::array<double, 768> rand_vec{};
+    std::array<uint32_t, 768> perm{};   // perm_x, perm_y, perm_z
+    static std::shared_ptr<const Perlin> generate(uint64_t seed);
+};
+
+// Arc<dyn Texture>: SolidColour, CheckerTexture (even / odd textures and
+// inv_scale = scale.recip()), NoiseTexture (scale + its own Perlin).
+struct Texture {
+    uint32_t kind = RTW_TEX_SOLID;
+    Colour colour{};
+    double scale = 1.0;                 // checker: inv_scale; noise: scale
+    std::shared_ptr<const Texture> even, odd;
+    std::shared_ptr<const Perlin> perlin;
+    static std::shared_ptr<const Texture> solid(Colour c);
+    static std::shared_ptr<const Texture> checker(std::shared_ptr<const Texture> even,
+                                                  std::shared_ptr<const Texture> odd, double scale);
+    static std::shared_ptr<const Texture> checker(Colour even, Colour odd, double scale);   // new_with_colours
+    static std::shared_ptr<const Texture> noise(double scale, uint64_t perlin_seed);
+};
+
 // One material record.  DynMaterial in the reference is a pointer to a trait
 // object; here it is a small value type with the parameters the kernels read.
+// `texture` (Lambertian, DiffuseLight) null = SolidColour(albedo).
 struct Material {
     uint32_t type = RTW_INVISIBLE;
     Colour albedo{};
     double fuzz = 0.0;
     double ior = 0.0;
+    std::shared_ptr<const Texture> texture;
 
-    static Material lambertian(Colour albedo) { return {RTW_LAMBERTIAN, albedo, 0.0, 0.0}; }
-    static Material metal(Colour albedo, double fuzz) { return {RTW_METAL, albedo, fuzz, 0.0}; }
-    static Material dialectric(double ior) { return {RTW_DIELECTRIC, {1, 1, 1}, 0.0, ior}; }
-    static Material invisible() { return {RTW_INVISIBLE, {0, 0, 0}, 0.0, 0.0}; }
-    static Material diffuse_light(Colour emit) { return {RTW_DIFFUSE_LIGHT, emit, 0.0, 0.0}; }
+    static Material lambertian(Colour albedo) { return {RTW_LAMBERTIAN, albedo, 0.0, 0.0, nullptr}; }
+    static Material lambertian_tex(std::shared_ptr<const Texture> t) { return {RTW_LAMBERTIAN, {}, 0.0, 0.0, t}; }
+    static Material metal(Colour albedo, double fuzz) { return {RTW_METAL, albedo, fuzz, 0.0, nullptr}; }
+    static Material dialectric(double ior) { return {RTW_DIELECTRIC, {1, 1, 1}, 0.0, ior, nullptr}; }
+    static Material invisible() { return {RTW_INVISIBLE, {0, 0, 0}, 0.0, 0.0, nullptr}; }
+    static Material diffuse_light(Colour emit) { return {RTW_DIFFUSE_LIGHT, emit, 0.0, 0.0, nullptr}; }
+    static Material diffuse_light_tex(std::shared_ptr<const Texture> t) { return {RTW_DIFFUSE_LIGHT, {}, 0.0, 0.0, t}; }
 };
 
 struct Sphere {
@@ -107,8 +138,18 @@ class HittableList {
     const std::vector<Plane>& planes() const { return planes_; }
     const std::vector<Quad>& quads() const { return quads_; }
     const std::vector<std::pair<Kind, size_t>>& order() const { return order_; }
+    // BoundedVolumeHierarchy::from(list) (bvh.rs:106-143): the same closest
+    // hit as the list; as a light list its pdf_value is (sum / n * n) / n
+    // (a leaf, n <= 5; deeper BVH light lists are outside this build)
+    HittableList into_bvh() const {
+        HittableList h = *this;
+        h.bvh_ = true;
+        return h;
+    }
+    bool is_bvh() const { return bvh_; }
 
    private:
+    bool bvh_ = false;
     std::vector<Sphere> spheres_;
     std::vector<Plane> planes_;
     std::vector<Quad> quads_;
@@ -120,6 +161,10 @@ class HittableList {
 struct FlatScene {
     std::vector<double> spheres, planes, quads, mat_params, lights, light_quads, boxes;
     std::vector<uint32_t> sphere_mat, plane_mat, quad_mat, mat_type, light_kinds, box_mat;
+    std::vector<uint32_t> mat_tex, tex_type, tex_refs, perlin_perm;
+    std::vector<double> tex_params, perlin_vec;
+    uint32_t n_light_other = 0, light_flags = 0;
+    bool textured = false;
     rtw_scene view() const;
 };
 // world's spheres/planes/quads with one material record each; lights
@@ -193,6 +238,13 @@ namespace scenes {
 std::tuple<HittableList, HittableList, CameraBuilder> simple(uint64_t seed, int n = 11);
 // scenes::cornell_box (scenes/src/lib.rs:292-395)
 std::tuple<HittableList, HittableList, CameraBuilder> cornell_box();
+// the other generators (scenes/src/lib.rs); `seed` drives the Perlin tables
+std::tuple<HittableList, HittableList, CameraBuilder> perlin_spheres(uint64_t seed);     // :40-89
+std::tuple<HittableList, HittableList, CameraBuilder> plane();                           // :91-121
+std::tuple<HittableList, HittableList, CameraBuilder> checkered_spheres();               // :123-153
+std::tuple<HittableList, HittableList, CameraBuilder> simple_light(uint64_t seed);       // :235-290
+std::tuple<HittableList, HittableList, CameraBuilder> debugging_scene(uint64_t seed);    // :397-530
+std::tuple<HittableList, HittableList, CameraBuilder> simple_transform(uint64_t seed);   // :532-653
 }  // namespace scenes
 
 // host RNG used by the scene generator (the same xoshiro256++/splitmix64 and
@@ -203,6 +255,8 @@ class HostRng {
     uint64_t next();
     double standard();                               // Standard f64
     double uniform_incl(double low, double high);    // Uniform::new_inclusive(low, high).sample
+    uint64_t uniform_u64(uint64_t low, uint64_t high);   // Uniform::new(low, high).sample (usize)
+    Vec3 unit_sphere();                              // utils.rs:99-122 (shuffle not drawn)
 
    private:
     uint64_t s_[4];

@@ -34,14 +34,50 @@ namespace dev {
 template <typename R>
 __device__ __forceinline__ V3<R> v3of(const R* a) { return mk(a[0], a[1], a[2]); }
 
-// One plane, plane.rs:61-76 (one-sided: only rays moving along +n hit it).
+// Plane::get_plane_uv, plane.rs:40-54, on the host-computed per-plane
+// constants of the record (rtw_kernels.h kPlaneR): the oracle's plane_uv.
 template <typename R>
-__device__ __forceinline__ bool plane_t(const R* pl, V3<R> o, V3<R> d, R tmin, R& t) {
+__device__ __forceinline__ void plane_uv(const R* pl, V3<R> pnt, R& u, R& v) {
+    const R mode = pl[12];
+    if (mode == (R)0) {
+        u = pnt.x;
+        v = pnt.z;
+        return;
+    }
+    if (mode == (R)2) {
+        u = v = (R)NAN;
+        return;
+    }
+    const V3<R> k = q3(pl, 15);
+    const V3<R> vec = pnt - q3(pl, 0);
+    const R ct = pl[13], st = pl[14];
+    const V3<R> rot = ((vec * ct) + cross(k, vec) * st) + (k * dot(k, vec)) * ((R)1 - ct);
+    u = rot.x - trunc_(rot.x);
+    v = rot.z - trunc_(rot.z);
+}
+
+// One plane, plane.rs:61-76 (one-sided: only rays moving along +n hit it).
+// Plane::hit computes the UV before its range test and panics on a
+// non-finite one (plane.rs:66-69): counted in *panic (a rare event: one
+// atomic at the site, no register kept live).  The UV is not formed
+// here: it is NaN for every point of a mode-2 plane, (x, z) for mode 0, and a
+// rotation of the finite constants for mode 1 -- non-finite exactly when the
+// point is (up to overflow inside the rotation itself, |p| ~ 1e308).
+template <typename R>
+__device__ __forceinline__ bool plane_t(const R* pl, V3<R> o, V3<R> d, R tmin, R& t,
+                                        unsigned long long* panic) {
     V3<R> n = mk(pl[3], pl[4], pl[5]);
     R denom = dot(d, n);
     if (!(denom > P<R>::kEps)) return false;
     V3<R> op = o - mk(pl[0], pl[1], pl[2]);
     R tt = -P<R>::div_(dot(op, n), denom);
+    {
+        const V3<R> q = o + d * tt;
+        const R mode = pl[12];
+        const bool fin = mode == (R)0 ? __builtin_isfinite(q.x) && __builtin_isfinite(q.z)
+                                      : mode == (R)1 && __builtin_isfinite(q.x + q.y + q.z);
+        if (!fin && panic) atomicAdd(panic, 1ull);
+    }
     if (!(tmin <= tt && tt <= (R)INFINITY)) return false;
     t = tt;
     return true;
@@ -705,14 +741,81 @@ __device__ __forceinline__ R lights_pdf_mixed(const DevScene<R>& sc, const R4<R>
     R acc = (R)0;
     for (uint32_t k = 0; k < sc.n_list; ++k) {
         const uint32_t ref = sc.lref[k];
-        if (ref >> 31) {
-            acc = acc + quad_pdf_value(sc.lquads + kQuadR * (ref & 0x7fffffffu), o, d);
+        if (ref & kLrefQuad) {
+            acc = acc + quad_pdf_value(sc.lquads + kQuadR * (ref & 0x3fffffffu), o, d);
+        } else if (ref & kLrefDefault) {
+            acc = acc + (R)0;                      // Hittable::pdf_value default, hittable.rs:175-177
         } else {
             const R4<R> L = li[ref];
             acc = acc + sphere_pdf_value(mk(L.x, L.y, L.z), L.w, o, d);
         }
     }
     return acc;
+}
+
+// ---------------------------------------------------------------------------
+// Textures (kOptTex kernels): Texture::get_colour, texture.rs:15-102
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ double fmod_(double a, double b) { return ::fmod(a, b); }
+__device__ __forceinline__ float fmod_(float a, float b) { return ::fmodf(a, b); }
+
+// Perlin::noise (perlin.rs:59-82) + perlin_interpolation (:96-108): the
+// oracle's rtwo_perlin_noise, term for term (iproduct order, Sum from -0.0)
+template <typename R>
+__device__ __forceinline__ R perlin_noise(const R4<R>* __restrict__ vec, const uint32_t* __restrict__ perm,
+                                          V3<R> p) {
+    const R u = p.x - floor_(p.x), v = p.y - floor_(p.y), w = p.z - floor_(p.z);
+    const R i = floor_(p.x), j = floor_(p.y), k = floor_(p.z);
+    R acc = (R)-0.0;
+#pragma unroll
+    for (int di = 0; di < 2; ++di) {
+        const uint32_t px = perm[perlin_index(i + (R)di)];
+#pragma unroll
+        for (int dj = 0; dj < 2; ++dj) {
+            const uint32_t py = perm[256 + perlin_index(j + (R)dj)];
+#pragma unroll
+            for (int dk = 0; dk < 2; ++dk) {
+                const R4<R> c = vec[px ^ py ^ perm[512 + perlin_index(k + (R)dk)]];
+                const R fi = (R)di, fj = (R)dj, fk = (R)dk;
+                const V3<R> wv = mk(u - fi, v - fj, w - fk);
+                const R term = (fi * u + ((R)1 - fi) * ((R)1 - u)) * (fj * v + ((R)1 - fj) * ((R)1 - v)) *
+                               (fk * w + ((R)1 - fk) * ((R)1 - w)) * dot(mk(c.x, c.y, c.z), wv);
+                acc = acc + term;
+            }
+        }
+    }
+    return acc;
+}
+
+// CheckerTexture (nested textures followed iteratively), NoiseTexture
+// (0.5 (1 + sin(scale z + 10 turb(p, 7)))), SolidColour
+template <typename R>
+__device__ V3<R> tex_colour(const DevScene<R>& sc, uint32_t tid, R u, R v, V3<R> p) {
+    for (int depth = 0; depth < 64; ++depth) {
+        const uint32_t kind = sc.tex_type[tid];
+        const R4<R> tp = sc.tex_p[tid];
+        if (kind == 1u) {
+            const R s = floor_(u * tp.w) + floor_(v * tp.w);
+            tid = fmod_(s, (R)2) == (R)0 ? sc.tex_refs[2 * tid] : sc.tex_refs[2 * tid + 1];
+            continue;
+        }
+        if (kind == 2u) {
+            const uint32_t q = sc.tex_refs[2 * tid];
+            const R4<R>* vec = sc.perlin_vec + 256 * q;
+            const uint32_t* perm = sc.perlin_perm + 768 * q;
+            R accum = (R)0, weight = (R)1;        // Perlin::turb, perlin.rs:84-94
+            V3<R> t = p;
+            for (int o = 0; o < 7; ++o) {
+                accum = accum + weight * perlin_noise(vec, perm, t);
+                t = t * (R)2;
+                weight = weight * (R)0.5;
+            }
+            const R x = rt_sin(tp.w * p.z + accum * (R)10) + (R)1;
+            return mk((R)0.5 * x, (R)0.5 * x, (R)0.5 * x);
+        }
+        return mk(tp.x, tp.y, tp.z);
+    }
+    return mk((R)NAN, (R)NAN, (R)NAN);
 }
 
 // RTW_EXP (profiling builds only, tools/exp_cost.sh): repeat one part of the
@@ -726,7 +829,8 @@ __device__ __forceinline__ R lights_pdf_mixed(const DevScene<R>& sc, const R4<R>
 // kOpt: compile-time options, chosen per launch by the host
 //   kOptRobust   (f32) closest-approach sphere and light tests (far geometry)
 //   kOptLightBvh (BVH kernels) light pdf through the light BVH (long light lists)
-enum : int { kOptRobust = 1, kOptLightBvh = 2 };
+//   kOptTex      textured materials (DevScene::mat_tex): hit UVs + Texture::get_colour
+enum : int { kOptRobust = 1, kOptLightBvh = 2, kOptTex = 4 };
 
 template <typename R, int kWorld, int kOpt>
 // f32: ask for 5 waves per SIMD (<= 96 VGPRs; the kernel fits without
@@ -735,6 +839,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? 5 : 1) render_kernel(
     using PR = P<R>;
     constexpr bool kRobust = (kOpt & kOptRobust) != 0;
     constexpr bool kLightBvh = (kOpt & kOptLightBvh) != 0 && kWorld >= kWorldBvh;
+    constexpr bool kTex = (kOpt & kOptTex) != 0;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     R4<R>* s_sph = reinterpret_cast<R4<R>*>(smem);
     R4<R>* s_li = s_sph + p.sc.n_sph;
@@ -885,16 +990,16 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? 5 : 1) render_kernel(
 #if RTW_EXP == 5
             for (int32_t k = 0; k < nplanes; ++k) {
                 R t;
-                const R* pl = p.sc.planes + 12 * k;
+                const R* pl = p.sc.planes + kPlaneR * k;
                 if (aabb_hit_ref(pl + 6, pl + 9, o, mk(d.y, d.x, d.z), tmin) &&
-                    plane_t(pl, o, mk(d.y, d.x, d.z), tmin, t) && t == (R)-7)
+                    plane_t(pl, o, mk(d.y, d.x, d.z), tmin, t, nullptr) && t == (R)-7)
                     ++segs;
             }
 #endif
             for (int32_t k = 0; k < nplanes; ++k) {
                 R t;
-                const R* pl = p.sc.planes + 12 * k;
-                if (aabb_hit_ref(pl + 6, pl + 9, o, d, tmin) && plane_t(pl, o, d, tmin, t) &&
+                const R* pl = p.sc.planes + kPlaneR * k;
+                if (aabb_hit_ref(pl + 6, pl + 9, o, d, tmin) && plane_t(pl, o, d, tmin, t, p.counters + 4) &&
                     (best < 0 || t < tb)) {
                     tb = t;
                     best = k;
@@ -954,6 +1059,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? 5 : 1) render_kernel(
                 int32_t next_self = -1;
                 bool box_hit = false;
                 bool box_front = false;
+                R hu = (R)0, hv = (R)0;                            // HitRecord u, v (kTex)
                 if (best >= bbase && best < sbase) {
                     // Transformed<Cuboid>: the record of the object-space hit,
                     // its point mapped back (transform_point3d); the normal and
@@ -966,17 +1072,30 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? 5 : 1) render_kernel(
                     const V3<R> n = q3(B + kQuadR * qd, 12);
                     box_front = dot(d2, n) < (R)0;
                     outward = n;
-                    pnt = mat3_mul(B + kBoxRot, o2 + d2 * t2) + q3(B, kBoxT);
+                    const V3<R> po = o2 + d2 * t2;
+                    pnt = mat3_mul(B + kBoxRot, po) + q3(B, kBoxT);
                     m = p.sc.box_mat[best - bbase];
                     box_hit = true;
+                    if constexpr (kTex) {                          // get_quad_uv, object space
+                        const R* Q = B + kQuadR * qd;
+                        const V3<R> pq = po - q3(Q, 0);
+                        hu = dot(cross(pq, q3(Q, 6)), q3(Q, 9));
+                        hv = dot(cross(q3(Q, 3), pq), q3(Q, 9));
+                    }
                 } else if (best < nplanes) {
-                    const R* pl = p.sc.planes + 12 * best;
+                    const R* pl = p.sc.planes + kPlaneR * best;
                     outward = mk(pl[3], pl[4], pl[5]);
                     m = p.sc.plane_mat[best];
+                    if constexpr (kTex) plane_uv(pl, pnt, hu, hv);
                 } else if (best < bbase) {
                     const R* Q = p.sc.quads + kQuadR * (best - nplanes);
                     outward = q3(Q, 12);                           // quadrilateral.rs:97
                     m = p.sc.quad_mat[best - nplanes];
+                    if constexpr (kTex) {                          // get_quad_uv, quadrilateral.rs:58-63
+                        const V3<R> pq = pnt - q3(Q, 0);
+                        hu = dot(cross(pq, q3(Q, 6)), q3(Q, 9));
+                        hv = dot(cross(q3(Q, 3), pq), q3(Q, 9));
+                    }
                 } else {
                     const uint32_t k = (uint32_t)(best - sbase);
                     const R4<R> sk = p.sc.sph[k];
@@ -984,6 +1103,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? 5 : 1) render_kernel(
                     const uint32_t mw = p.sc.sph_mat[k];
                     m = mw & 0x7fffffffu;
                     next_self = (mw >> 31) ? (int32_t)k : -1;   // bit 31: isolated sphere
+                    if constexpr (kTex) sphere_uv(outward, hu, hv);
                 }
                 const bool front = box_hit ? box_front : dot(d, outward) < (R)0;
                 const V3<R> nrm = front ? outward : -outward;
@@ -991,7 +1111,13 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? 5 : 1) render_kernel(
                 const R4<R> mp = p.sc.mat_p[m];
                 // Material::emitted: DiffuseLight's colour (material.rs:508-514),
                 // black for every other material (material.rs:42-44)
-                const V3<R> emitted = mtype == kMatDiffuseLight ? mk(mp.x, mp.y, mp.z) : zero;
+                // the material's colour: its texture at (u, v, p) (kTex) or its SolidColour
+                V3<R> colour = mk(mp.x, mp.y, mp.z);
+                if constexpr (kTex) {
+                    if (mtype == kMatDiffuseLight || mtype == kMatLambertian)
+                        colour = tex_colour(p.sc, p.sc.mat_tex[m], hu, hv, pnt);
+                }
+                const V3<R> emitted = mtype == kMatDiffuseLight ? colour : zero;
                 if (mtype == kMatMetal) {
                     // Metal::scatter, material.rs:407-421
                     V3<R> refl = reflect(PR::normalize(d), nrm);
@@ -1025,16 +1151,24 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? 5 : 1) render_kernel(
                     // Lambertian + MixturePdf(HittablePdf(lights), CosinePdf):
                     // material.rs:357-376, pdf.rs:33-101, camera.rs:504-521
                     ++lambs;
-                    const V3<R> att = mk(mp.x, mp.y, mp.z);
+                    const V3<R> att = colour;
                     const Onb<R> uvw(nrm);
                     V3<R> dir;
                     if (PR::u_std(g.next()) < (R)0.5) {
                         // HittableList::random (hittable_list.rs:414-419): a
                         // uniform light (one gen_index draw), then its random()
-                        if (p.sc.lref) {
+                        if (p.sc.n_list == 0) {
+                            // an empty list panics there (:417): counted; the
+                            // sample goes on along a NaN direction and ends NaN
+                            // at its next world query, as in the oracle
+                            atomicAdd(p.counters + 5, 1ull);
+                            dir = mk((R)NAN, (R)NAN, (R)NAN);
+                        } else if (p.sc.lref) {
                             const uint32_t ref = p.sc.lref[g.index(p.sc.n_list)];
-                            if (ref >> 31) {
-                                dir = quad_random(p.sc.lquads + kQuadR * (ref & 0x7fffffffu), pnt, g);
+                            if (ref & kLrefQuad) {
+                                dir = quad_random(p.sc.lquads + kQuadR * (ref & 0x3fffffffu), pnt, g);
+                            } else if (ref & kLrefDefault) {
+                                dir = mk<R>(1, 0, 0);              // Hittable::random default
                             } else {
                                 const R4<R> L = li[ref];
                                 dir = sphere_random(mk(L.x, L.y, L.z), L.w, pnt, g);
@@ -1072,7 +1206,9 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? 5 : 1) render_kernel(
 #if RTW_EXP == 2
                     segs += lights_pdf_sum<kRobust>(li, p.sc.n_lights, pnt, mk(dir.y, dir.z, dir.x)) == (R)-7 ? 1u : 0u;
 #endif
-                    const R lpdf = PR::div_(acc, (R)p.sc.n_list);
+                    // / len; a BVH leaf list multiplies by len and divides again (bvh.rs:67-76, 191-194)
+                    R lpdf = PR::div_(acc, (R)p.sc.n_list);
+                    if (p.sc.light_flags & 1u) lpdf = PR::div_(lpdf * (R)p.sc.n_list, (R)p.sc.n_list);
                     const R pdf = lpdf * (R)0.5 + PR::max_(cos_w, (R)0) * (R)0.5;
                     const R spdf = PR::max_(PR::over_pi(dot(nrm, ndir)), (R)0);
                     const V3<R> w = PR::divs(att * spdf, pdf);
@@ -1176,6 +1312,11 @@ inline void launch_world(const KParams<R>& p, int world, size_t lds_bytes, uint3
                          hipStream_t stream) {
     const size_t stacks = (size_t)kWavesPerBlock * p.stack * 64 * sizeof(int32_t);
     constexpr int kBrute = kOpt & ~dev::kOptLightBvh;   // the light BVH needs the BVH kernels' stack
+    // textured scenes are small: their kernels exist for the brute-force and
+    // binary while-while worlds only (launch_render_impl maps the others)
+    if constexpr ((kOpt & dev::kOptTex) != 0) {
+        if (world == kWorldBvh4 || world == kWorldBvh) world = kWorldBvhWW;
+    }
     switch (world) {
     case kWorldLds:
         allow_lds<R, kWorldLds, kBrute>(lds_bytes);
@@ -1188,16 +1329,18 @@ inline void launch_world(const KParams<R>& p, int world, size_t lds_bytes, uint3
                            stream, p);
         break;
     case kWorldBvh4:
-        hipLaunchKernelGGL((dev::render_kernel<R, kWorldBvh4, kOpt>), dim3(blocks), dim3(kBlock), stacks,
-                           stream, p);
+        if constexpr ((kOpt & dev::kOptTex) == 0)
+            hipLaunchKernelGGL((dev::render_kernel<R, kWorldBvh4, kOpt>), dim3(blocks), dim3(kBlock), stacks,
+                               stream, p);
         break;
     case kWorldBvhWW:
         hipLaunchKernelGGL((dev::render_kernel<R, kWorldBvhWW, kOpt>), dim3(blocks), dim3(kBlock), stacks,
                            stream, p);
         break;
     case kWorldBvh:
-        hipLaunchKernelGGL((dev::render_kernel<R, kWorldBvh, kOpt>), dim3(blocks), dim3(kBlock), stacks,
-                           stream, p);
+        if constexpr ((kOpt & dev::kOptTex) == 0)
+            hipLaunchKernelGGL((dev::render_kernel<R, kWorldBvh, kOpt>), dim3(blocks), dim3(kBlock), stacks,
+                               stream, p);
         break;
     default:
         hipLaunchKernelGGL((dev::render_kernel<R, kWorldGlobal, kBrute>), dim3(blocks), dim3(kBlock), 0, stream,
@@ -1215,7 +1358,18 @@ inline int launch_render_impl(const KParams<R>& p, int world, size_t lds_bytes, 
     if (blocks) {
         const bool robust = sizeof(R) == 4 && p.sc.robust;
         const bool lbvh = p.light_bvh != 0;
-        if constexpr (sizeof(R) == 4) {
+        constexpr int T = dev::kOptTex;
+        if (p.sc.mat_tex) {
+            if constexpr (sizeof(R) == 4) {
+                if (robust && lbvh) launch_world<R, T | dev::kOptRobust | dev::kOptLightBvh>(p, world, lds_bytes, blocks, stream);
+                else if (robust) launch_world<R, T | dev::kOptRobust>(p, world, lds_bytes, blocks, stream);
+                else if (lbvh) launch_world<R, T | dev::kOptLightBvh>(p, world, lds_bytes, blocks, stream);
+                else launch_world<R, T>(p, world, lds_bytes, blocks, stream);
+            } else {
+                if (lbvh) launch_world<R, T | dev::kOptLightBvh>(p, world, lds_bytes, blocks, stream);
+                else launch_world<R, T>(p, world, lds_bytes, blocks, stream);
+            }
+        } else if constexpr (sizeof(R) == 4) {
             if (robust && lbvh) launch_world<R, dev::kOptRobust | dev::kOptLightBvh>(p, world, lds_bytes, blocks, stream);
             else if (robust) launch_world<R, dev::kOptRobust>(p, world, lds_bytes, blocks, stream);
             else if (lbvh) launch_world<R, dev::kOptLightBvh>(p, world, lds_bytes, blocks, stream);

@@ -403,5 +403,114 @@ __device__ __forceinline__ R reflectance(R cosine, R ref_idx) {
     return r0 + ((R)1 - r0) * p5;
 }
 
+// ---------------------------------------------------------------------------
+// Textures (texture.rs, perlin.rs)
+// ---------------------------------------------------------------------------
+// f64::sin of a general argument: fdlibm's medium Cody-Waite reduction by
+// pi/2 and __kernel_sin/__kernel_cos with the tail -- the oracle's rtwo_sin
+// operation for operation (|x| >= 2^19 pi/2 falls back to the library).
+__device__ __forceinline__ double k_sin_y(double x, double y) {
+    const double S1 = -1.66666666666666324348e-01, S2 = 8.33333333332248946124e-03,
+                 S3 = -1.98412698298579493134e-04, S4 = 2.75573137070700676789e-06,
+                 S5 = -2.50507602534068634195e-08, S6 = 1.58969099521155010221e-10;
+    double z = x * x;
+    double v = z * x;
+    double r = S2 + z * (S3 + z * (S4 + z * (S5 + z * S6)));
+    return x - ((z * (0.5 * y - v * r) - y) - v * S1);
+}
+__device__ __forceinline__ double k_cos_y(double x, double y) {
+    const double C1 = 4.16666666666666019037e-02, C2 = -1.38888888888741095749e-03,
+                 C3 = 2.48015872894767294178e-05, C4 = -2.75573143513906633035e-07,
+                 C5 = 2.08757232129817482790e-09, C6 = -1.13596475577881948265e-11;
+    double z = x * x;
+    double r = z * (C1 + z * (C2 + z * (C3 + z * (C4 + z * (C5 + z * C6)))));
+    double ax = __builtin_fabs(x);
+    if (ax < 0.3) return 1.0 - (0.5 * z - (z * r - x * y));
+    double qx;
+    if (ax > 0.78125) {
+        qx = 0.28125;
+    } else {
+        unsigned long long b = (unsigned long long)__double_as_longlong(ax);
+        b = (b - 0x0020000000000000ULL) & 0xFFFFFFFF00000000ULL;
+        qx = __longlong_as_double((long long)b);
+    }
+    double hz = 0.5 * z - qx;
+    double a = 1.0 - qx;
+    return a - (hz - (z * r - x * y));
+}
+__device__ __forceinline__ int exp_bits(double x) {
+    return (int)(((unsigned long long)__double_as_longlong(x) >> 52) & 0x7ff);
+}
+__device__ inline double rt_sin(double x) {
+    const double ax = __builtin_fabs(x);
+    if (ax <= 0.78539816339744828) return k_sin_y(x, 0.0);
+    if (!(ax < 823549.6)) return ::sin(x);
+    const double invpio2 = 6.36619772367581382433e-01, pio2_1 = 1.57079632673412561417e+00,
+                 pio2_1t = 6.07710050650619224932e-11, pio2_2 = 6.07710050630396597660e-11,
+                 pio2_2t = 2.02226624879595063154e-21, pio2_3 = 2.02226624871116645580e-21,
+                 pio2_3t = 8.47842766036889956997e-32;
+    const int n = (int)(ax * invpio2 + 0.5);
+    const double fn = (double)n;
+    double r = ax - fn * pio2_1;
+    double w = fn * pio2_1t;
+    double y0 = r - w;
+    const int j = exp_bits(ax);
+    if (j - exp_bits(y0) > 16) {
+        double t = r;
+        w = fn * pio2_2;
+        r = t - w;
+        w = fn * pio2_2t - ((t - r) - w);
+        y0 = r - w;
+        if (j - exp_bits(y0) > 49) {
+            t = r;
+            w = fn * pio2_3;
+            r = t - w;
+            w = fn * pio2_3t - ((t - r) - w);
+            y0 = r - w;
+        }
+    }
+    double y1 = (r - y0) - w;
+    int q = n;
+    if (x < 0.0) {
+        y0 = -y0;
+        y1 = -y1;
+        q = -n;
+    }
+    switch (q & 3) {
+        case 0: return k_sin_y(y0, y1);
+        case 1: return k_cos_y(y0, y1);
+        case 2: return -k_sin_y(y0, y1);
+        default: return -k_cos_y(y0, y1);
+    }
+}
+__device__ __forceinline__ float rt_sin(float x) { return ::sinf(x); }
+
+__device__ __forceinline__ double floor_(double x) { return __builtin_floor(x); }
+__device__ __forceinline__ float floor_(float x) { return __builtin_floorf(x); }
+__device__ __forceinline__ double trunc_(double x) { return __builtin_trunc(x); }
+__device__ __forceinline__ float trunc_(float x) { return __builtin_truncf(x); }
+
+// f64::rem_euclid(256.) then `as usize` of an integral value (a floor plus 0
+// or 1): x mod 256 in two's complement; non-finite -> NaN -> 0; values too
+// large for the integer type are multiples of 256 -> 0.
+__device__ __forceinline__ uint32_t perlin_index(double x) {
+    return __builtin_fabs(x) < 9.2e18 ? (uint32_t)((long long)x & 255) : 0u;
+}
+__device__ __forceinline__ uint32_t perlin_index(float x) {
+    return __builtin_fabsf(x) < 2147483648.f ? (uint32_t)((int)x & 255) : 0u;   // beyond: multiples of 256
+}
+
+// Sphere::get_sphere_uv, sphere.rs:49-54 (the library atan2 / acos: the f64
+// results may differ from libm's in the last ulp, which moves a checker edge
+// only for points within an ulp of it)
+__device__ __forceinline__ void sphere_uv(V3<double> n, double& u, double& v) {
+    u = ::atan2(-n.z, n.x) / P<double>::kTau;
+    v = ::acos(n.y) / P<double>::kPi;
+}
+__device__ __forceinline__ void sphere_uv(V3<float> n, float& u, float& v) {
+    u = ::atan2f(-n.z, n.x) * 0.159154943091895335769f;
+    v = ::acosf(n.y) * P<float>::kInvPi;
+}
+
 }  // namespace dev
 }  // namespace rtw

@@ -35,7 +35,7 @@ struct alignas(4 * sizeof(R)) R4 {
 //   sph      : n_sph   x R4 {cx, cy, cz, r*r}   -- staged into LDS by the brute kernel
 //   sph_r    : n_sph   x R  radius              -- read once per hit (normal)
 //   sph_mat  : n_sph   x u32 material id
-//   planes   : n_pl    x 12 R {px, py, pz, nx, ny, nz, aabb lo xyz, aabb hi xyz}
+//   planes   : n_pl    x kPlaneR R {p, n, aabb lo, aabb hi, uv mode, cos, sin, k} (layout below)
 //   plane_mat: n_pl    x u32
 //   mat_type : n_mat   x u32
 //   mat_p    : n_mat   x R4 {albedo r, g, b, fuzz | ior}
@@ -91,16 +91,35 @@ struct DevScene {
     const R* quads;                   // n_quads x kQuadR (see quad layout below)
     const uint32_t* quad_mat;
     const R* lquads;                  // the light list's quads, n_lquads x kQuadR
-    const uint32_t* lref;             // light list in order: bit 31 = quad, low bits = index
-                                      // (null when the list is spheres only)
+    const uint32_t* lref;             // light list in order (kLref* bits | index; null when the
+                                      // list is spheres only)
     const R* boxes;                   // n_boxes x kBoxR (transformed cuboids, layout below)
     const uint32_t* box_mat;
+    // textures (null mat_tex: every material is its SolidColour albedo, mat_p)
+    const uint32_t* mat_tex;          // n_mat texture ids
+    const uint32_t* tex_type;         // RTW_TEX_*
+    const R4<R>* tex_p;               // {r, g, b, inv_scale | scale}
+    const uint32_t* tex_refs;         // 2 per texture: checker even/odd, noise Perlin table
+    const R4<R>* perlin_vec;          // 256 per table: rand_vec {x, y, z, 0}
+    const uint32_t* perlin_perm;      // 768 per table: perm_x, perm_y, perm_z
     uint32_t n_sph, n_planes, n_mat, n_lights, n_nodes, bvh_depth;
     uint32_t n_nodes4, bvh4_stack, n_lnodes, lbvh_depth;
     uint32_t robust;                  // f32: closest-approach sphere / light tests (far geometry)
     uint32_t n_quads, n_lquads, n_list;   // world quads, light quads, light-list length
     uint32_t n_boxes;
+    uint32_t light_flags;             // RTW_LIGHTS_BVH_LEAF
 };
+
+// Plane record, kPlaneR values of precision R: point [0..2], unit normal
+// [3..5], the reference's AABB lo [6..8] hi [9..11] (plane.rs:79-102), and
+// Plane::get_plane_uv's per-plane constants (plane.rs:40-54): [12] mode (0:
+// theta <= EPSILON, uv = (x, z); 1: Rodrigues rotation; 2: k is not finite,
+// so every uv is NaN and Plane::hit panics), [13] cos(theta), [14]
+// sin(theta), [15..17] k = normalize(n x (0, 1, 0)).
+constexpr uint32_t kPlaneR = 20;
+// light-list entry encoding (DevScene::lref): bit 31 quad, bit 30 an entry
+// with the Hittable defaults (pdf 0, random (1, 0, 0)), else a sphere
+constexpr uint32_t kLrefQuad = 0x80000000u, kLrefDefault = 0x40000000u;
 
 // Quad record (Quad::new's derived fields, quadrilateral.rs:37-56), kQuadR
 // values of precision R: Q[0..2], u[3..5], v[6..8], w = n/|n|^2 [9..11],
@@ -121,7 +140,8 @@ template <typename R>
 struct KParams {
     DevScene<R> sc;
     R* partial;                       // [n_chunks][n_local_tiles][64][3] item (chunk) sums
-    unsigned long long* counters;     // [0] segments, [1] lambertian
+    unsigned long long* counters;     // [0] segments, [1] lambertian, [2] node visits,
+                                      // [3] sphere tests, [4] plane-UV panics, [5] empty-light panics
     R center[3], p00[3], du[3], dv[3], disk_u[3], disk_v[3], bg[3];
     R u_scale;                        // Uniform::new_inclusive(-0.5, 0.5) scale
     uint64_t seed;

@@ -116,21 +116,46 @@ def test_empty_world_is_background():
 
 
 def test_lambertian_without_lights_is_an_error():
-    """hittable_list.rs:417 panics ('HittableList shouldn't be empty'); the C-ABI returns an error."""
+    """hittable_list.rs:417 panics ('HittableList shouldn't be empty') when a
+    Lambertian bounce draws from the empty light list; the render returns
+    RTW_E_NO_LIGHTS with the same panic count as the oracle.  A scene whose
+    Lambertian surfaces are never hit renders normally."""
     soa = rtw.flatten(rtw.HittableList([rtw.Sphere((0, 0, -1), 0.5, rtw.Lambertian((0.5, 0.5, 0.5)))]),
                       rtw.HittableList())
-    with rtw.Renderer(precision=rtw.RTW_F64) as r:
-        with pytest.raises(rtw.RenderError) as e:
+    cam = rtw.CameraBuilder().with_image_width(8).with_image_height(8).with_samples_per_pixel(4).build()
+    ref, st = _render_oracle_allow_panic(soa, cam, 5, 1)
+    assert st.panic_no_lights > 0
+    for prec in (rtw.RTW_F64, rtw.RTW_F32):
+        with rtw.Renderer(precision=prec) as r:
             r.set_scene(soa)
-        assert e.value.code == -3
+            with pytest.raises(rtw.RenderError) as e:
+                r.render(cam, 5)
+            assert e.value.code == -3
+            if prec == rtw.RTW_F64:
+                assert r.stats.panic_no_lights == st.panic_no_lights and r.stats.panic_plane_uv == 0
+    away = rtw.CameraBuilder().with_image_width(8).with_image_height(8).with_samples_per_pixel(4) \
+        .with_lookat((0, 0, 1)).with_background((0.5, 0.5, 0.5)).build()
+    with rtw.Renderer(precision=rtw.RTW_F64) as r:
+        r.set_scene(soa)
+        np.testing.assert_array_equal(r.render(away, 5), np.full((8, 8, 3), 2.0))
+
+
+def _render_oracle_allow_panic(soa, cam, seed, chunk, accel=None):
+    ocam = O.Camera()
+    for name, _ in O.Camera._fields_:
+        setattr(ocam, name, getattr(cam.raw, name))
+    return O.render(ocam, O.Scene(**soa.__dict__), seed, chunk=chunk,
+                    accel=O.ACCEL_BRUTE if accel is None else accel, allow_panic=True)
 
 
 def test_mixed_materials_custom_scene():
     """A hand-built scene with every in-scope material, a light that a
-    Lambertian sphere sits inside (NaN path, sphere.rs:105,121), an upward-
-    facing plane seen from below, and defocus blur on."""
+    Lambertian sphere sits inside (NaN path, sphere.rs:105,121), a tilted
+    one-sided plane, and defocus blur on."""
     world = rtw.HittableList()
-    world.add(rtw.Plane((0, -0.5, 0), (0, -1, 0), rtw.Lambertian((0.8, 0.8, 0.0))))
+    # a tilted plane facing down, hit by rays moving down (plane.rs:61-76); its
+    # UV takes the rotation branch of get_plane_uv (plane.rs:47-53)
+    world.add(rtw.Plane((0, -0.5, 0), (0.1, -1, 0.05), rtw.Lambertian((0.8, 0.8, 0.0))))
     world.add(rtw.Sphere((0, 0, -1.2), 0.5, rtw.Lambertian((0.1, 0.2, 0.5))))
     world.add(rtw.Sphere((-1, 0, -1), 0.5, rtw.Dialectric(1.5)))
     world.add(rtw.Sphere((-1, 0, -1), 0.4, rtw.Dialectric(1 / 1.5)))
@@ -505,3 +530,127 @@ def test_cornell_box_f32_tracks_f64():
     ref, _ = _render_oracle(soa, cam, 73, 0, O.ACCEL_BRUTE)
     ok = ~(np.isnan(bvh).any(-1) | np.isnan(ref).any(-1))
     assert abs(bvh[ok].mean() - ref[ok].mean()) < 0.03 * ref[ok].mean()
+
+
+# ---- textures, UVs and the remaining reference scenes
+
+def _named(name, w, h, spp, depth, **over):
+    soa, b = rtw.scenes.named_soa(name)
+    b = b.with_image_width(w).with_image_height(h).with_samples_per_pixel(spp).with_max_depth(depth)
+    for k, v in over.items():
+        getattr(b, "with_" + k)(v)
+    return soa, b.build()
+
+
+@pytest.mark.parametrize("name", ["checkered_spheres", "simple_light", "debug", "simple_transform", "plane"])
+@pytest.mark.parametrize("accel", [rtw.RTW_ACCEL_BRUTE, rtw.RTW_ACCEL_BVH])
+def test_reference_scene_f64_matches_oracle(name, accel):
+    """Every scenes/src/lib.rs generator with textures (checker on spheres,
+    Perlin noise on planes and spheres), DiffuseLight spheres / quads /
+    cuboids, BVH light lists and Hittable-default lights: the f64 kernel is
+    bit-identical to the oracle (brute-force world, list tie order)."""
+    soa, cam = _named(name, 32, 24, 4, 12, vfov=40.0)
+    gpu, chunk, (segs, lambs) = _render_gpu(soa, cam, 83, rtw.RTW_F64, accel=accel)
+    ref, st = _render_oracle(soa, cam, 83, chunk, O.ACCEL_BRUTE)
+    mae, exact = _compare_f64(gpu, ref, 4)
+    assert mae < F64_MAE_TOL and exact > 0.999, (name, mae, exact)
+    assert segs == st.segments and lambs == st.lambertian
+
+
+# integration-tests/src/lib.rs:7-112, each camera as the test builds it
+INTEGRATION = {
+    "plane_test": ("plane", dict(image_width=3, image_height=2, samples_per_pixel=10, max_depth=3,
+                                 lookfrom=(-13, 2, 3), lookat=(0, 0, 0), vup=(0, 1, 0), focus_dist=10.0), True),
+    "small_light_test": ("simple_light", dict(image_width=3, image_height=2, samples_per_pixel=10, max_depth=5,
+                                              lookfrom=(4, 2, 10), lookat=(4, 2, -2), vup=(0, 1, 0),
+                                              focus_dist=4.0), True),
+    "debugging_test": ("debug", dict(image_width=3, image_height=2, samples_per_pixel=50, max_depth=10,
+                                     vfov=40.0, lookat=(0, 0, 0), lookfrom=(0, 20, 0)), False),
+    "cornell_box_test": ("cornell_box", dict(image_width=3, image_height=2, samples_per_pixel=50,
+                                             max_depth=10, vfov=40.0), False),
+}
+
+
+@pytest.mark.parametrize("test", sorted(INTEGRATION))
+def test_integration_test_configs_f64_match_oracle(test):
+    """The reference's own smoke renders (integration-tests/src/lib.rs) --
+    which assert only 'does not panic' -- rendered through the C-ABI and
+    compared bit for bit with the oracle."""
+    name, kw, fresh = INTEGRATION[test]
+    soa, b = rtw.scenes.named_soa(name)
+    if fresh:
+        b = rtw.CameraBuilder()
+    for k, v in kw.items():
+        getattr(b, "with_" + k)(v)
+    cam = b.build()
+    gpu, chunk, (segs, lambs) = _render_gpu(soa, cam, 89, rtw.RTW_F64)
+    ref, st = _render_oracle(soa, cam, 89, chunk, O.ACCEL_BRUTE)
+    mae, exact = _compare_f64(gpu, ref, cam.raw.samples_per_pixel)
+    assert mae < F64_MAE_TOL and exact == 1.0 and segs == st.segments
+
+
+def test_perlin_spheres_panics_like_the_reference():
+    """perlin_spheres (scenes/src/lib.rs:40-89) has no lights: the reference
+    panics on the first Lambertian light draw; the C-ABI returns
+    RTW_E_NO_LIGHTS and counts the same draws as the oracle."""
+    soa, cam = _named("perlin_spheres", 16, 16, 2, 10)
+    ref, st = _render_oracle_allow_panic(soa, cam, 97, 1)
+    with rtw.Renderer(precision=rtw.RTW_F64) as r:
+        r.set_scene(soa)
+        with pytest.raises(rtw.RenderError) as e:
+            r.render(cam, 97)
+        assert e.value.code == -3 and r.stats.panic_no_lights == st.panic_no_lights > 0
+
+
+def test_down_facing_plane_panics_like_the_reference():
+    """Plane::hit computes the UV before its range test; for n = -y it is NaN
+    and the reference panics (plane.rs:66-69): RTW_E_PANIC, same count."""
+    world = rtw.HittableList([rtw.Plane((0, -1, 0), (0, -1, 0), rtw.Lambertian((0.5, 0.5, 0.5))),
+                              rtw.Sphere((0, 0, -2), 0.5, rtw.Metal((0.8, 0.8, 0.8), 0.0))])
+    soa = rtw.flatten(world, rtw.HittableList([rtw.Sphere((0, 5, 0), 1.0)]))
+    cam = rtw.CameraBuilder().with_image_width(8).with_image_height(8).with_samples_per_pixel(2) \
+        .with_lookfrom((0, 3, 0)).with_lookat((0, 0, 0.1)).build()
+    ref, st = _render_oracle_allow_panic(soa, cam, 3, 1)
+    assert st.panic_plane_uv > 0
+    with rtw.Renderer(precision=rtw.RTW_F64) as r:
+        r.set_scene(soa)
+        with pytest.raises(rtw.RenderError) as e:
+            r.render(cam, 3)
+        assert e.value.code == -6 and r.stats.panic_plane_uv == st.panic_plane_uv
+
+
+@pytest.mark.parametrize("name", ["checkered_spheres", "simple_light", "debug"])
+def test_reference_scene_f32_tracks_f64(name):
+    """f32 speed mode on the textured scenes: BVH == brute force bit for bit,
+    image mean within 3 % of the f64 oracle."""
+    soa, cam = _named(name, 48, 32, 16, 12, vfov=40.0)
+    brute, _, cb = _render_gpu(soa, cam, 101, rtw.RTW_F32, accel=rtw.RTW_ACCEL_BRUTE)
+    bvh, _, cv = _render_gpu(soa, cam, 101, rtw.RTW_F32, accel=rtw.RTW_ACCEL_BVH)
+    assert _same(brute, bvh) and cb == cv
+    ref, _ = _render_oracle(soa, cam, 101, 0, O.ACCEL_BRUTE)
+    ok = ~(np.isnan(bvh).any(-1) | np.isnan(ref).any(-1))
+    assert abs(bvh[ok].mean() - ref[ok].mean()) < 0.03 * ref[ok].mean(), (bvh[ok].mean(), ref[ok].mean())
+
+
+def test_python_textured_scene_on_the_gpu():
+    """The Python mirror's textures (CheckerTexture of a NoiseTexture, a
+    textured DiffuseLight) through flatten and the C-ABI, vs the oracle."""
+    noise = rtw.NoiseTexture.new(2.0, 7)
+    check = rtw.CheckerTexture.new(noise, rtw.SolidColour((0.9, 0.2, 0.1)), 0.5)
+    world = rtw.HittableList([
+        rtw.Sphere((0, 0, -2), 1.0, rtw.Lambertian(check)),
+        rtw.Quad((-3, -1, -5), (6, 0, 0), (0, 4, 0), rtw.Lambertian(rtw.CheckerTexture.new_with_colours(
+            (0.1, 0.1, 0.1), (0.8, 0.8, 0.8), 0.1))),
+        rtw.Sphere((1.5, 1.2, -1.5), 0.3, rtw.DiffuseLight(rtw.CheckerTexture.new_with_colours(
+            (4, 4, 4), (1, 0, 0), 0.05))),
+        rtw.Plane((0, -1, 0), (0, 1, 0.2), rtw.Lambertian(noise)),
+    ])
+    lights = rtw.HittableList([rtw.Sphere((1.5, 1.2, -1.5), 0.3)])
+    soa = rtw.flatten(world, lights)
+    cam = rtw.CameraBuilder().with_image_width(32).with_image_height(24).with_samples_per_pixel(4) \
+        .with_max_depth(12).with_lookfrom((0, 0.5, 2)).with_lookat((0, 0, -2)).with_vfov(60) \
+        .with_background((0.2, 0.3, 0.4)).build()
+    gpu, chunk, _ = _render_gpu(soa, cam, 103, rtw.RTW_F64)
+    ref, _ = _render_oracle(soa, cam, 103, chunk, O.ACCEL_BRUTE)
+    mae, exact = _compare_f64(gpu, ref, 4)
+    assert mae < F64_MAE_TOL and exact > 0.999

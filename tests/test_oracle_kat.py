@@ -265,12 +265,27 @@ def test_empty_world_returns_background_sums():
     assert st.segments == 5 * 4 * 7
 
 
-def test_lambertian_without_lights_rejected():
+def test_lambertian_without_lights_panics_when_the_light_branch_is_drawn():
+    """HittableList::random on an empty list panics (hittable_list.rs:414-419)
+    -- only when MixturePdf::generate picks the light half (pdf.rs:94-100);
+    a scene whose Lambertian surfaces are never hit renders fine (the
+    reference's `plane` scene)."""
     sc = O.Scene(np.array([[0, 0, -1, 0.5]]), np.array([0], np.uint32), np.zeros((0, 6)),
                  np.zeros(0, np.uint32), np.array([0], np.uint32), np.array([[0.5, 0.5, 0.5, 0, 0]]),
                  np.zeros((0, 4)))
-    with pytest.raises(ValueError):
-        O.render(O.camera_build(image_width=2, image_height=2), sc, 1)
+    with pytest.raises(O.ReferencePanic) as e:
+        O.render(O.camera_build(image_width=4, image_height=4, samples_per_pixel=8), sc, 1)
+    st = e.value.stats
+    assert 0 < st.panic_no_lights < st.lambertian and st.panic_plane_uv == 0
+    # the cosine half divides by the empty list's 0 / 0 pdf: NaN samples
+    img, st = O.render(O.camera_build(image_width=4, image_height=4, samples_per_pixel=8), sc, 1,
+                       allow_panic=True)
+    assert st.nan_samples >= st.panic_no_lights
+    # never hit: no panic, background only
+    cam = O.camera_build(image_width=3, image_height=2, samples_per_pixel=4, lookat=(0, 0, 1),
+                         background=(0.5, 0.25, 1.0))
+    img, st = O.render(cam, sc, 1)
+    assert st.lambertian == 0 and np.all(img == np.array([2.0, 1.0, 4.0]))
 
 
 def test_bvh_variants_equal_brute_force():
