@@ -5,14 +5,17 @@
 //
 //   rtw <scene> [--debug] [--seed N] [--f64] [--device N] [--config PATH] [--out PATH]
 //
-// The `simple` and `cornell_box` scenes are in this build's scope; the other
-// reference scenes need Quad/Cuboid/DiffuseLight/textures (§8f).
+// <scene> is one of clap's ValueEnum names of main.rs:29-38 (cornell-box,
+// debug, checkered-spheres, perlin-spheres, plane, simple, simple-light,
+// simple-transform; snake_case accepted too).  --seed drives simple's
+// generator and the Perlin tables (the reference uses thread_rng).
 #include <math.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
 #include <fstream>
+#include <functional>
 #include <map>
 #include <sstream>
 #include <string>
@@ -63,9 +66,23 @@ int main(int argc, char** argv) {
         else if (scene.empty()) scene = s;
         else { fprintf(stderr, "unexpected argument %s\n", s.c_str()); return 2; }
     }
-    if (scene != "simple" && scene != "cornell_box") {
-        fprintf(stderr, "scene '%s' is not in this build's scope (supported: simple, cornell_box)\n",
-                scene.c_str());
+    for (char& ch : scene)
+        if (ch == '-') ch = '_';
+    using Gen = std::function<std::tuple<rtw::HittableList, rtw::HittableList, rtw::CameraBuilder>()>;
+    const uint64_t seed = opt.seed;
+    const std::map<std::string, Gen> gens = {
+        {"cornell_box", [] { return rtw::scenes::cornell_box(); }},
+        {"debug", [seed] { return rtw::scenes::debugging_scene(seed); }},
+        {"checkered_spheres", [] { return rtw::scenes::checkered_spheres(); }},
+        {"perlin_spheres", [seed] { return rtw::scenes::perlin_spheres(seed); }},
+        {"plane", [] { return rtw::scenes::plane(); }},
+        {"simple", [seed] { return rtw::scenes::simple(seed); }},
+        {"simple_light", [seed] { return rtw::scenes::simple_light(seed); }},
+        {"simple_transform", [seed] { return rtw::scenes::simple_transform(seed); }},
+    };
+    if (!gens.count(scene)) {
+        fprintf(stderr, "unknown scene '%s' (cornell-box, debug, checkered-spheres, perlin-spheres, plane, "
+                        "simple, simple-light, simple-transform)\n", scene.c_str());
         return 2;
     }
     std::map<std::string, std::string> kv;
@@ -88,7 +105,7 @@ int main(int argc, char** argv) {
     const uint32_t spp = (uint32_t)atol(kv["samples_per_pixel"].c_str());
     const uint32_t depth = (uint32_t)atol(kv["max_depth"].c_str());
 
-    auto [world, lights, builder] = scene == "cornell_box" ? rtw::scenes::cornell_box() : rtw::scenes::simple(opt.seed);
+    auto [world, lights, builder] = gens.at(scene)();
     try {
         rtw::Camera cam = builder.with_vfov(40.0)
                               .with_aspect_ratio(aspect)
