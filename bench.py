@@ -103,9 +103,11 @@ def cpu_baseline(scene, target_s):
         rows = int(max(1, min(H, target_s * threads / (per_sample * W * SPP))))
         step = max(1, H // rows)
         t0 = time.perf_counter()
-        _, st = O.render(cam, sc, 99, accel=accel, threads=threads, rows=(0, H, step))
+        img, st = O.render(cam, sc, 99, accel=accel, threads=threads, rows=(0, H, step))
         dt = time.perf_counter() - t0
         res[name] = (st.samples / dt / 1e6, st.samples, step, dt)
+        if name == "bvh_ref":
+            ref_img = img
         if target_s < 5:
             break
     v, n, step, dt = res["bvh_ref"]
@@ -115,6 +117,38 @@ def cpu_baseline(scene, target_s):
                      f"per-visit node-AABB recomputation (bvh.rs:147-152), {threads} threads"}
     if "bvh_cached" in res:
         out["value_bvh_cached"] = round(res["bvh_cached"][0], 4)
+    out["parity"] = parity_on_sample(scene, (0, H, step), 99, ref_img)
+    return out
+
+
+def parity_on_sample(scene, oracle_rows, seed, ref_full):
+    """BASELINE.json's second metric, per-pixel MAE vs the reference CPU
+    renderer, on the same sampled rows of the headline workload: the GPU
+    renders the full 1200x800x500spp image in f64 (parity mode) and in f32
+    (the benchmarked mode) with the oracle's seed; the oracle's rows (already
+    rendered above) are the reference.  MAE of sum/spp over NaN-free pixels."""
+    rows = list(range(*oracle_rows))
+    ref = ref_full[rows]
+    builder = rtw.scenes.simple_soa(SCENE_SEED)[1]
+    gcam = builder.with_image_width(W).with_image_height(H).with_samples_per_pixel(SPP).with_max_depth(DEPTH).build()
+    out = {"rows": len(rows), "pixels": len(rows) * W, "spp": SPP, "seed": seed}
+    for name, prec in (("f64", rtw.RTW_F64), ("f32", rtw.RTW_F32)):
+        with rtw.Renderer(device=torch.cuda.current_device(), precision=prec) as r:
+            # one sample per work item (chunk 1), so the per-pixel fold is the
+            # reference's sample-by-sample fold: f64 can be compared bit for bit
+            r.set_tuning("partial_max", 16 << 30)
+            r.set_scene(scene)
+            t0 = time.perf_counter()
+            img = r.render(gcam, seed)[rows]
+            t = time.perf_counter() - t0
+            chunk = int(r.stats.chunk)
+        ok = ~(np.isnan(img).any(-1) | np.isnan(ref).any(-1))
+        out[name] = {"mae": float(np.abs(img[ok] - ref[ok]).mean() / SPP),
+                     "max_abs": float(np.abs(img[ok] - ref[ok]).max() / SPP),
+                     "bit_identical": float((img == ref).all(-1)[ok].mean()),
+                     "nan_mask_equal": bool(np.array_equal(np.isnan(img).any(-1), np.isnan(ref).any(-1))),
+                     "render_s": round(t, 3), "chunk": chunk}
+    out["tolerance"] = "f64: MAE < 1e-5 (north_star); f32: statistical (DESIGN.md §2)"
     return out
 
 

@@ -654,3 +654,43 @@ def test_python_textured_scene_on_the_gpu():
     ref, _ = _render_oracle(soa, cam, 103, chunk, O.ACCEL_BRUTE)
     mae, exact = _compare_f64(gpu, ref, 4)
     assert mae < F64_MAE_TOL and exact > 0.999
+
+
+# ---- BASELINE.json's headline size (C2: 1200 x 800, depth 50) at few spp:
+# every 40th row against the oracle, and the rank split reassembled
+
+def test_c2_full_frame_f64_rows_match_oracle():
+    soa, b = _scene()
+    cam = b.with_image_width(1200).with_image_height(800).with_samples_per_pixel(3).with_max_depth(50).build()
+    gpu, chunk, _ = _render_gpu(soa, cam, 107, rtw.RTW_F64)
+    ocam = O.Camera()
+    for name, _ in O.Camera._fields_:
+        setattr(ocam, name, getattr(cam.raw, name))
+    ref, st = O.render(ocam, O.Scene(**soa.__dict__), 107, chunk=chunk, accel=O.ACCEL_BVH_CACHED,
+                       rows=(3, 800, 40))
+    rows = list(range(3, 800, 40))
+    mae, exact = _compare_f64(gpu[rows], ref[rows], 3)
+    assert mae < F64_MAE_TOL and exact == 1.0, (mae, exact)
+
+
+@pytest.mark.parametrize("nranks", [2, 8])
+def test_c2_full_frame_rank_split_is_the_single_render(nranks):
+    """rtw_render_device over nranks (the multi-GPU row-tile split, DESIGN.md
+    §7) reassembles the one-rank C2-size image bit for bit (f32)."""
+    import torch
+    from ray_tracing_weekend_amd import sharding
+    soa, b = _scene()
+    H, W = 800, 1200
+    cam = b.with_image_width(W).with_image_height(H).with_samples_per_pixel(2).with_max_depth(50).build()
+    with rtw.Renderer(precision=rtw.RTW_F32) as r:
+        r.set_scene(soa)
+        full = torch.zeros((H, W, 3), dtype=torch.float32, device="cuda:0")
+        r.render_device(cam, 109, full.data_ptr(), full.numel() * 4)
+        rows_max = max(rtw.rows_for_rank(H, k, nranks) for k in range(nranks))
+        bufs = [torch.zeros((rows_max, W, 3), dtype=torch.float32, device="cuda:0") for _ in range(nranks)]
+        for k in range(nranks):
+            r.render_device(cam, 109, bufs[k].data_ptr(), bufs[k].numel() * 4, rank=k, nranks=nranks)
+        torch.cuda.synchronize()
+        img = torch.empty_like(full)
+        sharding.assemble(img, bufs, H)
+    assert torch.equal(torch.nan_to_num(img, nan=-7.0), torch.nan_to_num(full, nan=-7.0))
