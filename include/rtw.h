@@ -103,8 +103,11 @@ typedef struct rtw_camera {
 } rtw_camera;
 
 /* Flattened world + lights, struct-of-arrays, caller-owned host memory.
- * world  = planes + spheres (closest hit over all of them, bvh.rs:164-188)
- * lights = spheres (HittableList::pdf_value / random, hittable_list.rs:408-419) */
+ * world  = planes + spheres + quads + transformed cuboids (closest hit over
+ *          all of them, bvh.rs:164-188), materials and their textures
+ * lights = the light list in order: spheres, quads and entries with the
+ *          Hittable defaults (HittableList::pdf_value / random,
+ *          hittable_list.rs:408-419) */
 typedef struct rtw_scene {
     uint32_t n_spheres;
     const double *spheres;        /* n_spheres x {cx, cy, cz, radius} */
@@ -191,7 +194,9 @@ int rtw_set_accel(rtw_ctx *ctx, int accel);
  * "lds" (1 = stage the sphere list in LDS when it fits, 0 = read it from HBM),
  * "robust" (f32 ray-sphere tests in closest-approach form: 1 on, 0 off,
  * 2 = by the scene's distance-to-radius ratio, the default),
- * "bvh_leaf" (spheres per BVH leaf, 1..15, default 4; takes effect at the
+ * "xcd" (1 = contiguous task runs per XCD; 0 = round-robin, the default),
+ * "bvh_leaf" (spheres per BVH leaf, 1..15; 0 = auto, the default: 4, or 8 for
+ * scenes of >= 100k spheres; takes effect at the
  * next rtw_set_scene), "light_bvh_min" (light lists this long or longer take the light BVH in
  * the BVH kernels, default 64), "partial_max" (bytes of chunk sums an auto chunk may use, default 8 GiB),
  * "bvh_kind" (3 = binary while-while on the tree staged in LDS, the

@@ -36,7 +36,11 @@ struct rtw_ctx {
     size_t bvh_lds_max = 32 * 1024;   // LDS per workgroup allowed for bvh_kind 3
     int robust = 2;                   // f32 closest-approach tests: 1 on, 0 off, 2 by scene scale
     double scene_extent = 0.0, min_radius = 0.0;   // of the staged scene (robust = 2)
-    uint32_t bvh_leaf = 4;            // spheres per BVH leaf (set before rtw_set_scene)
+    uint32_t bvh_leaf = 0;            // spheres per BVH leaf (set before rtw_set_scene); 0 = auto:
+                                      // 4, or 8 for scenes of >= 100k spheres (C5: +12 %)
+    uint32_t xcd = 0;                 // 1: contiguous task runs per XCD (measured 2x SLOWER on C2,
+                                      // C3 and C5: each XCD gets an image band, sky bands finish
+                                      // early -- the round-robin default balances), 0: off
     uint32_t light_bvh_min = 64;      // light lists at least this long use the light BVH
                                       // (C2, 19 lights: the linear masked loop is faster)
     hipStream_t stream = nullptr;
@@ -638,6 +642,7 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
     p.group = std::max<uint32_t>(1, std::min<uint32_t>(group, std::max<uint32_t>(p.n_chunks, 1)));
     p.n_groups = p.n_chunks ? (p.n_chunks + p.group - 1) / p.group : 0;
     p.n_tasks = p.n_local_tiles * p.n_groups;
+    p.xcd = c->xcd;
     const size_t partial_bytes = std::max<size_t>((size_t)p.n_chunks * p.n_local_tiles * 64 * 3 * sizeof(R), 64);
     int rc = ensure(c, &c->d_partial, &c->partial_cap, partial_bytes);
     if (rc) return rc;
@@ -793,7 +798,8 @@ int rtw_set_tuning(rtw_ctx* c, const char* key, int64_t value) {
     if (k == "chunk") c->chunk = (uint32_t)value;
     else if (k == "auto_chunk") c->auto_chunk = std::max<uint32_t>(1, (uint32_t)value);
     else if (k == "robust") c->robust = (int)std::min<int64_t>(value, 2);
-    else if (k == "bvh_leaf") c->bvh_leaf = (uint32_t)std::max<int64_t>(1, std::min<int64_t>(value, 15));
+    else if (k == "bvh_leaf") c->bvh_leaf = (uint32_t)std::min<int64_t>(value, 15);
+    else if (k == "xcd") c->xcd = value ? 1u : 0u;
     else if (k == "light_bvh_min") c->light_bvh_min = (uint32_t)std::min<int64_t>(value, 1u << 30);
     else if (k == "partial_max") c->partial_max = std::max<size_t>(1 << 20, (size_t)value);
     else if (k == "group") c->group = (uint32_t)value;
@@ -904,8 +910,9 @@ int rtw_set_scene(rtw_ctx* c, const rtw_scene* s) {
     // pointer member of DevScene must be listed in `rebase`)
     rtw::DevScene<float> tmp32{};
     rtw::DevScene<double> tmp64{};
-    std::vector<unsigned char> blob = c->precision == RTW_F32 ? stage_scene<float>(s, &tmp32, 0, c->bvh_leaf)
-                                                               : stage_scene<double>(s, &tmp64, 0, c->bvh_leaf);
+    const uint32_t leaf = c->bvh_leaf ? c->bvh_leaf : (s->n_spheres >= 100000 ? 8u : 4u);
+    std::vector<unsigned char> blob = c->precision == RTW_F32 ? stage_scene<float>(s, &tmp32, 0, leaf)
+                                                               : stage_scene<double>(s, &tmp64, 0, leaf);
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     if (c->scene_bytes < blob.size()) {
         if (c->d_scene) (void)hipFree(c->d_scene);

@@ -972,7 +972,21 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? RTW_WAVES : 1) render
     if constexpr (kWorld == kWorldBvhLds) li = l_li;
 
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const uint32_t task = blockIdx.x * kWavesPerBlock + wave;
+    // Workgroups are dispatched round-robin over the 8 XCDs (block b -> XCD
+    // b % 8), each with its own L2.  With p.xcd the block -> task map hands
+    // every XCD one contiguous run of tasks (neighbouring tiles: similar rays,
+    // the same BVH nodes and spheres) instead of every 8th task; the work of
+    // a task is unchanged, so the image is too.  Measured 2x slower (C2, C3,
+    // C5): an XCD then owns an image band, and the sky bands finish first --
+    // off by default.
+    uint32_t blk = blockIdx.x;
+    if (p.xcd) {
+        const uint32_t nb = gridDim.x, per = nb / 8u, rem = nb % 8u;
+        const uint32_t x = blk % 8u, k = blk / 8u;
+        // XCD x runs blocks x, x + 8, ...: (per + (x < rem)) of them
+        blk = x * per + min(x, rem) + k;
+    }
+    const uint32_t task = blk * kWavesPerBlock + wave;
     if (task >= p.n_tasks) return;
     const uint32_t lt = task / p.n_groups;
     const uint32_t cg = task - lt * p.n_groups;
@@ -1292,7 +1306,12 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? RTW_WAVES : 1) render
                     else
                         acc = lights_pdf_sum<kRobust>(li, p.sc.n_lights, pnt, dir);
 #if RTW_EXP == 2
-                    segs += lights_pdf_sum<kRobust>(li, p.sc.n_lights, pnt, mk(dir.y, dir.z, dir.x)) == (R)-7 ? 1u : 0u;
+                    if constexpr (kLightBvh)
+                        segs += lights_pdf_bvh<kRobust>(p.sc, pnt, mk(dir.y, dir.z, dir.x),
+                                                        reinterpret_cast<int32_t*>(smem) + wave * p.stack * 64 + lane) ==
+                                (R)-7 ? 1u : 0u;
+                    else
+                        segs += lights_pdf_sum<kRobust>(li, p.sc.n_lights, pnt, mk(dir.y, dir.z, dir.x)) == (R)-7 ? 1u : 0u;
 #endif
                     // / len; a BVH leaf list multiplies by len and divides again (bvh.rs:67-76, 191-194)
                     R lpdf = PR::div_(acc, (R)p.sc.n_list);

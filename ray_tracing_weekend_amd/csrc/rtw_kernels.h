@@ -153,6 +153,7 @@ struct KParams {
     uint32_t n_tasks;                 // n_local_tiles * n_groups
     uint32_t stack;                   // BVH traversal stack entries per lane (LDS)
     uint32_t light_bvh;               // 1: light pdf through sc.lbvh (BVH kernels only)
+    uint32_t xcd;                     // 1: XCD-aware workgroup -> task mapping
 };
 
 // Host-side launch helpers (defined in render_f32.hip / render_f64.hip).
