@@ -195,6 +195,7 @@ int rtw_set_accel(rtw_ctx *ctx, int accel);
  * "robust" (f32 ray-sphere tests in closest-approach form: 1 on, 0 off,
  * 2 = by the scene's distance-to-radius ratio, the default),
  * "xcd" (1 = contiguous task runs per XCD; 0 = round-robin, the default),
+ * "item_order" (wave item pool: 1 = sample-major, the default; 0 = pixel-major),
  * "bvh_leaf" (spheres per BVH leaf, 1..15; 0 = auto, the default: 4, or 8 for
  * scenes of >= 100k spheres; takes effect at the
  * next rtw_set_scene), "light_bvh_min" (light lists this long or longer take the light BVH in

@@ -38,6 +38,7 @@ struct rtw_ctx {
     double scene_extent = 0.0, min_radius = 0.0;   // of the staged scene (robust = 2)
     uint32_t bvh_leaf = 0;            // spheres per BVH leaf (set before rtw_set_scene); 0 = auto:
                                       // 4, or 8 for scenes of >= 100k spheres (C5: +12 %)
+    uint32_t item_order = 1;          // wave item pool: 1 sample-major (C2 +1.3 %, C3 +5 %, C5 +2 %), 0 pixel-major
     uint32_t xcd = 0;                 // 1: contiguous task runs per XCD (measured 2x SLOWER on C2,
                                       // C3 and C5: each XCD gets an image band, sky bands finish
                                       // early -- the round-robin default balances), 0: off
@@ -643,6 +644,7 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
     p.n_groups = p.n_chunks ? (p.n_chunks + p.group - 1) / p.group : 0;
     p.n_tasks = p.n_local_tiles * p.n_groups;
     p.xcd = c->xcd;
+    p.item_order = c->item_order;
     const size_t partial_bytes = std::max<size_t>((size_t)p.n_chunks * p.n_local_tiles * 64 * 3 * sizeof(R), 64);
     int rc = ensure(c, &c->d_partial, &c->partial_cap, partial_bytes);
     if (rc) return rc;
@@ -800,6 +802,7 @@ int rtw_set_tuning(rtw_ctx* c, const char* key, int64_t value) {
     else if (k == "robust") c->robust = (int)std::min<int64_t>(value, 2);
     else if (k == "bvh_leaf") c->bvh_leaf = (uint32_t)std::min<int64_t>(value, 15);
     else if (k == "xcd") c->xcd = value ? 1u : 0u;
+    else if (k == "item_order") c->item_order = value ? 1u : 0u;
     else if (k == "light_bvh_min") c->light_bvh_min = (uint32_t)std::min<int64_t>(value, 1u << 30);
     else if (k == "partial_max") c->partial_max = std::max<size_t>(1 << 20, (size_t)value);
     else if (k == "group") c->group = (uint32_t)value;

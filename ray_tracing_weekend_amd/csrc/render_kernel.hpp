@@ -995,7 +995,23 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? RTW_WAVES : 1) render
     const uint32_t ty = tr * p.nranks + p.rank;
     const uint32_t c_begin = cg * p.group;
     const uint32_t c_end = min(c_begin + p.group, p.n_chunks);
-    const uint32_t n_items = 64u * (c_end - c_begin);
+    const uint32_t glen = c_end - c_begin;
+    const uint32_t n_items = 64u * glen;
+    // item q -> (pixel px, chunk c): pixel-major (p.item_order 0: q = chunk
+    // offset * 64 + px -- the 64 lanes start on the tile's 64 pixels) or
+    // sample-major (1: q = px * glen + chunk offset -- the lanes start on a
+    // few pixels' consecutive samples: coherent primary rays and first hits).
+    // Every item is still one (pixel, chunk) folded in order by the reduce
+    // kernel, so the image does not depend on it.
+    auto decode = [&](uint32_t qq, uint32_t& px_out, uint32_t& c_out) {
+        if (p.item_order) {
+            px_out = qq / glen;
+            c_out = c_begin + (qq - px_out * glen);
+        } else {
+            px_out = qq & 63u;
+            c_out = c_begin + (qq >> 6);
+        }
+    };
 
     const V3<R> center = v3of(p.center), p00 = v3of(p.p00), du = v3of(p.du), dv = v3of(p.dv);
     const V3<R> bg = v3of(p.bg);
@@ -1047,8 +1063,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? RTW_WAVES : 1) render
                     (uint32_t)(want >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)want, 0u));
                 q = next_q + below;
                 if (q < n_items) {
-                    px = q & 63u;
-                    c = c_begin + (q >> 6);
+                    decode(q, px, c);
                     i = tx * kTile + (px & 7u);
                     j = ty * kTile + (px >> 3);
                     if (i < p.W && j < p.H) {
@@ -1069,8 +1084,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? RTW_WAVES : 1) render
     };
     // the first 64 items go to lanes 0..63 in order
     need = false;
-    px = lane;
-    c = c_begin;
+    decode(lane, px, c);
     i = tx * kTile + (px & 7u);
     j = ty * kTile + (px >> 3);
     if (i < p.W && j < p.H) {

@@ -154,6 +154,7 @@ struct KParams {
     uint32_t stack;                   // BVH traversal stack entries per lane (LDS)
     uint32_t light_bvh;               // 1: light pdf through sc.lbvh (BVH kernels only)
     uint32_t xcd;                     // 1: XCD-aware workgroup -> task mapping
+    uint32_t item_order;              // 0: pixel-major item pool, 1: sample-major
 };
 
 // Host-side launch helpers (defined in render_f32.hip / render_f64.hip).

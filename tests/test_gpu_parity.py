@@ -694,3 +694,15 @@ def test_c2_full_frame_rank_split_is_the_single_render(nranks):
         img = torch.empty_like(full)
         sharding.assemble(img, bufs, H)
     assert torch.equal(torch.nan_to_num(img, nan=-7.0), torch.nan_to_num(full, nan=-7.0))
+
+
+@pytest.mark.parametrize("prec", [rtw.RTW_F32, rtw.RTW_F64])
+def test_scheduling_knobs_do_not_change_the_image(prec):
+    """The wave item pool order (pixel- / sample-major), the XCD task mapping
+    and the task size only move work between lanes: same image bit for bit."""
+    soa, b = _scene()
+    cam = b.with_image_width(40).with_image_height(24).with_samples_per_pixel(9).with_max_depth(50).build()
+    base, _, cb = _render_gpu(soa, cam, 113, prec)
+    for t in ({"item_order": 1}, {"xcd": 1}, {"item_order": 1, "target_tasks": 1000}):
+        img, _, cv = _render_gpu(soa, cam, 113, prec, tuning=t)
+        assert _same(base, img) and cb == cv, t
