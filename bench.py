@@ -72,8 +72,14 @@ def pmc_traffic(workload, precision, world):
     FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md "HBM"), or None."""
     import glob
     dtype = "float" if precision == "f32" else "double"
+    import re
     best = None
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json"))):
+
+    def version(f):   # profiles/r01_v11_traffic.json -> (1, 11): the newest profile wins
+        m = re.search(r"r(\d+)_v(\d+)_traffic", os.path.basename(f))
+        return (int(m.group(1)), int(m.group(2))) if m else (0, 0)
+
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json")), key=version):
         with open(f) as fh:
             d = json.load(fh)
         if d.get("workload") == workload and any(

@@ -490,90 +490,6 @@ __device__ __forceinline__ void bvh_traverse_ww(const DevScene<R>& sc, int32_t b
     }
 }
 
-// Variant of bvh_traverse_ww (RTW_TRAV >= 1, experiments): the inner-node
-// step without data-dependent branches -- the near/far children, the push
-// and the pop are selects around one unconditional read of the stack top.
-// RTW_TRAV >= 2 also tests both children's slabs with packed f32 FMAs
-// (v_pk_fma_f32: the node keeps each bound of the two children adjacent).
-#ifndef RTW_TRAV
-#define RTW_TRAV 0
-#endif
-template <typename R>
-__device__ __forceinline__ void slab2(const BvhNode<R>& nd, R ix, R iy, R iz, R oix, R oiy, R oiz, R tb,
-                                      R (&tn)[2], R (&tf)[2]) {
-    if constexpr (sizeof(R) == 4 && RTW_TRAV >= 2) {
-        typedef float f2 __attribute__((ext_vector_type(2)));
-        const f2 vix = {ix, ix}, viy = {iy, iy}, viz = {iz, iz};
-        const f2 nox = {-oix, -oix}, noy = {-oiy, -oiy}, noz = {-oiz, -oiz};
-        const f2 x0 = __builtin_elementwise_fma(*reinterpret_cast<const f2*>(nd.lo_x), vix, nox);
-        const f2 x1 = __builtin_elementwise_fma(*reinterpret_cast<const f2*>(nd.hi_x), vix, nox);
-        const f2 y0 = __builtin_elementwise_fma(*reinterpret_cast<const f2*>(nd.lo_y), viy, noy);
-        const f2 y1 = __builtin_elementwise_fma(*reinterpret_cast<const f2*>(nd.hi_y), viy, noy);
-        const f2 z0 = __builtin_elementwise_fma(*reinterpret_cast<const f2*>(nd.lo_z), viz, noz);
-        const f2 z1 = __builtin_elementwise_fma(*reinterpret_cast<const f2*>(nd.hi_z), viz, noz);
-#pragma unroll
-        for (int c = 0; c < 2; ++c) {
-            tn[c] = fmax(fmax(fmin(x0[c], x1[c]), fmin(y0[c], y1[c])), fmax(fmin(z0[c], z1[c]), (R)0));
-            tf[c] = fmin(fmin(fmax(x0[c], x1[c]), fmax(y0[c], y1[c])), fmin(fmax(z0[c], z1[c]), tb));
-        }
-    } else {
-#pragma unroll
-        for (int c = 0; c < 2; ++c) {
-            const R x0 = nd.lo_x[c] * ix - oix, x1 = nd.hi_x[c] * ix - oix;
-            const R y0 = nd.lo_y[c] * iy - oiy, y1 = nd.hi_y[c] * iy - oiy;
-            const R z0 = nd.lo_z[c] * iz - oiz, z1 = nd.hi_z[c] * iz - oiz;
-            tn[c] = fmax(fmax(fmin(x0, x1), fmin(y0, y1)), fmax(fmin(z0, z1), (R)0));
-            tf[c] = fmin(fmin(fmax(x0, x1), fmax(y0, y1)), fmin(fmax(z0, z1), tb));
-        }
-    }
-}
-
-template <typename R, typename TT>
-__device__ __forceinline__ void bvh_traverse_ww2(const DevScene<R>& sc, int32_t base, V3<R> o, V3<R> d,
-                                                 TT& T, int32_t* __restrict__ stk,
-                                                 uint32_t& nvis, uint32_t& ntest, bool skip) {
-    constexpr int32_t kDone = 0x7fffffff;
-    const R ix = inv_(d.x), iy = inv_(d.y), iz = inv_(d.z);
-    const R oix = o.x * ix, oiy = o.y * iy, oiz = o.z * iz;
-    const BvhNode<R>* __restrict__ nodes = sc.bvh;
-    int32_t sp = 0;
-    int32_t node = skip ? kDone : 0;   // inner node index, leaf code (< 0) or kDone
-    int32_t leaf = 0;   // parked leaf code, 0 = none
-    for (;;) {
-        for (;;) {
-            {   // park a reached leaf and continue with the stack
-                const bool park = node < 0 && leaf == 0;
-                const int32_t top = stk[max(sp - 1, 0) * 64];
-                leaf = park ? node : leaf;
-                node = park ? (sp ? top : kDone) : node;
-                sp -= (park && sp) ? 1 : 0;
-            }
-            const bool inner = node >= 0 && node != kDone;
-            if (!__any(inner) || __all(leaf != 0 || node == kDone)) break;
-            if (inner) {
-                ++nvis;
-                const BvhNode<R>& nd = nodes[node];
-                R tn[2], tf[2];
-                slab2(nd, ix, iy, iz, oix, oiy, oiz, T.bound(), tn, tf);
-                const bool h0 = tn[0] <= tf[0], h1 = tn[1] <= tf[1];
-                const int32_t c0 = nd.child[0], c1 = nd.child[1];
-                const bool first0 = tn[0] <= tn[1];
-                const bool both = h0 && h1, any = h0 || h1;
-                const int32_t cnear = (h0 && (!h1 || first0)) ? c0 : c1;
-                const int32_t top = stk[max(sp - 1, 0) * 64];
-                stk[sp * 64] = first0 ? c1 : c0;          // kept only when both are hit
-                node = any ? cnear : (sp ? top : kDone);
-                sp += both ? 1 : ((!any && sp) ? -1 : 0);
-            }
-        }
-        if (!__any(leaf != 0)) break;   // no parked leaves: every lane is done
-        if (leaf != 0) {
-            test_leaf(sc, base, leaf, T, ntest);
-            leaf = 0;
-        }
-    }
-}
-
 __device__ __forceinline__ uint32_t sign_bit(float x) { return __float_as_uint(x) >> 31; }
 __device__ __forceinline__ int32_t link_of(float x) { return (int32_t)__float_as_uint(x); }
 __device__ __forceinline__ int32_t link_of(double x) { return (int32_t)__double_as_longlong(x); }
@@ -685,7 +601,6 @@ __device__ __forceinline__ void bvh_dispatch(const DevScene<R>& sc, int32_t base
         ++ntest;
     }
     if constexpr (kKind == kWorldBvh4) bvh4_traverse(sc, base, o, d, T, stk, nvis, ntest, skip);
-    else if constexpr (kKind == kWorldBvhWW && RTW_TRAV >= 1) bvh_traverse_ww2(sc, base, o, d, T, stk, nvis, ntest, skip);
     else if constexpr (kKind == kWorldBvhWW) bvh_traverse_ww(sc, base, o, d, T, stk, nvis, ntest, skip);
     else bvh_traverse(sc, base, o, d, T, stk, nvis, ntest, skip);
 }

@@ -1,7 +1,7 @@
 #!/bin/bash
 # A/B timing of compile-time kernel variants (profiling only).
-#   tools/variants.sh build "base:" "trav1:-DRTW_TRAV=1" ...   (here, CPU: hipcc cross-compiles)
-#   tools/variants.sh run base trav1 ...                        (on the GPU box)
+#   tools/variants.sh build "base:" "exp1:-DRTW_EXP=1" ...   (here, CPU: hipcc cross-compiles)
+#   tools/variants.sh run base exp1 ...                        (on the GPU box)
 # build puts each variant's librtw.so under build/variants/<name>/ (git-ignored,
 # shipped to the box with the tree); run times the C2 render with each through
 # RTW_LIB_OVERRIDE (tools/sweep.py, default tuning), twice in alternation.
