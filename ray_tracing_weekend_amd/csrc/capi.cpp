@@ -801,7 +801,7 @@ int rtw_set_tuning(rtw_ctx* c, const char* key, int64_t value) {
     else if (k == "auto_chunk") c->auto_chunk = std::max<uint32_t>(1, (uint32_t)value);
     else if (k == "robust") c->robust = (int)std::min<int64_t>(value, 2);
     else if (k == "bvh_leaf") c->bvh_leaf = (uint32_t)std::min<int64_t>(value, 15);
-    else if (k == "xcd") c->xcd = value ? 1u : 0u;
+    else if (k == "xcd") c->xcd = (uint32_t)std::min<int64_t>(value, 2);
     else if (k == "item_order") c->item_order = value ? 1u : 0u;
     else if (k == "light_bvh_min") c->light_bvh_min = (uint32_t)std::min<int64_t>(value, 1u << 30);
     else if (k == "partial_max") c->partial_max = std::max<size_t>(1 << 20, (size_t)value);

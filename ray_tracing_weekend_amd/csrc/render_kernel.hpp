@@ -894,14 +894,29 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? RTW_WAVES : 1) render
     // a task is unchanged, so the image is too.  Measured 2x slower (C2, C3,
     // C5): an XCD then owns an image band, and the sky bands finish first --
     // off by default.
+    // p.xcd == 2: XCD x = blockIdx % 8 takes the tile rows tr = x (mod 8) --
+    // every XCD still samples the whole image (balanced, like the multi-GPU
+    // interleave), and all tasks of a tile, and of its row, share one L2.
     uint32_t blk = blockIdx.x;
-    if (p.xcd) {
-        const uint32_t nb = gridDim.x, per = nb / 8u, rem = nb % 8u;
-        const uint32_t x = blk % 8u, k = blk / 8u;
-        // XCD x runs blocks x, x + 8, ...: (per + (x < rem)) of them
-        blk = x * per + min(x, rem) + k;
+    uint32_t task;
+    if (p.xcd == 2) {
+        const uint32_t x = blk & 7u, k = blk >> 3;
+        const uint32_t per_row = p.tiles_x * p.n_groups;          // tasks of one tile row
+        const uint32_t ltr = p.n_local_tiles / p.tiles_x;          // this rank's tile rows
+        const uint32_t rows_x = x < ltr ? (ltr - x + 7u) / 8u : 0u;
+        const uint32_t i = k * kWavesPerBlock + wave;              // index in XCD x's task list
+        if (i >= rows_x * per_row) return;
+        const uint32_t r = i / per_row;
+        task = (x + 8u * r) * per_row + (i - r * per_row);
+    } else {
+        if (p.xcd == 1) {
+            const uint32_t nb = gridDim.x, per = nb / 8u, rem = nb % 8u;
+            const uint32_t x = blk % 8u, k = blk / 8u;
+            // XCD x runs blocks x, x + 8, ...: (per + (x < rem)) of them
+            blk = x * per + min(x, rem) + k;
+        }
+        task = blk * kWavesPerBlock + wave;
     }
-    const uint32_t task = blk * kWavesPerBlock + wave;
     if (task >= p.n_tasks) return;
     const uint32_t lt = task / p.n_groups;
     const uint32_t cg = task - lt * p.n_groups;
@@ -1390,7 +1405,13 @@ inline void launch_world(const KParams<R>& p, int world, size_t lds_bytes, uint3
 template <typename R>
 inline int launch_render_impl(const KParams<R>& p, int world, size_t lds_bytes, R* out,
                               hipStream_t stream, hipEvent_t mid) {
-    const uint32_t blocks = (p.n_tasks + kWavesPerBlock - 1) / kWavesPerBlock;
+    uint32_t blocks = (p.n_tasks + kWavesPerBlock - 1) / kWavesPerBlock;
+    if (p.xcd == 2 && p.tiles_x) {
+        // 8 XCD lanes of blocks, each as long as the longest XCD task list
+        const uint32_t ltr = p.n_local_tiles / p.tiles_x;
+        const uint32_t longest = (ltr + 7u) / 8u * p.tiles_x * p.n_groups;
+        blocks = 8u * ((longest + kWavesPerBlock - 1) / kWavesPerBlock);
+    }
     if (blocks) {
         const bool robust = sizeof(R) == 4 && p.sc.robust;
         const bool lbvh = p.light_bvh != 0;

@@ -703,6 +703,7 @@ def test_scheduling_knobs_do_not_change_the_image(prec):
     soa, b = _scene()
     cam = b.with_image_width(40).with_image_height(24).with_samples_per_pixel(9).with_max_depth(50).build()
     base, _, cb = _render_gpu(soa, cam, 113, prec)
-    for t in ({"item_order": 1}, {"xcd": 1}, {"item_order": 1, "target_tasks": 1000}):
+    for t in ({"item_order": 0}, {"xcd": 1}, {"xcd": 2}, {"xcd": 2, "target_tasks": 1000},
+              {"item_order": 0, "target_tasks": 1000}):
         img, _, cv = _render_gpu(soa, cam, 113, prec, tuning=t)
         assert _same(base, img) and cb == cv, t
