@@ -233,6 +233,7 @@ std::vector<unsigned char> stage_scene(const rtw_scene* s, rtw::DevScene<R>* ds,
     const size_t o_sph = reserve(sizeof(R4) * s->n_spheres);
     const size_t o_r = reserve(sizeof(R) * s->n_spheres);
     const size_t o_smat = reserve(sizeof(uint32_t) * s->n_spheres);
+    const size_t o_sshade = reserve(sizeof(R4) * s->n_spheres);
     const size_t o_pl = reserve(sizeof(R) * rtw::kPlaneR * s->n_planes);
     const size_t o_quads = reserve(sizeof(R) * rtw::kQuadR * s->n_quads);
     const size_t o_qmat = reserve(sizeof(uint32_t) * s->n_quads);
@@ -285,7 +286,11 @@ std::vector<unsigned char> stage_scene(const rtw_scene* s, rtw::DevScene<R>* ds,
         // passes (sphere.rs:42-45): r^2 = -inf makes the discriminant -inf
         reinterpret_cast<R4*>(b + o_sph)[k] = R4{(R)p[0], (R)p[1], (R)p[2], p[3] < 0 ? (R)-INFINITY : r * r};
         reinterpret_cast<R*>(b + o_r)[k] = r;
-        reinterpret_cast<uint32_t*>(b + o_smat)[k] = s->sphere_mat[k];
+        const uint32_t m = s->sphere_mat[k], t = s->mat_type[m];
+        reinterpret_cast<uint32_t*>(b + o_smat)[k] = m | (t << 24);
+        const double* mp = s->mat_params + 5 * m;
+        const double w = t == RTW_METAL ? mp[3] : (t == RTW_DIELECTRIC ? mp[4] : 0.0);
+        reinterpret_cast<R4*>(b + o_sshade)[k] = R4{(R)mp[0], (R)mp[1], (R)mp[2], (R)w};
     }
     for (uint32_t k = 0; k < s->n_spheres; ++k)
         if (iso[k]) reinterpret_cast<uint32_t*>(b + o_smat)[k] |= 0x80000000u;
@@ -397,6 +402,7 @@ std::vector<unsigned char> stage_scene(const rtw_scene* s, rtw::DevScene<R>* ds,
     ds->sph = reinterpret_cast<const R4*>(base + o_sph);
     ds->sph_r = reinterpret_cast<const R*>(base + o_r);
     ds->sph_mat = reinterpret_cast<const uint32_t*>(base + o_smat);
+    ds->sph_shade = reinterpret_cast<const R4*>(base + o_sshade);
     ds->planes = reinterpret_cast<const R*>(base + o_pl);
     ds->plane_mat = reinterpret_cast<const uint32_t*>(base + o_pmat);
     ds->mat_type = reinterpret_cast<const uint32_t*>(base + o_mt);
@@ -527,6 +533,7 @@ int validate_scene(rtw_ctx* c, const rtw_scene* s) {
                                           "BVH aux_random indexes it inconsistently (bvh.rs:78-92)");
     for (uint32_t k = 0; k < s->n_materials; ++k)
         if (s->mat_type[k] > RTW_DIFFUSE_LIGHT) return fail(c, RTW_E_INVALID, "unknown material type");
+    if (s->n_materials >= (1u << 24)) return fail(c, RTW_E_UNSUPPORTED, "more than 2^24 materials");
     if (s->mat_tex) {
         if ((s->n_textures && (!s->tex_type || !s->tex_params || !s->tex_refs)) ||
             (s->n_perlin && (!s->perlin_vec || !s->perlin_perm)))
@@ -943,7 +950,7 @@ int rtw_set_scene(rtw_ctx* c, const rtw_scene* s) {
             using T = std::remove_reference_t<decltype(ptr)>;
             ptr = reinterpret_cast<T>(reinterpret_cast<uintptr_t>(ptr) + base);
         };
-        fix(ds.sph); fix(ds.sph_r); fix(ds.sph_mat); fix(ds.planes); fix(ds.plane_mat);
+        fix(ds.sph); fix(ds.sph_r); fix(ds.sph_mat); fix(ds.sph_shade); fix(ds.planes); fix(ds.plane_mat);
         fix(ds.mat_type); fix(ds.mat_p); fix(ds.lights); fix(ds.bvh); fix(ds.bsph); fix(ds.bid);
         fix(ds.bvh4); fix(ds.lbvh); fix(ds.lsph); fix(ds.lid);
         fix(ds.quads); fix(ds.quad_mat); fix(ds.lquads);
@@ -952,7 +959,7 @@ int rtw_set_scene(rtw_ctx* c, const rtw_scene* s) {
         if (ds.mat_tex) fix(ds.mat_tex);
         fix(ds.tex_type); fix(ds.tex_p); fix(ds.tex_refs); fix(ds.perlin_vec); fix(ds.perlin_perm);
     };
-    static_assert(offsetof(rtw::DevScene<float>, n_sph) == 27 * sizeof(void*),
+    static_assert(offsetof(rtw::DevScene<float>, n_sph) == 28 * sizeof(void*),
                   "DevScene gained a pointer: update rebase");
     if (c->precision == RTW_F32) {
         rebase(tmp32);

@@ -1101,7 +1101,8 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? RTW_WAVES : 1) render
                 // HitRecord::new, hittable.rs:101-129
                 V3<R> pnt = o + d * tb;
                 V3<R> outward;
-                uint32_t m;
+                uint32_t m, mtype;
+                R4<R> mp;
                 int32_t next_self = -1;
                 bool box_hit = false;
                 bool box_front = false;
@@ -1121,6 +1122,8 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? RTW_WAVES : 1) render
                     const V3<R> po = o2 + d2 * t2;
                     pnt = mat3_mul(B + kBoxRot, po) + q3(B, kBoxT);
                     m = p.sc.box_mat[best - bbase];
+                    mtype = p.sc.mat_type[m];
+                    mp = p.sc.mat_p[m];
                     box_hit = true;
                     if constexpr (kTex) {                          // get_quad_uv, object space
                         const R* Q = B + kQuadR * qd;
@@ -1132,11 +1135,15 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? RTW_WAVES : 1) render
                     const R* pl = p.sc.planes + kPlaneR * best;
                     outward = mk(pl[3], pl[4], pl[5]);
                     m = p.sc.plane_mat[best];
+                    mtype = p.sc.mat_type[m];
+                    mp = p.sc.mat_p[m];
                     if constexpr (kTex) plane_uv(pl, pnt, hu, hv);
                 } else if (best < bbase) {
                     const R* Q = p.sc.quads + kQuadR * (best - nplanes);
                     outward = q3(Q, 12);                           // quadrilateral.rs:97
                     m = p.sc.quad_mat[best - nplanes];
+                    mtype = p.sc.mat_type[m];
+                    mp = p.sc.mat_p[m];
                     if constexpr (kTex) {                          // get_quad_uv, quadrilateral.rs:58-63
                         const V3<R> pq = pnt - q3(Q, 0);
                         hu = dot(cross(pq, q3(Q, 6)), q3(Q, 9));
@@ -1146,15 +1153,18 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? RTW_WAVES : 1) render
                     const uint32_t k = (uint32_t)(best - sbase);
                     const R4<R> sk = p.sc.sph[k];
                     outward = PR::divs(pnt - mk(sk.x, sk.y, sk.z), p.sc.sph_r[k]);  // sphere.rs:82-83
+                    // one level of loads: the sphere's material kind and
+                    // parameters are copied per sphere (sph_mat word: id,
+                    // kind, isolated flag; sph_shade: albedo + fuzz | ior)
                     const uint32_t mw = p.sc.sph_mat[k];
-                    m = mw & 0x7fffffffu;
+                    m = mw & 0xffffffu;
+                    mtype = (mw >> 24) & 0x7fu;
+                    mp = p.sc.sph_shade[k];
                     next_self = (mw >> 31) ? (int32_t)k : -1;   // bit 31: isolated sphere
                     if constexpr (kTex) sphere_uv(outward, hu, hv);
                 }
                 const bool front = box_hit ? box_front : dot(d, outward) < (R)0;
                 const V3<R> nrm = front ? outward : -outward;
-                const uint32_t mtype = p.sc.mat_type[m];
-                const R4<R> mp = p.sc.mat_p[m];
                 // Material::emitted: DiffuseLight's colour (material.rs:508-514),
                 // black for every other material (material.rs:42-44)
                 // the material's colour: its texture at (u, v, p) (kTex) or its SolidColour

@@ -34,7 +34,8 @@ struct alignas(4 * sizeof(R)) R4 {
 // Device-resident scene, precision R.  HBM layout (all arrays tightly packed):
 //   sph      : n_sph   x R4 {cx, cy, cz, r*r}   -- staged into LDS by the brute kernel
 //   sph_r    : n_sph   x R  radius              -- read once per hit (normal)
-//   sph_mat  : n_sph   x u32 material id
+//   sph_mat  : n_sph   x u32 {material id (bits 0-23), kind (24-30), isolated (31)}
+//   sph_shade: n_sph   x R4 {albedo r, g, b, fuzz | ior} -- the material's, per sphere
 //   planes   : n_pl    x kPlaneR R {p, n, aabb lo, aabb hi, uv mode, cos, sin, k} (layout below)
 //   plane_mat: n_pl    x u32
 //   mat_type : n_mat   x u32
@@ -76,6 +77,7 @@ struct DevScene {
     const R4<R>* sph;
     const R* sph_r;
     const uint32_t* sph_mat;
+    const R4<R>* sph_shade;
     const R* planes;
     const uint32_t* plane_mat;
     const uint32_t* mat_type;
