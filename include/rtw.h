@@ -198,8 +198,10 @@ int rtw_set_accel(rtw_ctx *ctx, int accel);
  * "item_order" (wave item pool: 1 = sample-major, the default; 0 = pixel-major),
  * "bvh_leaf" (spheres per BVH leaf, 1..15; 0 = auto, the default: 4, or 8 for
  * scenes of >= 100k spheres; takes effect at the
- * next rtw_set_scene), "light_bvh_min" (light lists this long or longer take the light BVH in
- * the BVH kernels, default 64), "partial_max" (bytes of chunk sums an auto chunk may use, default 8 GiB),
+ * next rtw_set_scene), "light_bvh_min" (light lists this long or longer take the light grid
+ * or light BVH in the BVH kernels, default 64), "light_grid" (light-grid resolution in
+ * 1/16 cells per light, default 4; 0 = the light BVH instead; next rtw_set_scene),
+ * "light_leaf" (light spheres per light-BVH leaf, 1..15; 0 = 4), "partial_max" (bytes of chunk sums an auto chunk may use, default 8 GiB),
  * "bvh_kind" (3 = binary while-while on the tree staged in LDS, the
  * default, 1 = binary while-while from L1/L2, 2 = 4-wide octant BVH, 0 =
  * binary single loop), "bvh_lds_max" (LDS bytes per workgroup bvh_kind 3 may

@@ -38,6 +38,9 @@ struct rtw_ctx {
     double scene_extent = 0.0, min_radius = 0.0;   // of the staged scene (robust = 2)
     uint32_t bvh_leaf = 0;            // spheres per BVH leaf (set before rtw_set_scene); 0 = auto:
                                       // 4, or 8 for scenes of >= 100k spheres (C5: +12 %)
+    uint32_t light_leaf = 0;          // light spheres per light-BVH leaf; 0 = 4
+    uint32_t light_grid = 4;          // light pdf through the light grid at light_grid / 16
+                                      // cells per light (set before rtw_set_scene); 0: light BVH
     uint32_t item_order = 1;          // wave item pool: 1 sample-major (C2 +1.3 %, C3 +5 %, C5 +2 %), 0 pixel-major
     uint32_t xcd = 0;                 // 1: contiguous task runs per XCD (measured 2x SLOWER on C2,
                                       // C3 and C5: each XCD gets an image band, sky bands finish
@@ -222,7 +225,7 @@ void box_derive(const double* b, double* out) {
 // host staging blob, and fill the DevScene pointers relative to `base`.
 template <typename R>
 std::vector<unsigned char> stage_scene(const rtw_scene* s, rtw::DevScene<R>* ds, uintptr_t base,
-                                       uint32_t leaf_max) {
+                                       uint32_t leaf_max, uint32_t light_leaf, double grid_density) {
     using R4 = rtw::R4<R>;
     size_t off = 0;
     auto reserve = [&](size_t bytes) {
@@ -273,10 +276,16 @@ std::vector<unsigned char> stage_scene(const rtw_scene* s, rtw::DevScene<R>* ds,
     // BVH over the light spheres for the light pdf (a query for EVERY light
     // the ray hits, so boxes only cull; the sum itself keeps list order in f64)
     const rtw::BvhBuild lb = rtw::build_bvh(s->lights, s->n_lights,
-                                            std::is_same<R, float>::value ? 1e-5 : 1e-12);
+                                            std::is_same<R, float>::value ? 1e-5 : 1e-12, light_leaf);
     const size_t o_lnodes = reserve(sizeof(rtw::BvhNode<R>) * lb.nodes.size());
     const size_t o_lsph = reserve(sizeof(R4) * s->n_lights);
     const size_t o_lid = reserve(sizeof(uint32_t) * s->n_lights);
+    // uniform grid over the light spheres (grid_density cells per light; 0: none)
+    const rtw::LightGrid lg = grid_density > 0 ? rtw::build_light_grid(s->lights, s->n_lights, grid_density)
+                                               : rtw::LightGrid{};
+    const size_t o_lgs = reserve(sizeof(uint32_t) * lg.start.size());
+    const size_t o_lgsph = reserve(sizeof(R4) * lg.items.size());
+    const size_t o_lgid = reserve(sizeof(uint32_t) * lg.items.size());
     std::vector<unsigned char> blob(align_up(off, 64) + 64, 0);
     unsigned char* b = blob.data();
     for (uint32_t k = 0; k < s->n_spheres; ++k) {
@@ -493,6 +502,25 @@ std::vector<unsigned char> stage_scene(const rtw_scene* s, rtw::DevScene<R>* ds,
     ds->lid = reinterpret_cast<const uint32_t*>(base + o_lid);
     ds->n_lnodes = (uint32_t)lb.nodes.size();
     ds->lbvh_depth = lb.depth;
+    if (!lg.start.empty())
+        memcpy(b + o_lgs, lg.start.data(), sizeof(uint32_t) * lg.start.size());
+    for (size_t k = 0; k < lg.items.size(); ++k) {
+        const uint32_t id = lg.items[k];
+        reinterpret_cast<R4*>(b + o_lgsph)[k] = reinterpret_cast<const R4*>(b + o_li)[id];
+        reinterpret_cast<uint32_t*>(b + o_lgid)[k] = id;
+    }
+    ds->lg_start = reinterpret_cast<const uint32_t*>(base + o_lgs);
+    ds->lg_sph = reinterpret_cast<const R4*>(base + o_lgsph);
+    ds->lg_id = reinterpret_cast<const uint32_t*>(base + o_lgid);
+    for (int a = 0; a < 3; ++a) {
+        ds->lg_lo[a] = (R)lg.lo[a];
+        ds->lg_hi[a] = (R)(lg.lo[a] + lg.n[a] * lg.cell[a]);
+        ds->lg_cell[a] = (R)lg.cell[a];
+        ds->lg_inv[a] = (R)(1.0 / lg.cell[a]);
+        ds->lg_n[a] = lg.n[a];
+    }
+    ds->lg_big = lg.n_big;
+    ds->lg_on = lg.start.empty() ? 0u : 1u;
     ds->bvh4 = reinterpret_cast<const rtw::Bvh4Node<R>*>(base + o_nodes4);
     ds->n_nodes4 = (uint32_t)n4;
     ds->bvh4_stack = b4.max_stack;
@@ -682,9 +710,11 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
         // the light pdf goes through the light BVH (same per-lane stack) for
         // longer light lists
         const uint32_t light_stack = p.sc.lbvh_depth + 1;
-        p.light_bvh = (p.sc.n_lights >= c->light_bvh_min && light_stack <= rtw::kBvhStack &&
-                       p.sc.n_lquads == 0) ? 1u : 0u;
-        const uint32_t min_stack = p.light_bvh ? light_stack : 1u;
+        if (p.sc.n_lights >= c->light_bvh_min && p.sc.n_lquads == 0) {
+            if (p.sc.lg_on) p.light_bvh = 2;                          // light grid
+            else if (light_stack <= rtw::kBvhStack) p.light_bvh = 1;  // light BVH
+        }
+        const uint32_t min_stack = p.light_bvh == 1 ? light_stack : 1u;
         // binary traversal pushes at most one entry per inner level
         const uint32_t bin_stack = std::max(p.sc.bvh_depth + 1, min_stack);
         const size_t stacks = (size_t)rtw::kWavesPerBlock * 64 * sizeof(int32_t);
@@ -714,7 +744,7 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
     if (p.sc.mat_tex && (world == rtw::kWorldBvh4 || world == rtw::kWorldBvh)) {
         world = rtw::kWorldBvhWW;
         bvh_width = 2;
-        p.stack = std::max(p.sc.bvh_depth + 1, p.light_bvh ? p.sc.lbvh_depth + 1 : 1u);
+        p.stack = std::max(p.sc.bvh_depth + 1, p.light_bvh == 1 ? p.sc.lbvh_depth + 1 : 1u);
         if (p.stack > rtw::kBvhStack) return fail(c, RTW_E_UNSUPPORTED, "BVH deeper than the kernel's traversal stack");
     }
     hipEvent_t* ev = c->ring[c->n_renders % rtw_ctx::kRing];
@@ -808,6 +838,8 @@ int rtw_set_tuning(rtw_ctx* c, const char* key, int64_t value) {
     else if (k == "auto_chunk") c->auto_chunk = std::max<uint32_t>(1, (uint32_t)value);
     else if (k == "robust") c->robust = (int)std::min<int64_t>(value, 2);
     else if (k == "bvh_leaf") c->bvh_leaf = (uint32_t)std::min<int64_t>(value, 15);
+    else if (k == "light_leaf") c->light_leaf = (uint32_t)std::min<int64_t>(value, 15);
+    else if (k == "light_grid") c->light_grid = (uint32_t)std::min<int64_t>(value, 1024);
     else if (k == "xcd") c->xcd = (uint32_t)std::min<int64_t>(value, 2);
     else if (k == "item_order") c->item_order = value ? 1u : 0u;
     else if (k == "light_bvh_min") c->light_bvh_min = (uint32_t)std::min<int64_t>(value, 1u << 30);
@@ -921,8 +953,12 @@ int rtw_set_scene(rtw_ctx* c, const rtw_scene* s) {
     rtw::DevScene<float> tmp32{};
     rtw::DevScene<double> tmp64{};
     const uint32_t leaf = c->bvh_leaf ? c->bvh_leaf : (s->n_spheres >= 100000 ? 8u : 4u);
-    std::vector<unsigned char> blob = c->precision == RTW_F32 ? stage_scene<float>(s, &tmp32, 0, leaf)
-                                                               : stage_scene<double>(s, &tmp64, 0, leaf);
+    const uint32_t light_leaf = c->light_leaf ? c->light_leaf : rtw::kLeafMax;
+    // the light grid only for light lists long enough to skip the linear loop
+    const double grid = s->n_lights >= c->light_bvh_min ? c->light_grid / 16.0 : 0.0;
+    std::vector<unsigned char> blob = c->precision == RTW_F32
+                                          ? stage_scene<float>(s, &tmp32, 0, leaf, light_leaf, grid)
+                                          : stage_scene<double>(s, &tmp64, 0, leaf, light_leaf, grid);
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     if (c->scene_bytes < blob.size()) {
         if (c->d_scene) (void)hipFree(c->d_scene);
@@ -952,14 +988,14 @@ int rtw_set_scene(rtw_ctx* c, const rtw_scene* s) {
         };
         fix(ds.sph); fix(ds.sph_r); fix(ds.sph_mat); fix(ds.sph_shade); fix(ds.planes); fix(ds.plane_mat);
         fix(ds.mat_type); fix(ds.mat_p); fix(ds.lights); fix(ds.bvh); fix(ds.bsph); fix(ds.bid);
-        fix(ds.bvh4); fix(ds.lbvh); fix(ds.lsph); fix(ds.lid);
+        fix(ds.bvh4); fix(ds.lbvh); fix(ds.lsph); fix(ds.lid); fix(ds.lg_start); fix(ds.lg_sph); fix(ds.lg_id);
         fix(ds.quads); fix(ds.quad_mat); fix(ds.lquads);
         if (ds.lref) fix(ds.lref);
         fix(ds.boxes); fix(ds.box_mat);
         if (ds.mat_tex) fix(ds.mat_tex);
         fix(ds.tex_type); fix(ds.tex_p); fix(ds.tex_refs); fix(ds.perlin_vec); fix(ds.perlin_perm);
     };
-    static_assert(offsetof(rtw::DevScene<float>, n_sph) == 28 * sizeof(void*),
+    static_assert(offsetof(rtw::DevScene<float>, n_sph) == 31 * sizeof(void*),
                   "DevScene gained a pointer: update rebase");
     if (c->precision == RTW_F32) {
         rebase(tmp32);

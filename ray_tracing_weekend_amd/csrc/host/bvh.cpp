@@ -3,6 +3,7 @@
 
 #include <math.h>
 
+#include <cmath>
 #include <algorithm>
 #include <numeric>
 
@@ -358,6 +359,130 @@ Bvh4Build collapse_bvh4(const BvhBuild& b) {
     c.emit(0, 0, &need);
     out.max_stack = need;
     return out;
+}
+
+LightGrid build_light_grid(const double* L, uint32_t n, double cells_per_light) {
+    LightGrid g;
+    std::vector<uint8_t> big(n, 0);
+    for (uint32_t k = 0; k < n; ++k)
+        for (int a = 0; a < 4; ++a)
+            if (!std::isfinite(L[4 * k + a])) big[k] = 1;
+    // lights much larger than the typical one would stretch the grid box (the
+    // scenes::simple field: r = 0.2 lights at y = 0.2 and one r = 1 sphere --
+    // with it the box is 5x as tall and grazing rays walk 5x as far)
+    {
+        std::vector<double> r;
+        for (uint32_t k = 0; k < n; ++k)
+            if (!big[k]) r.push_back(fabs(L[4 * k + 3]));
+        if (!r.empty()) {
+            std::nth_element(r.begin(), r.begin() + r.size() / 2, r.end());
+            const double med = r[r.size() / 2];
+            for (uint32_t k = 0; k < n; ++k)
+                if (!big[k] && fabs(L[4 * k + 3]) > kGridBigRadius * med) big[k] = 1;
+        }
+    }
+    // cells overlapped by light k's AABB, padded by more than the rounding of
+    // the kernel's cell walk and closest-approach parameter (f32 included)
+    auto range = [&](uint32_t k, int a, int64_t& i0, int64_t& i1) {
+        const double c = L[4 * k + a], r = fabs(L[4 * k + 3]);
+        const double pad = 1e-3 * g.cell[a] + 4e-6 * (fabs(c) + r);
+        i0 = (int64_t)floor((c - r - pad - g.lo[a]) / g.cell[a]);
+        i1 = (int64_t)floor((c + r + pad - g.lo[a]) / g.cell[a]);
+        i0 = std::max<int64_t>(0, std::min<int64_t>(i0, (int64_t)g.n[a] - 1));
+        i1 = std::max<int64_t>(0, std::min<int64_t>(i1, (int64_t)g.n[a] - 1));
+    };
+    // pass 0 sizes the grid over every finite light and sends the lights that
+    // span too many cells to the big list; pass 1 sizes it over the rest
+    for (int pass = 0; pass < 2; ++pass) {
+        double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        uint32_t m = 0;
+        for (uint32_t k = 0; k < n; ++k) {
+            if (big[k]) continue;
+            const double r = fabs(L[4 * k + 3]);
+            for (int a = 0; a < 3; ++a) {
+                lo[a] = std::min(lo[a], L[4 * k + a] - r);
+                hi[a] = std::max(hi[a], L[4 * k + a] + r);
+            }
+            ++m;
+        }
+        if (m == 0) {
+            g = LightGrid{};
+            break;
+        }
+        double scale = 0.0, e[3];
+        for (int a = 0; a < 3; ++a) scale = std::max(scale, std::max(fabs(lo[a]), fabs(hi[a])));
+        for (int a = 0; a < 3; ++a) {
+            const double pb = 1e-4 * (hi[a] - lo[a]) + 1e-5 * scale + 1e-6;
+            lo[a] -= pb;
+            hi[a] += pb;
+            e[a] = hi[a] - lo[a];
+        }
+        // cubic cells of side h with ~cells_per_light * m cells; an extent
+        // thinner than h gets one cell and h is re-solved over the others
+        const double target = std::max(1.0, cells_per_light * m);
+        bool flat[3] = {false, false, false};
+        double h = std::max(e[0], std::max(e[1], e[2]));
+        for (int it = 0; it < 3; ++it) {
+            double vol = 1.0;
+            int dims = 0;
+            for (int a = 0; a < 3; ++a)
+                if (!flat[a]) {
+                    vol *= e[a];
+                    ++dims;
+                }
+            if (dims == 0) break;
+            h = pow(vol / target, 1.0 / dims);
+            bool changed = false;
+            for (int a = 0; a < 3; ++a)
+                if (!flat[a] && e[a] < h) flat[a] = changed = true;
+            if (!changed) break;
+        }
+        for (;;) {
+            uint64_t cells = 1;
+            for (int a = 0; a < 3; ++a) {
+                g.n[a] = flat[a] ? 1u : (uint32_t)std::min(4096.0, std::max(1.0, ceil(e[a] / h)));
+                cells *= g.n[a];
+            }
+            if (cells <= (1u << 24)) break;
+            h *= 1.25;
+        }
+        for (int a = 0; a < 3; ++a) {
+            g.lo[a] = lo[a];
+            g.cell[a] = e[a] / g.n[a];
+        }
+        if (pass == 0)
+            for (uint32_t k = 0; k < n; ++k) {
+                if (big[k]) continue;
+                uint64_t span = 1;
+                for (int a = 0; a < 3; ++a) {
+                    int64_t i0, i1;
+                    range(k, a, i0, i1);
+                    span *= (uint64_t)(i1 - i0 + 1);
+                }
+                if (span > kGridBigCells) big[k] = 1;
+            }
+    }
+    const uint64_t cells = (uint64_t)g.n[0] * g.n[1] * g.n[2];
+    auto each_cell = [&](uint32_t k, auto&& f) {
+        int64_t i0[3], i1[3];
+        for (int a = 0; a < 3; ++a) range(k, a, i0[a], i1[a]);
+        for (int64_t z = i0[2]; z <= i1[2]; ++z)
+            for (int64_t y = i0[1]; y <= i1[1]; ++y)
+                for (int64_t x = i0[0]; x <= i1[0]; ++x) f((uint64_t)((z * g.n[1] + y) * g.n[0] + x));
+    };
+    std::vector<uint32_t> cnt(cells, 0);
+    for (uint32_t k = 0; k < n; ++k)
+        if (big[k]) ++g.n_big;
+        else each_cell(k, [&](uint64_t c) { ++cnt[c]; });
+    g.start.assign(cells + 1, g.n_big);
+    for (uint64_t c = 0; c < cells; ++c) g.start[c + 1] = g.start[c] + cnt[c];
+    g.items.assign(g.start[cells], 0);
+    std::vector<uint32_t> fill(g.start.begin(), g.start.end() - 1);
+    uint32_t q = 0;
+    for (uint32_t k = 0; k < n; ++k)
+        if (big[k]) g.items[q++] = k;
+        else each_cell(k, [&](uint64_t c) { g.items[fill[c]++] = k; });
+    return g;
 }
 
 }  // namespace rtw

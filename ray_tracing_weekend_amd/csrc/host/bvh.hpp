@@ -65,4 +65,23 @@ Bvh4Build collapse_bvh4(const BvhBuild& b);
 // the render kernel skips the traversal for it (self-hit shortcut).
 std::vector<uint8_t> isolated_spheres(const double* spheres, uint32_t n, const BvhBuild& b, double margin);
 
+// Uniform grid over the light spheres for the light pdf's all-hits query
+// (render_kernel.hpp light_grid_walk).  Cell c lists every light whose
+// padded AABB overlaps it, in ascending light index; lights that are not
+// finite, larger than kGridBigRadius x the median radius or span more than
+// kGridBigCells cells form the "big" list every ray tests.  The grid box (lo, lo + n * cell) holds every listed light's AABB.
+struct LightGrid {
+    double lo[3] = {0, 0, 0}, cell[3] = {1, 1, 1};
+    uint32_t n[3] = {1, 1, 1};
+    uint32_t n_big = 0;
+    std::vector<uint32_t> start;     // n_cells + 1 offsets into items (start[0] = n_big)
+    std::vector<uint32_t> items;     // light indices: the big list, then cell by cell
+};
+
+constexpr uint32_t kGridBigCells = 64;
+constexpr double kGridBigRadius = 3.0;   // x the median light radius
+
+// lights: n x {cx, cy, cz, r}; cells_per_light: grid resolution target.
+LightGrid build_light_grid(const double* lights, uint32_t n, double cells_per_light);
+
 }  // namespace rtw

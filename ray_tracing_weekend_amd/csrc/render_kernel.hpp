@@ -732,6 +732,144 @@ __device__ __forceinline__ double lights_pdf_bvh(const DevScene<double>& sc, V3<
     return acc;
 }
 
+// Light pdf through the light grid (KParams::light_bvh == 2; host/bvh.hpp
+// LightGrid): a 3-D DDA walks the cells the ray (o, d), t in [0, inf), crosses
+// and calls item(k, te, tx) for every light listed in a cell, with [te, tx)
+// the ray-parameter interval the walk assigns to that cell.  The intervals
+// partition the real line (the first starts at -inf, the last ends at +inf,
+// each ends where the next starts, never decreasing), so a light counted only
+// where its closest-approach parameter falls is counted at most once however
+// the walk rounds; the host pads every light's cell range by more than that
+// rounding, so a hit light is counted exactly once.  (Fetching the next
+// cells' ranges ahead of the tests measured slower: C5 +3 % to +15 % time.)
+template <typename R, typename Item>
+__device__ __forceinline__ void light_grid_walk(const DevScene<R>& sc, V3<R> o, V3<R> d, Item&& item) {
+    const R kInf = (R)INFINITY;
+    const R ix = inv_(d.x), iy = inv_(d.y), iz = inv_(d.z);
+    R tn, tf;
+    {
+        const R x0 = (sc.lg_lo[0] - o.x) * ix, x1 = (sc.lg_hi[0] - o.x) * ix;
+        const R y0 = (sc.lg_lo[1] - o.y) * iy, y1 = (sc.lg_hi[1] - o.y) * iy;
+        const R z0 = (sc.lg_lo[2] - o.z) * iz, z1 = (sc.lg_hi[2] - o.z) * iz;
+        tn = fmax(fmax(fmin(x0, x1), fmin(y0, y1)), fmax(fmin(z0, z1), (R)0));
+        tf = fmin(fmax(x0, x1), fmin(fmax(y0, y1), fmax(z0, z1)));
+    }
+    if (!(tn <= tf)) return;
+    const int nx = (int)sc.lg_n[0], ny = (int)sc.lg_n[1], nz = (int)sc.lg_n[2];
+    // the entry cell (clamped; NaN -> 0)
+    auto cell_of = [&](R oc, R dc, R lo, R inv, int n) {
+        return (int)fmin(fmax((oc + tn * dc - lo) * inv, (R)0), (R)(n - 1));
+    };
+    int cx = cell_of(o.x, d.x, sc.lg_lo[0], sc.lg_inv[0], nx);
+    int cy = cell_of(o.y, d.y, sc.lg_lo[1], sc.lg_inv[1], ny);
+    int cz = cell_of(o.z, d.z, sc.lg_lo[2], sc.lg_inv[2], nz);
+    const int sx = d.x > 0 ? 1 : (d.x < 0 ? -1 : 0);
+    const int sy = d.y > 0 ? 1 : (d.y < 0 ? -1 : 0);
+    const int sz = d.z > 0 ? 1 : (d.z < 0 ? -1 : 0);
+    R te = -kInf;
+    // where the ray leaves cell c along one axis (+inf: never), not before te
+    auto exit_t = [&](int c, int s, R lo, R cell, R oc, R inv) {
+        return s == 0 ? kInf : fmax((lo + (R)(c + (s > 0 ? 1 : 0)) * cell - oc) * inv, te);
+    };
+    R tmx = exit_t(cx, sx, sc.lg_lo[0], sc.lg_cell[0], o.x, ix);
+    R tmy = exit_t(cy, sy, sc.lg_lo[1], sc.lg_cell[1], o.y, iy);
+    R tmz = exit_t(cz, sz, sc.lg_lo[2], sc.lg_cell[2], o.z, iz);
+    uint32_t c = (uint32_t)((cz * ny + cy) * nx + cx);
+    for (;;) {
+        int axis, ni, nn;
+        R tx;
+        if (tmx <= tmy && tmx <= tmz) {
+            axis = 0; tx = tmx; ni = cx + sx; nn = nx;
+        } else if (tmy <= tmz) {
+            axis = 1; tx = tmy; ni = cy + sy; nn = ny;
+        } else {
+            axis = 2; tx = tmz; ni = cz + sz; nn = nz;
+        }
+        const bool last = !(tx < kInf) || ni < 0 || ni >= nn;
+        if (last) tx = kInf;
+        const uint32_t b = sc.lg_start[c], e = sc.lg_start[c + 1];
+        for (uint32_t k = b; k < e; ++k) item(k, te, tx);
+        if (last) break;
+        te = tx;
+        if (axis == 0) {
+            cx = ni;
+            c += sx;
+            tmx = exit_t(cx, sx, sc.lg_lo[0], sc.lg_cell[0], o.x, ix);
+        } else if (axis == 1) {
+            cy = ni;
+            c += sy * nx;
+            tmy = exit_t(cy, sy, sc.lg_lo[1], sc.lg_cell[1], o.y, iy);
+        } else {
+            cz = ni;
+            c += sz * nx * ny;
+            tmz = exit_t(cz, sz, sc.lg_lo[2], sc.lg_cell[2], o.z, iz);
+        }
+    }
+}
+
+// f32: the big list, then the walk; a light counts in the cell whose interval
+// holds its closest-approach parameter tc = -(d . (o - c)) / (d . d)
+template <bool kRobust>
+__device__ __forceinline__ float lights_pdf_grid(const DevScene<float>& sc, V3<float> o, V3<float> d) {
+    const float a = len2_f32(d);
+    const float ia = __builtin_amdgcn_rcpf(a);
+    float acc = 0.f;
+    for (uint32_t k = 0; k < sc.lg_big; ++k) {
+        const R4<float> L = sc.lg_sph[k];
+        if (light_hit_f32<kRobust>(L, o, d, a, ia)) acc += light_pdf_f32(L, o);
+    }
+    light_grid_walk(sc, o, d, [&](uint32_t k, float te, float tx) {
+        const R4<float> L = sc.lg_sph[k];
+        const float fx = o.x - L.x, fy = o.y - L.y, fz = o.z - L.z;
+        const float tc = -__builtin_fmaf(d.z, fz, __builtin_fmaf(d.y, fy, d.x * fx)) * ia;
+        if (light_hit_f32<kRobust>(L, o, d, a, ia) & (tc >= te) & (tc < tx)) acc += light_pdf_f32(L, o);
+    });
+    return acc;
+}
+// f64 (parity mode): the hit lights' list indices, summed in LIST order as in
+// lights_pdf_bvh; more than 8 hits falls back to the linear loop.
+template <bool kRobust>
+__device__ __forceinline__ double lights_pdf_grid(const DevScene<double>& sc, V3<double> o, V3<double> d) {
+    constexpr uint32_t kMax = 8;
+    uint32_t ids[kMax];
+    uint32_t n = 0;
+    bool overflow = false;
+    auto add = [&](uint32_t id) {
+        if (n < kMax) {
+            uint32_t q = n;
+            while (q > 0 && ids[q - 1] > id) {
+                ids[q] = ids[q - 1];
+                --q;
+            }
+            ids[q] = id;
+            ++n;
+        } else {
+            overflow = true;
+        }
+    };
+    for (uint32_t k = 0; k < sc.lg_big; ++k) {
+        const R4<double> L = sc.lg_sph[k];
+        double t;
+        if (sphere_t(mk(L.x, L.y, L.z), L.w * L.w, o, d, 0.0, t)) add(sc.lg_id[k]);
+    }
+    const double ia = 1.0 / (d.x * d.x + d.y * d.y + d.z * d.z);
+    light_grid_walk(sc, o, d, [&](uint32_t k, double te, double tx) {
+        const R4<double> L = sc.lg_sph[k];
+        double t;
+        if (sphere_t(mk(L.x, L.y, L.z), L.w * L.w, o, d, 0.0, t)) {
+            const double tc = -((o.x - L.x) * d.x + (o.y - L.y) * d.y + (o.z - L.z) * d.z) * ia;
+            if (tc >= te && tc < tx) add(sc.lg_id[k]);
+        }
+    });
+    if (overflow) return lights_pdf_sum(sc.lights, sc.n_lights, o, d);
+    double acc = 0.0;
+    for (uint32_t q = 0; q < n; ++q) {
+        const R4<double> L = sc.lights[ids[q]];
+        acc = acc + sphere_pdf_value(mk(L.x, L.y, L.z), L.w, o, d);
+    }
+    return acc;
+}
+
 // Light list with quads (DevScene::lref set): HittableList::pdf_value over
 // the mixed list in list order (hittable_list.rs:408-412), reference
 // arithmetic per entry; `li` = the sphere lights (LDS-staged or global).
@@ -821,7 +959,8 @@ __device__ V3<R> tex_colour(const DevScene<R>& sc, uint32_t tid, R u, R v, V3<R>
 // RTW_EXP (profiling builds only, tools/exp_cost.sh): repeat one part of the
 // per-segment work so that the time difference prices it.  1 = closest-hit
 // query, 2 = light pdf sum, 3 = stream seeding, 4 = Lambertian direction
-// sampling, 5 = plane tests.
+// sampling, 5 = plane tests, 6 = closest-hit query along another direction,
+// 7 = light pdf sum along the same direction.
 #ifndef RTW_EXP
 #define RTW_EXP 0
 #endif
@@ -1074,11 +1213,14 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? RTW_WAVES : 1) render
                 }
             }
             if constexpr (kWorld >= kWorldBvh) {
-#if RTW_EXP == 1
+#if RTW_EXP == 1 || RTW_EXP == 6
                 {
+                    // 1: the same query again (warm caches); 6: a query along a
+                    // permuted direction (cold nodes: prices memory latency)
                     R tb2 = tb;
                     int32_t best2 = best;
-                    bvh_closest<kWorld == kWorldBvhLds ? kWorldBvhWW : kWorld, kRobust>(scw, sbase, o, d, tmin, tb2, best2,
+                    const V3<R> d2 = RTW_EXP == 6 ? mk(d.z, d.x, d.y) : d;
+                    bvh_closest<kWorld == kWorldBvhLds ? kWorldBvhWW : kWorld, kRobust>(scw, sbase, o, d2, tmin, tb2, best2,
                                         reinterpret_cast<int32_t*>(smem) + wave * p.stack * 64 + lane, nvis,
                                         ntest, self_s);
                     segs += best2 == -7 ? 1u : 0u;
@@ -1255,13 +1397,16 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? RTW_WAVES : 1) render
                     if (p.sc.lref)
                         acc = lights_pdf_mixed(p.sc, li, pnt, dir);
                     else if constexpr (kLightBvh)
-                        acc = lights_pdf_bvh<kRobust>(p.sc, pnt, dir,
-                                                      reinterpret_cast<int32_t*>(smem) + wave * p.stack * 64 + lane);
+                        acc = p.light_bvh == 2
+                                  ? lights_pdf_grid<kRobust>(p.sc, pnt, dir)
+                                  : lights_pdf_bvh<kRobust>(p.sc, pnt, dir,
+                                                            reinterpret_cast<int32_t*>(smem) + wave * p.stack * 64 + lane);
                     else
                         acc = lights_pdf_sum<kRobust>(li, p.sc.n_lights, pnt, dir);
-#if RTW_EXP == 2
+#if RTW_EXP == 2 || RTW_EXP == 7
+                    // 2: along a permuted direction; 7: the same direction again
                     if constexpr (kLightBvh)
-                        segs += lights_pdf_bvh<kRobust>(p.sc, pnt, mk(dir.y, dir.z, dir.x),
+                        segs += lights_pdf_bvh<kRobust>(p.sc, pnt, RTW_EXP == 7 ? dir : mk(dir.y, dir.z, dir.x),
                                                         reinterpret_cast<int32_t*>(smem) + wave * p.stack * 64 + lane) ==
                                 (R)-7 ? 1u : 0u;
                     else

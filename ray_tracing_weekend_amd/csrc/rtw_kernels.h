@@ -47,6 +47,8 @@ struct alignas(4 * sizeof(R)) R4 {
 //   bvh4     : 8 x n_nodes4 x Bvh4Node<R>      -- RTW_ACCEL_BVH, 4-wide
 //   lbvh     : n_lnodes x BvhNode<R>           -- light pdf query (BVH kernels)
 //   lsph/lid : n_li x R4 {c, r} / u32 in light-BVH leaf order
+//   lg_start : n_cells + 1 x u32                -- light grid (light pdf, long light lists)
+//   lg_sph/lg_id : n_items x R4 {c, r} / u32    -- big list, then each cell's lights
 template <typename R>
 struct BvhNode {
     // two child boxes per node (children tested together, the classic
@@ -90,6 +92,9 @@ struct DevScene {
     const BvhNode<R>* lbvh;           // binary BVH over the light spheres
     const R4<R>* lsph;                // lights {cx, cy, cz, r} in light-BVH leaf order
     const uint32_t* lid;              // light-list index of lsph[k]
+    const uint32_t* lg_start;         // light grid: n_cells + 1 offsets into lg_sph / lg_id
+    const R4<R>* lg_sph;              // light grid items {c, r}: the big list, then cell by cell
+    const uint32_t* lg_id;            // light-list index of lg_sph[k]
     const R* quads;                   // n_quads x kQuadR (see quad layout below)
     const uint32_t* quad_mat;
     const R* lquads;                  // the light list's quads, n_lquads x kQuadR
@@ -110,6 +115,10 @@ struct DevScene {
     uint32_t n_quads, n_lquads, n_list;   // world quads, light quads, light-list length
     uint32_t n_boxes;
     uint32_t light_flags;             // RTW_LIGHTS_BVH_LEAF
+    // light grid (host/bvh.hpp LightGrid): box lo / hi, cell size and its
+    // inverse, cells per axis, big-list length, 1 when staged
+    R lg_lo[3], lg_hi[3], lg_cell[3], lg_inv[3];
+    uint32_t lg_n[3], lg_big, lg_on;
 };
 
 // Plane record, kPlaneR values of precision R: point [0..2], unit normal
@@ -154,7 +163,7 @@ struct KParams {
     uint32_t tiles_x, n_local_tiles, rank, nranks;
     uint32_t n_tasks;                 // n_local_tiles * n_groups
     uint32_t stack;                   // BVH traversal stack entries per lane (LDS)
-    uint32_t light_bvh;               // 1: light pdf through sc.lbvh (BVH kernels only)
+    uint32_t light_bvh;               // light pdf (BVH kernels only): 1 through sc.lbvh, 2 the light grid
     uint32_t xcd;                     // 1: XCD-aware workgroup -> task mapping
     uint32_t item_order;              // 0: pixel-major item pool, 1: sample-major
 };

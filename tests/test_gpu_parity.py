@@ -358,10 +358,12 @@ def test_partial_buffer_cap_grows_the_chunk():
 
 @pytest.mark.parametrize("prec", [rtw.RTW_F64, rtw.RTW_F32])
 def test_light_bvh_equals_linear_light_sum(prec):
-    """The light pdf through the light BVH (tuning light_bvh_min) against the
-    linear loop over the light list (hittable_list.rs:408-412): f64 sums the
-    hit lights in list order, so the images are bit-identical; f32 sums in
-    walk order, so only the path statistics are compared."""
+    """The light pdf through the light BVH and the light grid at several
+    resolutions (tunings light_bvh_min, light_grid) against the linear loop
+    over the light list (hittable_list.rs:408-412): f64 sums the hit lights in
+    list order, so the images are bit-identical (a light counted twice or
+    missed by the grid walk would show); f32 sums in walk order, so only the
+    path statistics are compared."""
     world = rtw.HittableList()
     rng = np.random.default_rng(5)
     lights = rtw.HittableList()
@@ -374,25 +376,32 @@ def test_light_bvh_equals_linear_light_sum(prec):
         else:
             world.add(rtw.Sphere(c, r, rtw.Lambertian(tuple(rng.uniform(0.2, 0.9, 3)))))
     world.add(rtw.Plane((0, 0, 0), (0, 1, 0), rtw.Lambertian((0.5, 0.5, 0.5))))
+    lights.add(rtw.Sphere((1.0, 7.0, -2.0), 3.0))     # spans many grid cells: the grid's big list
     soa = rtw.flatten(world, lights)
     cam = rtw.CameraBuilder().with_image_width(40).with_image_height(24).with_samples_per_pixel(4) \
         .with_max_depth(12).with_lookfrom((8, 3, 8)).with_lookat((0, 0, 0)).with_vfov(45) \
         .with_background((0.7, 0.8, 1.0)).build()
     out = {}
-    for mode, m in (("bvh", 1), ("linear", 1 << 30)):
+    # light BVH (light_grid 0), light grid at 1/16, 1/4 (default) and 16 cells per light, linear loop
+    modes = (("bvh", 1, 0), ("grid1", 1, 1), ("grid", 1, 4), ("grid256", 1, 256), ("linear", 1 << 30, 4))
+    for mode, m, g in modes:
         with rtw.Renderer(device=0, precision=prec) as r:
             r.set_tuning("light_bvh_min", m)
+            r.set_tuning("light_grid", g)
             r.set_scene(soa)
             out[mode] = (r.render(cam, 31), r.stats.segments, r.stats.lambertian)
     if prec == rtw.RTW_F64:
-        assert _same(out["bvh"][0], out["linear"][0]) and out["bvh"][1:] == out["linear"][1:]
+        for mode, _, _ in modes[:-1]:
+            assert _same(out[mode][0], out["linear"][0]) and out[mode][1:] == out["linear"][1:], mode
         ref, st = _render_oracle(soa, cam, 31, 1)
-        mae, exact = _compare_f64(out["bvh"][0], ref, 4)
+        mae, exact = _compare_f64(out["grid"][0], ref, 4)
         assert mae < F64_MAE_TOL and exact > 0.999
     else:
-        a, b = out["bvh"][0], out["linear"][0]
-        ok = ~(np.isnan(a).any(-1) | np.isnan(b).any(-1))
-        assert abs(a[ok].mean() - b[ok].mean()) < 0.02 * b[ok].mean()
+        b = out["linear"][0]
+        for mode, _, _ in modes[:-1]:
+            a = out[mode][0]
+            ok = ~(np.isnan(a).any(-1) | np.isnan(b).any(-1))
+            assert abs(a[ok].mean() - b[ok].mean()) < 0.02 * b[ok].mean(), mode
 
 
 # ---- the large-scene configurations of SURVEY.md §8 (C3: 10k spheres, C5: 1M)
