@@ -17,6 +17,9 @@ import torch  # noqa: E402
 import ray_tracing_weekend_amd as rtw  # noqa: E402
 
 
+BUILD_KEYS = ("bvh_leaf", "light_leaf", "light_grid", "light_bvh_min")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=2)
@@ -47,9 +50,11 @@ def main():
         for c in combos:
             for k, v in zip(keys, c):
                 r.set_tuning(k, v)
-            if "bvh_leaf" in keys and staged.get("leaf") != dict(zip(keys, c))["bvh_leaf"]:
-                r.set_scene(scene)        # the leaf size is a build parameter
-                staged["leaf"] = dict(zip(keys, c))["bvh_leaf"]
+            # leaf sizes and the light grid are built at set_scene
+            build = {k: v for k, v in zip(keys, c) if k in BUILD_KEYS}
+            if build and staged.get("build") != build:
+                r.set_scene(scene)
+                staged["build"] = build
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             r.render_device(cam, 5 + rd, buf.data_ptr(), buf.numel() * buf.element_size())
