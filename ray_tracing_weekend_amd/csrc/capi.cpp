@@ -718,11 +718,13 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
         // binary traversal pushes at most one entry per inner level
         const uint32_t bin_stack = std::max(p.sc.bvh_depth + 1, min_stack);
         const size_t stacks = (size_t)rtw::kWavesPerBlock * 64 * sizeof(int32_t);
-        // kWorldBvhLds layout: stacks | nodes | leaf spheres | ids (padded to 8) | lights
+        // kWorldBvhLds layout: stacks | nodes | leaf spheres | ids (padded to 8) | lights | (f32) light pairs
         const size_t tree_lds = stacks * bin_stack + (size_t)p.sc.n_nodes * sizeof(rtw::BvhNode<R>) +
                                 (size_t)p.sc.n_sph * sizeof(rtw::R4<R>) +
                                 (size_t)((p.sc.n_sph + 7u) & ~7u) * sizeof(uint32_t) +
-                                (size_t)p.sc.n_lights * sizeof(rtw::R4<R>);
+                                (size_t)p.sc.n_lights * sizeof(rtw::R4<R>) +
+                                // f32: the light pairs of the packed light test
+                                (sizeof(R) == 4 ? (size_t)((p.sc.n_lights + 1u) & ~1u) * sizeof(rtw::R4<R>) : 0);
         if (c->bvh_kind == 2 && p.sc.bvh4_stack + 1 <= rtw::kBvhStack) {
             world = rtw::kWorldBvh4;       // 4-wide, when its stack bound fits
             p.stack = std::max(p.sc.bvh4_stack + 1, min_stack);

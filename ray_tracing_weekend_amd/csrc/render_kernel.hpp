@@ -293,6 +293,59 @@ __device__ __forceinline__ float lights_pdf_sum(const R4<float>* __restrict__ li
     return acc;
 }
 
+// The same with pass 1 on packed FP32 (v_pk_fma/mul/add_f32: two lights per
+// instruction).  lp = the light list as pairs, two R4 per pair {x0, x1, y0,
+// y1}, {z0, z1, r0^2, r1^2} (an odd list ends with r^2 = -inf: never hit),
+// staged in LDS; each packed lane does exactly light_hit_f32's operations, so
+// the mask -- and the sum -- are bit-identical to lights_pdf_sum.
+typedef float f2v __attribute__((ext_vector_type(2)));
+template <bool kRobust>
+__device__ __forceinline__ float lights_pdf_sum_pk(const R4<float>* __restrict__ li,
+                                                   const R4<float>* __restrict__ lp, uint32_t n,
+                                                   V3<float> o, V3<float> d) {
+    const float a = len2_f32(d);
+    const float ia = __builtin_amdgcn_rcpf(a);
+    const f2v ox = {o.x, o.x}, oy = {o.y, o.y}, oz = {o.z, o.z};
+    const f2v dx = {d.x, d.x}, dy = {d.y, d.y}, dz = {d.z, d.z};
+    const f2v a2 = {a, a}, ia2 = {ia, ia};
+    float acc = 0.f;
+    for (uint32_t base = 0; base < n; base += 32) {
+        const uint32_t m = min(32u, n - base);
+        uint32_t mask = 0;
+#pragma unroll 2
+        for (uint32_t k = 0; k < m; k += 2) {
+            const R4<float> A = lp[base + k], B = lp[base + k + 1];
+            const f2v fx = ox - f2v{A.x, A.y}, fy = oy - f2v{A.z, A.w}, fz = oz - f2v{B.x, B.y};
+            const f2v r2 = {B.z, B.w};
+            const f2v hb = __builtin_elementwise_fma(dz, fz, __builtin_elementwise_fma(dy, fy, dx * fx));
+            bool h0, h1;
+            if constexpr (kRobust) {
+                const f2v tc = -hb * ia2;
+                const f2v lx = __builtin_elementwise_fma(tc, dx, fx), ly = __builtin_elementwise_fma(tc, dy, fy),
+                          lz = __builtin_elementwise_fma(tc, dz, fz);
+                const f2v l2 = __builtin_elementwise_fma(lx, lx, __builtin_elementwise_fma(ly, ly, lz * lz));
+                const f2v f2 = __builtin_elementwise_fma(fx, fx, __builtin_elementwise_fma(fy, fy, fz * fz));
+                h0 = (l2.x < r2.x) & ((hb.x <= 0.f) | (f2.x <= r2.x));
+                h1 = (l2.y < r2.y) & ((hb.y <= 0.f) | (f2.y <= r2.y));
+            } else {
+                const f2v c = __builtin_elementwise_fma(fx, fx, __builtin_elementwise_fma(fy, fy,
+                                                                __builtin_elementwise_fma(fz, fz, -r2)));
+                const f2v disc = __builtin_elementwise_fma(hb, hb, -(a2 * c));
+                h0 = (disc.x > 0.f) & ((hb.x <= 0.f) | (c.x <= 0.f));
+                h1 = (disc.y > 0.f) & ((hb.y <= 0.f) | (c.y <= 0.f));
+            }
+            mask |= ((h0 ? 1u : 0u) | (h1 ? 2u : 0u)) << k;
+        }
+        while (mask) {
+            const uint32_t k = (uint32_t)__builtin_ctz(mask);
+            mask &= mask - 1u;
+            const R4<float> L = li[base + k];
+            acc += light_pdf_f32(L, o);
+        }
+    }
+    return acc;
+}
+
 // ---------------------------------------------------------------------------
 // BVH closest hit (RTW_ACCEL_BVH).  Box tests only cull; every surviving
 // sphere goes through the same per-sphere arithmetic as the brute-force
@@ -996,6 +1049,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? RTW_WAVES : 1) render
     const R4<R>* __restrict__ sph = kWorld == kWorldLds ? s_sph : p.sc.sph;
     const R4<R>* __restrict__ li = kWorld == kWorldLds ? s_li : p.sc.lights;
     R4<R>* l_li = nullptr;   // kWorldBvhLds: the light list in LDS
+    R4<R>* l_lp = nullptr;   // kWorldBvhLds, f32: the light list as pairs in LDS
     // World view of the closest-hit query.  kWorldBvhLds: the BVH nodes and
     // the leaf-ordered spheres + ids are copied into LDS once per workgroup
     // (after the traversal stacks), so traversal fetches go to the LDS
@@ -1018,6 +1072,18 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? RTW_WAVES : 1) render
         // the light list follows, 32-B aligned (read by the light pdf / sampling)
         l_li = reinterpret_cast<R4<R>*>(l_bid + ((p.sc.n_sph + 7u) & ~7u));
         for (uint32_t k = threadIdx.x; k < p.sc.n_lights; k += kBlock) l_li[k] = p.sc.lights[k];
+        if constexpr (sizeof(R) == 4) {
+            // and again as pairs for the packed light test (lights_pdf_sum_pk)
+            l_lp = l_li + p.sc.n_lights;
+            const uint32_t n = p.sc.n_lights;
+            for (uint32_t q = threadIdx.x; 2 * q < n; q += kBlock) {
+                const R4<R> A = p.sc.lights[2 * q];
+                const bool odd = 2 * q + 1 < n;
+                const R4<R> B = odd ? p.sc.lights[2 * q + 1] : R4<R>{0, 0, 0, 0};
+                l_lp[2 * q] = R4<R>{A.x, B.x, A.y, B.y};
+                l_lp[2 * q + 1] = R4<R>{A.z, B.z, A.w * A.w, odd ? B.w * B.w : (R)-INFINITY};
+            }
+        }
         __syncthreads();
         scw.bvh = l_nodes;
         scw.bsph = l_bsph;
@@ -1401,6 +1467,8 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? RTW_WAVES : 1) render
                                   ? lights_pdf_grid<kRobust>(p.sc, pnt, dir)
                                   : lights_pdf_bvh<kRobust>(p.sc, pnt, dir,
                                                             reinterpret_cast<int32_t*>(smem) + wave * p.stack * 64 + lane);
+                    else if constexpr (kWorld == kWorldBvhLds && sizeof(R) == 4)
+                        acc = lights_pdf_sum_pk<kRobust>(li, l_lp, p.sc.n_lights, pnt, dir);
                     else
                         acc = lights_pdf_sum<kRobust>(li, p.sc.n_lights, pnt, dir);
 #if RTW_EXP == 2 || RTW_EXP == 7
