@@ -1022,7 +1022,10 @@ __device__ V3<R> tex_colour(const DevScene<R>& sc, uint32_t tid, R u, R v, V3<R>
 //   kOptRobust   (f32) closest-approach sphere and light tests (far geometry)
 //   kOptLightBvh (BVH kernels) light pdf through the light BVH (long light lists)
 //   kOptTex      textured materials (DevScene::mat_tex): hit UVs + Texture::get_colour
-enum : int { kOptRobust = 1, kOptLightBvh = 2, kOptTex = 4 };
+//   kOptPrims    quads, transformed cuboids and mixed light lists (DevScene::lref); without
+//                it the kernel is spheres + planes only (the Book-1 scenes) and carries none
+//                of that code -- fewer live registers across the segment loop
+enum : int { kOptRobust = 1, kOptLightBvh = 2, kOptTex = 4, kOptPrims = 8 };
 
 template <typename R, int kWorld, int kOpt>
 // f32: ask for 5 waves per SIMD (<= 96 VGPRs; the kernel fits without
@@ -1035,6 +1038,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? RTW_WAVES : 1) render
     constexpr bool kRobust = (kOpt & kOptRobust) != 0;
     constexpr bool kLightBvh = (kOpt & kOptLightBvh) != 0 && kWorld >= kWorldBvh;
     constexpr bool kTex = (kOpt & kOptTex) != 0;
+    constexpr bool kPrims = (kOpt & kOptPrims) != 0;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     R4<R>* s_sph = reinterpret_cast<R4<R>*>(smem);
     R4<R>* s_li = s_sph + p.sc.n_sph;
@@ -1257,7 +1261,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? RTW_WAVES : 1) render
                 }
             }
             // quads, each behind its own AABB (bounded_hit, hittable.rs:190-196)
-            for (int32_t k = 0; k < nquads; ++k) {
+            for (int32_t k = 0; kPrims && k < nquads; ++k) {
                 R t;
                 const R* Q = p.sc.quads + kQuadR * k;
                 if (aabb_hit_ref(Q + 16, Q + 19, o, d, tmin) && quad_t_hit(Q, o, d, tmin, (R)INFINITY, t) &&
@@ -1267,7 +1271,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? RTW_WAVES : 1) render
                 }
             }
             // transformed cuboids, each behind its world AABB
-            for (int32_t k = 0; k < (int32_t)p.sc.n_boxes; ++k) {
+            for (int32_t k = 0; kPrims && k < (int32_t)p.sc.n_boxes; ++k) {
                 R t;
                 int qd;
                 V3<R> o2, d2;
@@ -1315,7 +1319,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? RTW_WAVES : 1) render
                 bool box_hit = false;
                 bool box_front = false;
                 R hu = (R)0, hv = (R)0;                            // HitRecord u, v (kTex)
-                if (best >= bbase && best < sbase) {
+                if (kPrims && best >= bbase && best < sbase) {
                     // Transformed<Cuboid>: the record of the object-space hit,
                     // its point mapped back (transform_point3d); the normal and
                     // front face stay in object space (transformations.rs:14-29)
@@ -1346,7 +1350,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? RTW_WAVES : 1) render
                     mtype = p.sc.mat_type[m];
                     mp = p.sc.mat_p[m];
                     if constexpr (kTex) plane_uv(pl, pnt, hu, hv);
-                } else if (best < bbase) {
+                } else if (kPrims && best < bbase) {
                     const R* Q = p.sc.quads + kQuadR * (best - nplanes);
                     outward = q3(Q, 12);                           // quadrilateral.rs:97
                     m = p.sc.quad_mat[best - nplanes];
@@ -1427,7 +1431,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? RTW_WAVES : 1) render
                             // at its next world query, as in the oracle
                             atomicAdd(p.counters + 5, 1ull);
                             dir = mk((R)NAN, (R)NAN, (R)NAN);
-                        } else if (p.sc.lref) {
+                        } else if (kPrims && p.sc.lref) {
                             const uint32_t ref = p.sc.lref[g.index(p.sc.n_list)];
                             if (ref & kLrefQuad) {
                                 dir = quad_random(p.sc.lquads + kQuadR * (ref & 0x3fffffffu), pnt, g);
@@ -1460,7 +1464,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? RTW_WAVES : 1) render
                     const V3<R> ndir = PR::normalize(dir);
                     const R cos_w = PR::over_pi(dot(ndir, uvw.w));
                     R acc;                                                // hittable_list.rs:408-412
-                    if (p.sc.lref)
+                    if (kPrims && p.sc.lref)
                         acc = lights_pdf_mixed(p.sc, li, pnt, dir);
                     else if constexpr (kLightBvh)
                         acc = p.light_bvh == 2
@@ -1638,7 +1642,10 @@ inline int launch_render_impl(const KParams<R>& p, int world, size_t lds_bytes, 
     if (blocks) {
         const bool robust = sizeof(R) == 4 && p.sc.robust;
         const bool lbvh = p.light_bvh != 0;
-        constexpr int T = dev::kOptTex;
+        // kOptPrims: always for textured and f64 kernels; the f32 Book-1
+        // kernels go without when the scene has no quads, cuboids or mixed list
+        const bool prims = p.sc.n_quads || p.sc.n_boxes || p.sc.lref;
+        constexpr int T = dev::kOptTex | dev::kOptPrims, Pr = dev::kOptPrims;
         if (p.sc.mat_tex) {
             if constexpr (sizeof(R) == 4) {
                 if (robust && lbvh) launch_world<R, T | dev::kOptRobust | dev::kOptLightBvh>(p, world, lds_bytes, blocks, stream);
@@ -1650,14 +1657,22 @@ inline int launch_render_impl(const KParams<R>& p, int world, size_t lds_bytes, 
                 else launch_world<R, T>(p, world, lds_bytes, blocks, stream);
             }
         } else if constexpr (sizeof(R) == 4) {
-            if (robust && lbvh) launch_world<R, dev::kOptRobust | dev::kOptLightBvh>(p, world, lds_bytes, blocks, stream);
-            else if (robust) launch_world<R, dev::kOptRobust>(p, world, lds_bytes, blocks, stream);
-            else if (lbvh) launch_world<R, dev::kOptLightBvh>(p, world, lds_bytes, blocks, stream);
-            else launch_world<R, 0>(p, world, lds_bytes, blocks, stream);
+            if (prims) {
+                if (robust && lbvh) launch_world<R, Pr | dev::kOptRobust | dev::kOptLightBvh>(p, world, lds_bytes, blocks, stream);
+                else if (robust) launch_world<R, Pr | dev::kOptRobust>(p, world, lds_bytes, blocks, stream);
+                else if (lbvh) launch_world<R, Pr | dev::kOptLightBvh>(p, world, lds_bytes, blocks, stream);
+                else launch_world<R, Pr>(p, world, lds_bytes, blocks, stream);
+            } else {
+                if (robust && lbvh) launch_world<R, dev::kOptRobust | dev::kOptLightBvh>(p, world, lds_bytes, blocks, stream);
+                else if (robust) launch_world<R, dev::kOptRobust>(p, world, lds_bytes, blocks, stream);
+                else if (lbvh) launch_world<R, dev::kOptLightBvh>(p, world, lds_bytes, blocks, stream);
+                else launch_world<R, 0>(p, world, lds_bytes, blocks, stream);
+            }
         } else {
             (void)robust;
-            if (lbvh) launch_world<R, dev::kOptLightBvh>(p, world, lds_bytes, blocks, stream);
-            else launch_world<R, 0>(p, world, lds_bytes, blocks, stream);
+            (void)prims;
+            if (lbvh) launch_world<R, Pr | dev::kOptLightBvh>(p, world, lds_bytes, blocks, stream);
+            else launch_world<R, Pr>(p, world, lds_bytes, blocks, stream);
         }
         if (hipGetLastError() != hipSuccess) return -1;
     }
