@@ -1,0 +1,96 @@
+// light_grid.hpp -- the light grid's cell walk (the light pdf's all-hits
+// query over long light lists, render_kernel.hpp lights_pdf_grid).  Host +
+// device: tests/native/grid_walk_check.cpp runs the f64 instance on the CPU
+// against a brute-force sweep (every hit light counted exactly once).
+#pragma once
+
+#include <math.h>
+#include <stdint.h>
+
+#include "rtw_device.hpp"
+#include "rtw_kernels.h"
+
+namespace rtw {
+namespace dev {
+
+// 1 / x as the render kernels compute it (f32: the hardware reciprocal)
+__host__ __device__ inline double grid_inv(double x) { return 1.0 / x; }
+__device__ inline float grid_inv(float x) { return __builtin_amdgcn_rcpf(x); }
+
+// Light pdf through the light grid (KParams::light_bvh == 2; host/bvh.hpp
+// LightGrid): a 3-D DDA walks the cells the ray (o, d), t in [0, inf), crosses
+// and calls item(k, te, tx) for every light listed in a cell, with [te, tx)
+// the ray-parameter interval the walk assigns to that cell.  The intervals
+// partition the real line (the first starts at -inf, the last ends at +inf,
+// each ends where the next starts, never decreasing), so a light counted only
+// where its closest-approach parameter falls is counted at most once however
+// the walk rounds; the host pads every light's cell range by more than that
+// rounding, so a hit light is counted exactly once.  (Fetching the next
+// cells' ranges ahead of the tests measured slower: C5 +3 % to +15 % time.)
+template <typename R, typename Item>
+__host__ __device__ inline void light_grid_walk(const DevScene<R>& sc, V3<R> o, V3<R> d, Item&& item) {
+    const R kInf = (R)INFINITY;
+    const R ix = grid_inv(d.x), iy = grid_inv(d.y), iz = grid_inv(d.z);
+    R tn, tf;
+    {
+        const R x0 = (sc.lg_lo[0] - o.x) * ix, x1 = (sc.lg_hi[0] - o.x) * ix;
+        const R y0 = (sc.lg_lo[1] - o.y) * iy, y1 = (sc.lg_hi[1] - o.y) * iy;
+        const R z0 = (sc.lg_lo[2] - o.z) * iz, z1 = (sc.lg_hi[2] - o.z) * iz;
+        tn = fmax(fmax(fmin(x0, x1), fmin(y0, y1)), fmax(fmin(z0, z1), (R)0));
+        tf = fmin(fmax(x0, x1), fmin(fmax(y0, y1), fmax(z0, z1)));
+    }
+    if (!(tn <= tf)) return;
+    const int nx = (int)sc.lg_n[0], ny = (int)sc.lg_n[1], nz = (int)sc.lg_n[2];
+    // the entry cell (clamped; NaN -> 0)
+    auto cell_of = [&](R oc, R dc, R lo, R inv, int n) {
+        return (int)fmin(fmax((oc + tn * dc - lo) * inv, (R)0), (R)(n - 1));
+    };
+    int cx = cell_of(o.x, d.x, sc.lg_lo[0], sc.lg_inv[0], nx);
+    int cy = cell_of(o.y, d.y, sc.lg_lo[1], sc.lg_inv[1], ny);
+    int cz = cell_of(o.z, d.z, sc.lg_lo[2], sc.lg_inv[2], nz);
+    const int sx = d.x > 0 ? 1 : (d.x < 0 ? -1 : 0);
+    const int sy = d.y > 0 ? 1 : (d.y < 0 ? -1 : 0);
+    const int sz = d.z > 0 ? 1 : (d.z < 0 ? -1 : 0);
+    R te = -kInf;
+    // where the ray leaves cell c along one axis (+inf: never), not before te
+    auto exit_t = [&](int c, int s, R lo, R cell, R oc, R inv) {
+        return s == 0 ? kInf : fmax((lo + (R)(c + (s > 0 ? 1 : 0)) * cell - oc) * inv, te);
+    };
+    R tmx = exit_t(cx, sx, sc.lg_lo[0], sc.lg_cell[0], o.x, ix);
+    R tmy = exit_t(cy, sy, sc.lg_lo[1], sc.lg_cell[1], o.y, iy);
+    R tmz = exit_t(cz, sz, sc.lg_lo[2], sc.lg_cell[2], o.z, iz);
+    uint32_t c = (uint32_t)((cz * ny + cy) * nx + cx);
+    for (;;) {
+        int axis, ni, nn;
+        R tx;
+        if (tmx <= tmy && tmx <= tmz) {
+            axis = 0; tx = tmx; ni = cx + sx; nn = nx;
+        } else if (tmy <= tmz) {
+            axis = 1; tx = tmy; ni = cy + sy; nn = ny;
+        } else {
+            axis = 2; tx = tmz; ni = cz + sz; nn = nz;
+        }
+        const bool last = !(tx < kInf) || ni < 0 || ni >= nn;
+        if (last) tx = kInf;
+        const uint32_t b = sc.lg_start[c], e = sc.lg_start[c + 1];
+        for (uint32_t k = b; k < e; ++k) item(k, te, tx);
+        if (last) break;
+        te = tx;
+        if (axis == 0) {
+            cx = ni;
+            c += sx;
+            tmx = exit_t(cx, sx, sc.lg_lo[0], sc.lg_cell[0], o.x, ix);
+        } else if (axis == 1) {
+            cy = ni;
+            c += sy * nx;
+            tmy = exit_t(cy, sy, sc.lg_lo[1], sc.lg_cell[1], o.y, iy);
+        } else {
+            cz = ni;
+            c += sz * nx * ny;
+            tmz = exit_t(cz, sz, sc.lg_lo[2], sc.lg_cell[2], o.z, iz);
+        }
+    }
+}
+
+}  // namespace dev
+}  // namespace rtw

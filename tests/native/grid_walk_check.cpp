@@ -1,0 +1,124 @@
+// grid_walk_check.cpp -- CPU check of the light grid (host/bvh.cpp
+// build_light_grid + light_grid.hpp light_grid_walk, the f64 instance the
+// parity kernels run): for random light sets and random rays, the walk's
+// closest-approach rule must count every light the ray hits exactly once and
+// no light twice.  Built and run by tests/test_light_grid_host.py:
+//   hipcc -x hip --cuda-host-only -O2 -std=c++17 -I<csrc> -I<include> \
+//       grid_walk_check.cpp <csrc>/host/bvh.cpp -o grid_walk_check
+#include <stdio.h>
+
+#include <random>
+#include <vector>
+
+#include "host/bvh.hpp"
+#include "light_grid.hpp"
+
+using rtw::R4;
+using V = rtw::dev::V3<double>;
+
+// ray t >= 0 vs sphere: -1 miss, 1 hit, 0 too close to tangent to call
+static int hit_class(const double* L, V o, V d) {
+    const double fx = o.x - L[0], fy = o.y - L[1], fz = o.z - L[2];
+    const double a = d.x * d.x + d.y * d.y + d.z * d.z;
+    const double hb = d.x * fx + d.y * fy + d.z * fz;
+    const double c = fx * fx + fy * fy + fz * fz - L[3] * L[3];
+    const double disc = hb * hb - a * c;
+    const double scale = hb * hb + fabs(a * c) + 1e-300;
+    if (disc < -1e-9 * scale) return -1;
+    if (disc < 1e-9 * scale) return 0;
+    const double far = (-hb + sqrt(disc)) / a;
+    if (far < -1e-9 * (fabs(hb) / a + 1.0)) return -1;
+    if (far < 1e-9 * (fabs(hb) / a + 1.0)) return 0;
+    return 1;
+}
+
+int main() {
+    std::mt19937_64 rng(12345);
+    std::uniform_real_distribution<double> U(0.0, 1.0);
+    long checked = 0, hits = 0, bad = 0;
+    for (int scene = 0; scene < 6; ++scene) {
+        // 0: a field of small lights in a thin layer + one large light (the
+        // scenes::simple shape); 1: random sizes in a box; 2: coincident
+        // centres and zero radii; 3: a few lights; 4: one huge light among
+        // small ones; 5: non-finite entries
+        const uint32_t n = scene == 3 ? 5 : 2000;
+        std::vector<double> L(4 * n);
+        for (uint32_t k = 0; k < n; ++k) {
+            double* l = &L[4 * k];
+            switch (scene) {
+            case 0: l[0] = -50 + 100 * U(rng); l[1] = 0.2; l[2] = -50 + 100 * U(rng); l[3] = 0.2; break;
+            case 1: for (int a = 0; a < 3; ++a) l[a] = -10 + 20 * U(rng); l[3] = 0.05 + 0.5 * U(rng); break;
+            case 2: l[0] = (k % 7) * 0.5; l[1] = 1.0; l[2] = (k % 3) * 0.5; l[3] = (k % 5) ? 0.3 : 0.0; break;
+            case 3: for (int a = 0; a < 3; ++a) l[a] = -3 + 6 * U(rng); l[3] = 0.5 + U(rng); break;
+            case 4: for (int a = 0; a < 3; ++a) l[a] = -20 + 40 * U(rng); l[3] = 0.1 + 0.2 * U(rng); break;
+            default: for (int a = 0; a < 3; ++a) l[a] = -5 + 10 * U(rng); l[3] = 0.2 + 0.3 * U(rng); break;
+            }
+            if (scene == 1 && k % 9 == 0) l[3] = -l[3];   // negative radius: same ball
+        }
+        if (scene == 0) { L[0] = 0; L[1] = 1; L[2] = 0; L[3] = 1.0; }
+        if (scene == 4) { L[4] = 0; L[5] = 0; L[6] = 0; L[7] = 30.0; }
+        if (scene == 5) { L[3] = INFINITY; L[4 * 7 + 1] = NAN; }
+        for (double density : {1.0 / 16, 0.25, 2.0, 16.0}) {
+            const rtw::LightGrid g = rtw::build_light_grid(L.data(), n, density);
+            std::vector<R4<double>> items(g.items.size());
+            for (size_t q = 0; q < g.items.size(); ++q) {
+                const double* l = &L[4 * g.items[q]];
+                items[q] = R4<double>{l[0], l[1], l[2], l[3]};
+            }
+            rtw::DevScene<double> sc{};
+            sc.lg_start = g.start.data();
+            sc.lg_sph = items.data();
+            sc.lg_id = g.items.data();
+            for (int a = 0; a < 3; ++a) {
+                sc.lg_lo[a] = g.lo[a];
+                sc.lg_hi[a] = g.lo[a] + g.n[a] * g.cell[a];
+                sc.lg_cell[a] = g.cell[a];
+                sc.lg_inv[a] = 1.0 / g.cell[a];
+                sc.lg_n[a] = g.n[a];
+            }
+            sc.lg_big = g.n_big;
+            std::vector<int> count(n);
+            for (int r = 0; r < 3000; ++r) {
+                // origins on or near light surfaces and in the open; grazing
+                // and axis-aligned directions included
+                V o, d;
+                const uint32_t t = (uint32_t)(U(rng) * n);
+                const double* lt = &L[4 * t];
+                if (r % 3 == 0 && std::isfinite(lt[0] + lt[1] + lt[2] + lt[3])) {
+                    o = V{lt[0] + lt[3], lt[1], lt[2]};
+                } else {
+                    o = V{-60 + 120 * U(rng), -1 + 4 * U(rng), -60 + 120 * U(rng)};
+                }
+                if (r % 5 == 0) {
+                    const double* tg = &L[4 * (uint32_t)(U(rng) * n)];
+                    d = V{tg[0] - o.x, tg[1] - o.y, tg[2] - o.z};
+                } else {
+                    d = V{-1 + 2 * U(rng), (-1 + 2 * U(rng)) * (r % 2 ? 0.01 : 1.0), -1 + 2 * U(rng)};
+                }
+                if (r % 17 == 0) d = V{1, 0, 0};
+                if (r % 19 == 0) d = V{0, 0, -2};
+                if (!std::isfinite(d.x + d.y + d.z)) continue;   // aimed at a NaN light
+                std::fill(count.begin(), count.end(), 0);
+                for (uint32_t q = 0; q < g.n_big; ++q) ++count[g.items[q]];
+                const double ia = 1.0 / (d.x * d.x + d.y * d.y + d.z * d.z);
+                rtw::dev::light_grid_walk(sc, o, d, [&](uint32_t q, double te, double tx) {
+                    const R4<double>& l = items[q];
+                    const double tc = -((o.x - l.x) * d.x + (o.y - l.y) * d.y + (o.z - l.z) * d.z) * ia;
+                    if (tc >= te && tc < tx && hit_class(&L[4 * g.items[q]], o, d) >= 0) ++count[g.items[q]];
+                });
+                for (uint32_t k = 0; k < n; ++k) {
+                    const int h = hit_class(&L[4 * k], o, d);
+                    ++checked;
+                    if (h == 1) ++hits;
+                    const bool ok = count[k] <= 1 && (h != 1 || count[k] == 1);
+                    if (!ok && bad < 10)
+                        printf("scene %d density %g ray %d light %u: counted %d, hit class %d\n", scene, density, r,
+                               k, count[k], h);
+                    bad += ok ? 0 : 1;
+                }
+            }
+        }
+    }
+    printf("checked %ld (ray, light) pairs, %ld hits, %ld wrong\n", checked, hits, bad);
+    return bad == 0 && hits > 1000 ? 0 : 1;
+}
