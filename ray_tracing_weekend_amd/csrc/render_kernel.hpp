@@ -1404,9 +1404,11 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? RTW_WAVES : 1) render
 #if RTW_EXP == 2 || RTW_EXP == 7
                     // 2: along a permuted direction; 7: the same direction again
                     if constexpr (kLightBvh)
-                        segs += lights_pdf_bvh<kRobust>(p.sc, pnt, RTW_EXP == 7 ? dir : mk(dir.y, dir.z, dir.x),
-                                                        reinterpret_cast<int32_t*>(smem) + wave * p.stack * 64 + lane) ==
-                                (R)-7 ? 1u : 0u;
+                        segs += (p.light_bvh == 2
+                                     ? lights_pdf_grid<kRobust>(p.sc, pnt, RTW_EXP == 7 ? dir : mk(dir.y, dir.z, dir.x))
+                                     : lights_pdf_bvh<kRobust>(p.sc, pnt, RTW_EXP == 7 ? dir : mk(dir.y, dir.z, dir.x),
+                                                               reinterpret_cast<int32_t*>(smem) + wave * p.stack * 64 +
+                                                                   lane)) == (R)-7 ? 1u : 0u;
                     else
                         segs += lights_pdf_sum<kRobust>(li, p.sc.n_lights, pnt, mk(dir.y, dir.z, dir.x)) == (R)-7 ? 1u : 0u;
 #endif
