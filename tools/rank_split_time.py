@@ -1,0 +1,57 @@
+#!/usr/bin/env python3
+"""Per-rank render time of the C2 headline split over N ranks, measured on ONE
+GPU (each rank's share rendered in turn with rtw_render_device(rank, nranks)):
+the compute part of the strong-scaling curve the driver's N-GPU bench measures
+(it adds the barrier and the one RCCL gather).  Prints one JSON line per N.
+
+    python tools/rank_split_time.py [--ns 1,2,4,8] [--reps 3]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+import ray_tracing_weekend_amd as rtw  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ns", default="1,2,4,8")
+    ap.add_argument("--reps", type=int, default=3)
+    a = ap.parse_args()
+    W, H, SPP = 1200, 800, 500
+    scene, b = rtw.scenes.simple_soa()
+    cam = b.with_image_width(W).with_image_height(H).with_samples_per_pixel(SPP).with_max_depth(50).build()
+    r = rtw.Renderer(precision=rtw.RTW_F32)
+    r.set_scene(scene)
+    buf = torch.empty((H, W, 3), dtype=torch.float32, device="cuda:0")
+    r.render_device(cam, 1, buf.data_ptr(), buf.numel() * 4)     # warm-up
+    torch.cuda.synchronize()
+    base = None
+    for n in (int(x) for x in a.ns.split(",")):
+        per_rank = []
+        for rank in range(n):
+            best = float("inf")
+            for _ in range(a.reps):
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                r.render_device(cam, 7, buf.data_ptr(), buf.numel() * 4, rank=rank, nranks=n)
+                torch.cuda.synchronize()
+                best = min(best, time.perf_counter() - t0)
+            per_rank.append(best * 1e3)
+        slowest = max(per_rank)
+        base = base or slowest
+        print(json.dumps({"nranks": n, "max_rank_ms": round(slowest, 2), "min_rank_ms": round(min(per_rank), 2),
+                          "speedup_vs_1": round(base / slowest, 2),
+                          "msamples_s_if_parallel": round(W * H * SPP / (slowest * 1e-3) / 1e6, 1)}), flush=True)
+    r.close()
+
+
+if __name__ == "__main__":
+    main()
