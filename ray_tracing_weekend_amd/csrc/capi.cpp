@@ -26,7 +26,8 @@ struct rtw_ctx {
                                   // sample-by-sample fold exactly
     size_t partial_max = (size_t)8 << 30;   // cap of the chunk-sum buffer (auto chunk grows)
     uint32_t group = 0;           // chunks per wave task (0 = from target_tasks)
-    uint64_t target_tasks = 1u << 18;
+    uint64_t target_tasks = 1u << 17;   // auto chunks-per-task: about this many tasks,
+                                        // at most kMaxAutoGroup chunks per task
     int world_pref = 1;           // 1: LDS-staged sphere list when it fits, 0: global
     int auto_accel = RTW_ACCEL_AUTO;    // RTW_ACCEL_AUTO resolves to this (AUTO: by scene size)
     int bvh_kind = 3;             // BVH traversal: 3 = binary while-while + leaf postponing on the
@@ -38,6 +39,8 @@ struct rtw_ctx {
     double scene_extent = 0.0, min_radius = 0.0;   // of the staged scene (robust = 2)
     uint32_t bvh_leaf = 0;            // spheres per BVH leaf (set before rtw_set_scene); 0 = auto:
                                       // 4, or 8 for scenes of >= 100k spheres (C5: +12 %)
+    uint32_t persist = 2048;          // workgroups of persistent waves (tasks from a counter);
+                                      // 0: one task per wave (then "xcd" maps blocks to tasks)
     uint32_t light_leaf = 0;          // light spheres per light-BVH leaf; 0 = 4
     uint32_t light_grid = 4;          // light pdf through the light grid at light_grid / 16
                                       // cells per light (set before rtw_set_scene); 0: light BVH
@@ -64,7 +67,7 @@ struct rtw_ctx {
     size_t partial_cap = 0;
     void* d_out = nullptr;
     size_t out_cap = 0;
-    static constexpr int kCounters = 6;   // rtw_kernels.h KParams::counters
+    static constexpr int kCounters = 7;   // rtw_kernels.h KParams::counters
     unsigned long long* d_counters = nullptr;
     std::vector<unsigned char> h_out;
     rtw_stats last{};
@@ -672,14 +675,21 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
     p.n_chunks = p.spp ? (p.spp + chunk - 1) / chunk : 0;
     uint32_t group = c->group;
     if (group == 0) {
+        // ~2^17 tasks: at one GPU (C2: 15k tiles) that caps at kMaxAutoGroup;
+        // a rank's share of a split render (C2 / 8 ranks: 1.9k tiles) gets 8
+        // chunks per task instead of the 4 a fixed 2^18 tasks gave -- that
+        // share measured 15.6 -> 12.7 ms (per-wave tail vs launch tail)
+        constexpr uint32_t kMaxAutoGroup = 32;
         const uint64_t n_groups = p.n_local_tiles ? (c->target_tasks + p.n_local_tiles - 1) / p.n_local_tiles : 1;
         group = (uint32_t)((p.n_chunks + n_groups - 1) / std::max<uint64_t>(n_groups, 1));
+        group = std::min(group, kMaxAutoGroup);
     }
     p.group = std::max<uint32_t>(1, std::min<uint32_t>(group, std::max<uint32_t>(p.n_chunks, 1)));
     p.n_groups = p.n_chunks ? (p.n_chunks + p.group - 1) / p.group : 0;
     p.n_tasks = p.n_local_tiles * p.n_groups;
     p.xcd = c->xcd;
     p.item_order = c->item_order;
+    p.persist = c->persist;
     const size_t partial_bytes = std::max<size_t>((size_t)p.n_chunks * p.n_local_tiles * 64 * 3 * sizeof(R), 64);
     int rc = ensure(c, &c->d_partial, &c->partial_cap, partial_bytes);
     if (rc) return rc;
@@ -841,6 +851,7 @@ int rtw_set_tuning(rtw_ctx* c, const char* key, int64_t value) {
     else if (k == "robust") c->robust = (int)std::min<int64_t>(value, 2);
     else if (k == "bvh_leaf") c->bvh_leaf = (uint32_t)std::min<int64_t>(value, 15);
     else if (k == "light_leaf") c->light_leaf = (uint32_t)std::min<int64_t>(value, 15);
+    else if (k == "persist") c->persist = (uint32_t)std::min<int64_t>(value, 1 << 20);
     else if (k == "light_grid") c->light_grid = (uint32_t)std::min<int64_t>(value, 1024);
     else if (k == "xcd") c->xcd = (uint32_t)std::min<int64_t>(value, 2);
     else if (k == "item_order") c->item_order = value ? 1u : 0u;

@@ -1032,9 +1032,28 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? RTW_WAVES : 1) render
     // p.xcd == 2: XCD x = blockIdx % 8 takes the tile rows tr = x (mod 8) --
     // every XCD still samples the whole image (balanced, like the multi-GPU
     // interleave), and all tasks of a tile, and of its row, share one L2.
+    // the wave's current task (wave-uniform): tile lt at (tx, ty), chunks
+    // [c_begin, c_begin + glen), a pool of n_items (pixel, chunk) items
+    uint32_t lt = 0, tx = 0, ty = 0, c_begin = 0, glen = 0, n_items = 0;
+    auto set_task = [&](uint32_t t) {
+        lt = t / p.n_groups;
+        const uint32_t cg = t - lt * p.n_groups;
+        const uint32_t tr = lt / p.tiles_x;
+        tx = lt - tr * p.tiles_x;
+        ty = tr * p.nranks + p.rank;
+        c_begin = cg * p.group;
+        glen = min(c_begin + p.group, p.n_chunks) - c_begin;
+        n_items = 64u * glen;
+    };
+    // p.persist: every wave takes tasks from a global counter until none are
+    // left, and its lanes move on to the next task's items while others still
+    // finish the last one -- no per-task drain, one workgroup setup (LDS
+    // staging) per resident workgroup.  Else one task per wave (static map).
+    bool more = p.persist != 0;       // wave-uniform: the counter may hold tasks
     uint32_t blk = blockIdx.x;
-    uint32_t task;
-    if (p.xcd == 2) {
+    uint32_t task = 0;
+    if (p.persist) {
+    } else if (p.xcd == 2) {
         const uint32_t x = blk & 7u, k = blk >> 3;
         const uint32_t per_row = p.tiles_x * p.n_groups;          // tasks of one tile row
         const uint32_t ltr = p.n_local_tiles / p.tiles_x;          // this rank's tile rows
@@ -1052,16 +1071,10 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? RTW_WAVES : 1) render
         }
         task = blk * kWavesPerBlock + wave;
     }
-    if (task >= p.n_tasks) return;
-    const uint32_t lt = task / p.n_groups;
-    const uint32_t cg = task - lt * p.n_groups;
-    const uint32_t tr = lt / p.tiles_x;
-    const uint32_t tx = lt - tr * p.tiles_x;
-    const uint32_t ty = tr * p.nranks + p.rank;
-    const uint32_t c_begin = cg * p.group;
-    const uint32_t c_end = min(c_begin + p.group, p.n_chunks);
-    const uint32_t glen = c_end - c_begin;
-    const uint32_t n_items = 64u * glen;
+    if (!p.persist) {
+        if (task >= p.n_tasks) return;
+        set_task(task);
+    }
     // item q -> (pixel px, chunk c): pixel-major (p.item_order 0: q = chunk
     // offset * 64 + px -- the 64 lanes start on the tile's 64 pixels) or
     // sample-major (1: q = px * glen + chunk offset -- the lanes start on a
@@ -1089,8 +1102,9 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? RTW_WAVES : 1) render
 
     // per-lane item state
     uint32_t q = lane;            // item index in the task's pool
-    uint32_t next_q = 64;         // wave-uniform: first unassigned item
+    uint32_t next_q = 0;          // wave-uniform: first unassigned item
     uint32_t px = 0, i = 0, j = 0, c = 0, s = 0, s_end = 0;
+    uint32_t my_lt = 0;           // local tile of the lane's item
     uint64_t pix = 0;
     V3<R> part = zero;            // fold(Colour::default(), +) of the item's samples
     Rng g;
@@ -1118,11 +1132,29 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? RTW_WAVES : 1) render
         depth = p.max_depth;
         self_s = -1;
     };
-    // Give every lane that needs one a valid item (or none: pool drained).
+    // Give every lane that needs one a valid item: from the current pool, then
+    // (p.persist) from the next task's; none once no task is left.
     auto acquire = [&]() {
         for (;;) {
             const uint64_t want = __ballot(need);
             if (want == 0) break;
+            if (next_q >= n_items) {
+                uint32_t t = 0xffffffffu;
+                if (more) {
+                    const uint64_t live = __ballot(true);
+                    const uint32_t leader = (uint32_t)__builtin_ctzll(live);
+                    if (lane == leader) t = (uint32_t)atomicAdd(p.counters + 6, 1ull);
+                    t = (uint32_t)__shfl((int)t, (int)leader);
+                }
+                if (t >= p.n_tasks) {   // every task is taken: these lanes are done
+                    more = false;
+                    need = false;
+                    break;
+                }
+                set_task(t);
+                next_q = 0;
+                continue;
+            }
             if (need) {
                 const uint32_t below = __builtin_amdgcn_mbcnt_hi(
                     (uint32_t)(want >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)want, 0u));
@@ -1132,6 +1164,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? RTW_WAVES : 1) render
                     i = tx * kTile + (px & 7u);
                     j = ty * kTile + (px >> 3);
                     if (i < p.W && j < p.H) {
+                        my_lt = lt;
                         pix = (uint64_t)j * p.W + i;
                         s = c * p.chunk;
                         s_end = min(s + p.chunk, p.spp);
@@ -1140,27 +1173,12 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? RTW_WAVES : 1) render
                         need = false;
                         start_sample();
                     }
-                } else {
-                    need = false;
                 }
             }
             next_q += (uint32_t)__popcll(want);
         }
     };
-    // the first 64 items go to lanes 0..63 in order
-    need = false;
-    decode(lane, px, c);
-    i = tx * kTile + (px & 7u);
-    j = ty * kTile + (px >> 3);
-    if (i < p.W && j < p.H) {
-        pix = (uint64_t)j * p.W + i;
-        s = c * p.chunk;
-        s_end = min(s + p.chunk, p.spp);
-        active = true;
-        start_sample();
-    } else {
-        need = true;
-    }
+    // the first 64 items of the first task go to lanes 0..63 in order
     acquire();
 
     while (__ballot(active) != 0) {
@@ -1450,7 +1468,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? RTW_WAVES : 1) render
 #endif
                     start_sample();
                 } else {
-                    R* dst = p.partial + (((size_t)c * p.n_local_tiles + lt) * 64 + px) * 3;
+                    R* dst = p.partial + (((size_t)c * p.n_local_tiles + my_lt) * 64 + px) * 3;
                     dst[0] = part.x;
                     dst[1] = part.y;
                     dst[2] = part.z;
@@ -1561,7 +1579,9 @@ template <typename R>
 inline int launch_render_impl(const KParams<R>& p, int world, size_t lds_bytes, R* out,
                               hipStream_t stream, hipEvent_t mid) {
     uint32_t blocks = (p.n_tasks + kWavesPerBlock - 1) / kWavesPerBlock;
-    if (p.xcd == 2 && p.tiles_x) {
+    if (p.persist) {
+        blocks = blocks < p.persist ? blocks : p.persist;   // resident-size grid, tasks from the counter
+    } else if (p.xcd == 2 && p.tiles_x) {
         // 8 XCD lanes of blocks, each as long as the longest XCD task list
         const uint32_t ltr = p.n_local_tiles / p.tiles_x;
         const uint32_t longest = (ltr + 7u) / 8u * p.tiles_x * p.n_groups;

@@ -152,7 +152,8 @@ struct KParams {
     DevScene<R> sc;
     R* partial;                       // [n_chunks][n_local_tiles][64][3] item (chunk) sums
     unsigned long long* counters;     // [0] segments, [1] lambertian, [2] node visits,
-                                      // [3] sphere tests, [4] plane-UV panics, [5] empty-light panics
+                                      // [3] sphere tests, [4] plane-UV panics, [5] empty-light panics,
+                                      // [6] next task (persistent waves)
     R center[3], p00[3], du[3], dv[3], disk_u[3], disk_v[3], bg[3];
     R u_scale;                        // Uniform::new_inclusive(-0.5, 0.5) scale
     uint64_t seed;
@@ -166,6 +167,8 @@ struct KParams {
     uint32_t light_bvh;               // light pdf (BVH kernels only): 1 through sc.lbvh, 2 the light grid
     uint32_t xcd;                     // 1: XCD-aware workgroup -> task mapping
     uint32_t item_order;              // 0: pixel-major item pool, 1: sample-major
+    uint32_t persist;                 // > 0: workgroups launched (waves take tasks from
+                                      // counters[6]); 0: one task per wave
 };
 
 // Host-side launch helpers (defined in render_f32.hip / render_f64.hip).

@@ -24,18 +24,22 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ns", default="1,2,4,8")
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--tuning", default="", help="k=v,... (rtw_set_tuning)")
     a = ap.parse_args()
     W, H, SPP = 1200, 800, 500
     scene, b = rtw.scenes.simple_soa()
     cam = b.with_image_width(W).with_image_height(H).with_samples_per_pixel(SPP).with_max_depth(50).build()
     r = rtw.Renderer(precision=rtw.RTW_F32)
+    for kv in filter(None, a.tuning.split(",")):
+        k, v = kv.split("=")
+        r.set_tuning(k, int(v))
     r.set_scene(scene)
     buf = torch.empty((H, W, 3), dtype=torch.float32, device="cuda:0")
     r.render_device(cam, 1, buf.data_ptr(), buf.numel() * 4)     # warm-up
     torch.cuda.synchronize()
     base = None
     for n in (int(x) for x in a.ns.split(",")):
-        per_rank = []
+        per_rank, kern = [], []
         for rank in range(n):
             best = float("inf")
             for _ in range(a.reps):
@@ -44,12 +48,14 @@ def main():
                 r.render_device(cam, 7, buf.data_ptr(), buf.numel() * 4, rank=rank, nranks=n)
                 torch.cuda.synchronize()
                 best = min(best, time.perf_counter() - t0)
+            kern.append(min(r.get_timings(a.reps)[1]))
             per_rank.append(best * 1e3)
         slowest = max(per_rank)
         base = base or slowest
-        print(json.dumps({"nranks": n, "max_rank_ms": round(slowest, 2), "min_rank_ms": round(min(per_rank), 2),
-                          "speedup_vs_1": round(base / slowest, 2),
-                          "msamples_s_if_parallel": round(W * H * SPP / (slowest * 1e-3) / 1e6, 1)}), flush=True)
+        print(json.dumps({"tuning": a.tuning, "nranks": n, "max_rank_ms": round(slowest, 2), "min_rank_ms": round(min(per_rank), 2),
+                          "speedup_vs_1": round(base / slowest, 2), "max_rank_launch_ms": round(max(kern), 2),
+                          "msamples_s_if_parallel": round(W * H * SPP / (slowest * 1e-3) / 1e6, 1),
+                          "per_rank_ms": [round(x, 2) for x in per_rank]}), flush=True)
     r.close()
 
 
