@@ -26,8 +26,8 @@ struct rtw_ctx {
                                   // sample-by-sample fold exactly
     size_t partial_max = (size_t)8 << 30;   // cap of the chunk-sum buffer (auto chunk grows)
     uint32_t group = 0;           // chunks per wave task (0 = from target_tasks)
-    uint64_t target_tasks = 1u << 17;   // auto chunks-per-task: about this many tasks,
-                                        // at most kMaxAutoGroup chunks per task
+    uint64_t target_tasks = 0;   // auto chunks-per-task: about this many tasks (0: 2^19 with
+                                 // persistent waves, 2^17 without), 4..32 chunks per task
     int world_pref = 1;           // 1: LDS-staged sphere list when it fits, 0: global
     int auto_accel = RTW_ACCEL_AUTO;    // RTW_ACCEL_AUTO resolves to this (AUTO: by scene size)
     int bvh_kind = 3;             // BVH traversal: 3 = binary while-while + leaf postponing on the
@@ -675,14 +675,16 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
     p.n_chunks = p.spp ? (p.spp + chunk - 1) / chunk : 0;
     uint32_t group = c->group;
     if (group == 0) {
-        // ~2^17 tasks: at one GPU (C2: 15k tiles) that caps at kMaxAutoGroup;
-        // a rank's share of a split render (C2 / 8 ranks: 1.9k tiles) gets 8
-        // chunks per task instead of the 4 a fixed 2^18 tasks gave -- that
-        // share measured 15.6 -> 12.7 ms (per-wave tail vs launch tail)
-        constexpr uint32_t kMaxAutoGroup = 32;
-        const uint64_t n_groups = p.n_local_tiles ? (c->target_tasks + p.n_local_tiles - 1) / p.n_local_tiles : 1;
+        // Persistent waves (default) have no per-task drain, only the launch's
+        // tail, which grows with the task size: ~2^19 tasks (C2 split over
+        // 1 / 2 / 4 / 8 ranks: 14 / 7 / 4 / 4 chunks per task, measured within
+        // 2 % of the best of 4..32 each).  One task per wave instead pays a
+        // drain per task: ~2^17 tasks.
+        constexpr uint32_t kMinAutoGroup = 4, kMaxAutoGroup = 32;
+        const uint64_t target = c->target_tasks ? c->target_tasks : (c->persist ? 1u << 19 : 1u << 17);
+        const uint64_t n_groups = p.n_local_tiles ? (target + p.n_local_tiles - 1) / p.n_local_tiles : 1;
         group = (uint32_t)((p.n_chunks + n_groups - 1) / std::max<uint64_t>(n_groups, 1));
-        group = std::min(group, kMaxAutoGroup);
+        group = std::max(kMinAutoGroup, std::min(group, kMaxAutoGroup));
     }
     p.group = std::max<uint32_t>(1, std::min<uint32_t>(group, std::max<uint32_t>(p.n_chunks, 1)));
     p.n_groups = p.n_chunks ? (p.n_chunks + p.group - 1) / p.group : 0;
