@@ -190,11 +190,15 @@ int rtw_precision(const rtw_ctx *ctx);
 int rtw_set_chunk(rtw_ctx *ctx, uint32_t chunk);
 int rtw_set_accel(rtw_ctx *ctx, int accel);
 /* scheduling knobs (benchmarking): "chunk" (samples per item, 0 = auto),
- * "auto_chunk", "group" (chunks per wave task, 0 = auto), "target_tasks",
+ * "auto_chunk", "group" (chunks per wave task, 0 = auto: 4..32), "target_tasks"
+ * (auto group: about this many tasks; 0 = 2^19 with persistent waves, 2^17 without),
+ * "persist" (workgroups of persistent waves that take tasks from a global counter,
+ * default 2048; 0 = one task per wave),
  * "lds" (1 = stage the sphere list in LDS when it fits, 0 = read it from HBM),
  * "robust" (f32 ray-sphere tests in closest-approach form: 1 on, 0 off,
  * 2 = by the scene's distance-to-radius ratio, the default),
- * "xcd" (1 = contiguous task runs per XCD; 0 = round-robin, the default),
+ * "xcd" (persist 0 only: 1 = contiguous task runs per XCD, 2 = tile rows per
+ * XCD; 0 = round-robin, the default),
  * "item_order" (wave item pool: 1 = sample-major, the default; 0 = pixel-major),
  * "bvh_leaf" (spheres per BVH leaf, 1..15; 0 = auto, the default: 4, or 8 for
  * scenes of >= 100k spheres; takes effect at the
