@@ -7,12 +7,12 @@ ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$ROOT"
 OUT="$ROOT/gpurun_out"
 mkdir -p "$OUT"
-TAG="${1:-r01}"
+TAG="${1:-r02}"
 STEPS="${STEPS:-3}"
 
 fatal() { case "$1" in 0|1) return 1;; *) return 0;; esac; }
 
-timeout -k 10 600 python -m pytest tests -m gpu -q -rA > "$OUT/pytest_gpu_$TAG.log" 2>&1
+timeout -k 10 600 python -u -m pytest tests -m gpu -v -rA --timeout 120 --timeout-method thread > "$OUT/pytest_gpu_$TAG.log" 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -5 "$OUT/pytest_gpu_$TAG.log"
 if fatal $rc; then exit $rc; fi
 
