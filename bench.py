@@ -4,8 +4,9 @@ the Book-1 final scene (scenes::simple), BASELINE.json configs[1]:
 1200x800, 500 spp, max_depth 50, f32 arithmetic, one MI355X per rank.
 
 A step = one full render of the image (every pixel x every sample) from the
-scene already resident in HBM; for N > 1 ranks the 8-row tile rows are
-interleaved over the ranks and gathered to rank 0 over RCCL inside the step.
+scene already resident in HBM; the image's 8x8 tiles are interleaved over
+the ranks (tile T -> rank T % N), and for N > 1 the ranks' packed tiles are
+gathered to rank 0 over RCCL and un-interleaved there inside the step.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...
@@ -33,12 +34,13 @@ SCENE_SEED = 0x5EED0001
 W, H, SPP, DEPTH = 1200, 800, 500, 50
 PEAK_FP32_TFLOPS = 157.3     # MI355X vector FP32 (MI355X_MICROARCH.md, chip table)
 PEAK_FP64_TFLOPS = 78.6      # MI355X vector FP64
-# Roofline flops.  ALGORITHMIC (the roofline's `achieved`):
-# per sample F = S*(23*N_s + 6*N_pl) + L*(23*N_L + 40) -- the reference's
-# brute-force world query (every sphere's 23-flop discriminant per segment)
-# plus the light loop, with S, L the measured segments and Lambertian
-# bounces per sample.  EXECUTED (reported beside it): the arithmetic the
-# BVH kernel actually performs, priced from its own counters.
+# Roofline flops.  `roofline.achieved` is the arithmetic the kernel EXECUTES,
+# priced from its own counters (node visits, sphere tests, segments, Lambertian
+# bounces) -- a fraction of the VALU peak.  The brute-force-
+# equivalent rate of SURVEY.md §8d (every sphere's 23-flop discriminant per
+# segment + the light loop, what the reference's algorithm would need) is
+# reported beside it as `algorithmic_equiv_tflops`: the BVH skips most of that
+# work, so that rate can exceed the peak and is not a roofline fraction.
 ALG_SPHERE = 23              # flops to the discriminant
 ALG_PLANE = 6
 ALG_LAMBERT_BASE = 40
@@ -57,7 +59,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--precision", choices=["f32", "f64"], default="f32")
+    ap.add_argument("--precision", choices=["f32", "f64"], default="f32",
+                    help="f32: the headline speed mode (BASELINE configs[1]); f64: the parity mode, "
+                         "bit-identical to the oracle (FP64 roofline)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="target CPU time of the cpu_baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -82,20 +86,49 @@ def pmc_traffic(workload, precision, world):
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json")), key=version):
         with open(f) as fh:
             d = json.load(fh)
-        if d.get("workload") == workload and any(
+        if d.get("workload") == workload and "bytes_per_launch" in d and any(
                 k.startswith(f"void rtw::dev::render_kernel<{dtype}, {world},") for k in d.get("kernel", [])):
             best = d
     return best
+
+
+def host_cpus():
+    """CPUs this process may use on the host, and what lscpu says about them:
+    the affinity mask, capped by a cgroup CPU quota when one is set (the GPU
+    box gives each GPU a share of a larger machine)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    info = {"affinity_cpus": aff, "cgroup_cpu_quota": quota, "os_cpu_count": os.cpu_count()}
+    try:
+        import subprocess
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        keys = {"Model name": "model", "Socket(s)": "sockets", "Core(s) per socket": "cores_per_socket",
+                "Thread(s) per core": "threads_per_core", "CPU(s)": "cpus"}
+        for line in out.splitlines():
+            k, _, v = line.partition(":")
+            if k.strip() in keys:
+                info[keys[k.strip()]] = v.strip()
+    except (OSError, ValueError, subprocess.SubprocessError):
+        pass
+    threads = aff if quota is None else max(1, min(aff, int(quota)))
+    return threads, info
 
 
 def cpu_baseline(scene, target_s):
     """The oracle (C restatement of the reference path, oracle/) timed on this
     host on a bounded sample of the same workload: every k-th image row of the
     1200x800x500spp render, faithful reference-BVH traversal (bvh.rs incl. its
-    per-visit node-AABB recomputation).  Test infrastructure used as the CPU
-    baseline only -- never on the GPU path."""
+    per-visit node-AABB recomputation), one task per pixel over every CPU this
+    process may use.  Test infrastructure used as the CPU baseline only --
+    never on the GPU path."""
     from oracle import oracle as O
-    threads = min(16, os.cpu_count() or 1)
+    threads, info = host_cpus()
     cam = O.camera_build(**dict(O.simple_camera_kw(), image_width=W, image_height=H,
                                 samples_per_pixel=SPP, max_depth=DEPTH))
     sc = O.Scene(**scene.__dict__)
@@ -120,7 +153,8 @@ def cpu_baseline(scene, target_s):
     out = {"value": round(v, 4), "unit": "Msamples/s", "cores": threads, "kind": "port",
            "sample": f"every {step}th row of the {W}x{H}x{SPP}spp depth-{DEPTH} render "
                      f"({n} samples, {dt:.1f} s), oracle f64, reference BVH restated incl. "
-                     f"per-visit node-AABB recomputation (bvh.rs:147-152), {threads} threads"}
+                     f"per-visit node-AABB recomputation (bvh.rs:147-152), {threads} threads",
+           "host": info}
     if "bvh_cached" in res:
         out["value_bvh_cached"] = round(res["bvh_cached"][0], 4)
     out["parity"] = parity_on_sample(scene, (0, H, step), 99, ref_img)
@@ -153,9 +187,53 @@ def parity_on_sample(scene, oracle_rows, seed, ref_full):
                      "max_abs": float(np.abs(img[ok] - ref[ok]).max() / SPP),
                      "bit_identical": float((img == ref).all(-1)[ok].mean()),
                      "nan_mask_equal": bool(np.array_equal(np.isnan(img).any(-1), np.isnan(ref).any(-1))),
+                     "nan_pixels": int(np.isnan(img).any(-1).sum()), "nan_pixels_ref": int(np.isnan(ref).any(-1).sum()),
+                     "image_mean_rel_bias": float(img[ok].mean() / ref[ok].mean() - 1.0),
                      "render_s": round(t, 3), "chunk": chunk}
-    out["tolerance"] = "f64: MAE < 1e-5 (north_star); f32: statistical (DESIGN.md §2)"
+    out["tolerance"] = ("f64: per-pixel MAE < 1e-5 and identical NaN masks (north_star); f32: the "
+                        "statistical tolerance of DESIGN.md §2 (tests/test_gpu_f32_tolerance.py)")
     return out
+
+
+def run_steps(step, steps, warmup, dist, sync, device=None):
+    """W untimed warm-up steps, then EXACTLY `steps` timed steps bracketed by a
+    barrier + device sync on both sides; the max over ranks of the elapsed
+    time (seconds)."""
+    for w in range(warmup):
+        step(1000 + w)
+    sync()
+    if dist is not None:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        step(k)
+    sync()
+    if dist is not None:
+        dist.barrier()
+    sync()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed
+
+
+def make_step(render, assemble, dist, rank, world_size, buf, gathered, image):
+    """One step: this rank renders its tiles into `buf` (packed); with N > 1
+    ranks they are gathered to rank 0 (ONE collective: RCCL over xGMI on the
+    GPU box, gloo in the CPU test) into the rows of `gathered` [N, numel(buf)],
+    which rank 0 un-interleaves into `image`."""
+    def step(seed):
+        render(seed, buf)
+        if dist is not None:
+            dist.gather(buf, list(gathered.unbind(0)) if rank == 0 else None, dst=0)
+            if rank == 0:
+                assemble(gathered, image)
+        else:
+            assemble(buf.view(1, -1), image)
+    return step
 
 
 def main():
@@ -184,42 +262,24 @@ def main():
         k, v = kv.split("=")
         r.set_tuning(k, int(v))
     r.set_scene(scene)
-    assert rtw.tile_rows() == sharding.TILE_ROWS
-    my_rows = rtw.rows_for_rank(H, rank, world_size)
-    max_rows = max(rtw.rows_for_rank(H, k, world_size) for k in range(world_size))
-    buf = torch.zeros((max_rows, W, 3), dtype=tdtype, device=dev)
-    gathered = [torch.empty_like(buf) for _ in range(world_size)] if (dist and rank == 0) else None
+    assert rtw.tile_size() == sharding.TILE
+    # equal-size packed tile buffers (rank 0 holds the most tiles), as the gather needs
+    max_tiles = rtw.tiles_for_rank(W, H, 0, world_size)
+    buf = torch.zeros((max_tiles * 64 * 3,), dtype=tdtype, device=dev)
+    gathered = torch.empty((world_size, buf.numel()), dtype=tdtype, device=dev) if (dist and rank == 0) else None
     image = torch.empty((H, W, 3), dtype=tdtype, device=dev) if rank == 0 else None
-    stream = torch.cuda.current_stream(dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
 
-    def step(seed):
-        r.render_device(cam, seed, buf.data_ptr(), buf.numel() * buf.element_size(),
-                        rank=rank, nranks=world_size, stream=stream.cuda_stream)
-        if dist is not None:
-            dist.gather(buf, gathered, dst=0)
-            if rank == 0:
-                sharding.assemble(image, gathered, H)
-        elif image is not None:
-            image.copy_(buf[:H])
+    def render(seed, out):
+        r.render_device(cam, seed, out.data_ptr(), out.numel() * out.element_size(),
+                        rank=rank, nranks=world_size, stream=stream)
 
-    for w in range(a.warmup):
-        step(1000 + w)
-    torch.cuda.synchronize(dev)
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for k in range(a.steps):
-        step(k)
-    torch.cuda.synchronize(dev)
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    elapsed = time.perf_counter() - t0
-    if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    def assemble(ranks, img):
+        r.assemble_tiles(ranks.data_ptr(), ranks.stride(0) * ranks.element_size(), ranks.shape[0], W, H,
+                         img.data_ptr(), stream=stream)
+
+    step = make_step(render, assemble, dist, rank, world_size, buf, gathered, image)
+    elapsed = run_steps(step, a.steps, a.warmup, dist, lambda: torch.cuda.synchronize(dev), device=dev)
 
     # live per-launch kernel times of the timed steps (HIP events on `stream`)
     render_ms, total_ms = r.get_timings(a.steps)
@@ -241,8 +301,8 @@ def main():
         st.segments * FLOP_PLANE * n_pl + st.lambertian * (FLOP_LIGHT * n_li + FLOP_LAMBERT_BASE)
     accel = ACCEL_NAMES.get(int(st.accel), str(st.accel))
     avg_ms = float(np.mean(render_ms)) if render_ms else float("nan")
-    achieved = alg_flops / (avg_ms * 1e-3) / 1e12
-    exe_achieved = exe_flops / (avg_ms * 1e-3) / 1e12
+    alg_rate = alg_flops / (avg_ms * 1e-3) / 1e12
+    exe_rate = exe_flops / (avg_ms * 1e-3) / 1e12
     peak = PEAK_FP32_TFLOPS if prec == rtw.RTW_F32 else PEAK_FP64_TFLOPS
     traffic = pmc_traffic(f"book1_simple_{W}x{H}_{SPP}spp_depth{DEPTH}", a.precision, int(st.kernel))
     out = {
@@ -261,26 +321,32 @@ def main():
                 f"{n_li} lights), per-(pixel,sample) xoshiro256++ streams",
         "config": {"workload": f"book1_simple_{W}x{H}_{SPP}spp_depth{DEPTH}", "width": W,
                    "height": H, "spp": SPP, "max_depth": DEPTH, "spheres": n_sph,
-                   "lights": n_li, "parallelism": f"rowtile{world_size}",
+                   "lights": n_li, "parallelism": f"tile8x8_interleave{world_size}",
                    "accel": accel if accel != "bvh" else f"bvh{int(st.bvh_width)}",
                    "chunk": int(st.chunk)},
-        "roofline": {"bound": "valu", "achieved": round(achieved, 3), "peak": peak,
-                     "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
+        "roofline": {"bound": "valu", "achieved": round(exe_rate, 3), "peak": peak,
+                     "unit": "TFLOP/s", "frac": round(exe_rate / peak, 4),
                      "traffic": traffic["bytes_per_launch"] if traffic else None,
                      "traffic_source": traffic["source"] if traffic else None,
                      "kernel": f"render_kernel<{a.precision}, {KERNEL_NAMES.get(int(st.kernel), st.kernel)}>",
                      "kernel_ms_avg": round(avg_ms, 3),
-                     "flops_per_launch": int(alg_flops),
-                     "flops_basis": "SURVEY.md 8d brute-force world query (23 flops x every sphere per "
-                                    "segment + light loop); frac > 1 = the BVH does less arithmetic",
-                     "executed": {"flops_per_launch": int(exe_flops), "achieved": round(exe_achieved, 3),
-                                  "frac": round(exe_achieved / peak, 4)},
+                     "flops_per_launch": int(exe_flops),
+                     "flops_basis": "executed: node visits x width x 20 + sphere tests x 17 + segments x planes x 6 "
+                                    "+ Lambertian bounces x (17 x lights + 40), from the kernel's counters (DESIGN.md §5)",
+                     "algorithmic_equiv_tflops": round(alg_rate, 3),
+                     "algorithmic_equiv_flops_per_launch": int(alg_flops),
+                     "algorithmic_equiv_basis": "SURVEY.md 8d brute-force world query (23 flops x every sphere per "
+                                                "segment + light loop); the BVH skips most of it, so this rate may exceed the peak",
                      "segments_per_sample": round(st.segments / max(st.samples, 1), 4),
                      "bvh_width": int(st.bvh_width),
                      "node_visits_per_segment": round(st.node_visits / max(st.segments, 1), 3),
                      "sphere_tests_per_segment": round(st.sphere_tests / max(st.segments, 1), 3),
                      "lambertian_per_sample": round(st.lambertian / max(st.samples, 1), 4)},
     }
+    if traffic:
+        for k in ("valu_issue_frac", "lanes_active_frac", "wave_wait_frac", "pmc_source"):
+            if k in traffic:
+                out["roofline"][k] = traffic[k]
     if world_size == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(scene, a.cpu_seconds)
     print(json.dumps(out), flush=True)

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define RTW_ABI_VERSION 5
+#define RTW_ABI_VERSION 6
 
 /* error codes */
 #define RTW_OK 0
@@ -197,8 +197,6 @@ int rtw_set_accel(rtw_ctx *ctx, int accel);
  * "lds" (1 = stage the sphere list in LDS when it fits, 0 = read it from HBM),
  * "robust" (f32 ray-sphere tests in closest-approach form: 1 on, 0 off,
  * 2 = by the scene's distance-to-radius ratio, the default),
- * "xcd" (persist 0 only: 1 = contiguous task runs per XCD, 2 = tile rows per
- * XCD; 0 = round-robin, the default),
  * "item_order" (wave item pool: 1 = sample-major, the default; 0 = pixel-major),
  * "bvh_leaf" (spheres per BVH leaf, 1..15; 0 = auto, the default: 4, or 8 for
  * scenes of >= 100k spheres; takes effect at the
@@ -229,16 +227,28 @@ int rtw_render(rtw_ctx *ctx, const rtw_camera *cam, const rtw_scene *scene,
                uint64_t seed, double *out_sum, rtw_stats *stats);
 
 /* Device-resident form for benchmarking and multi-GPU sharding.
- * Renders the 8-row tile rows t with t % nranks == rank into d_out, a device
- * buffer of rtw_rows_for_rank(H, rank, nranks) * W * 3 elements of the
- * context's precision (float or double), the rank's image rows packed in
- * increasing order.  Asynchronous on `stream` (a hipStream_t; NULL = the
- * context's own stream).  No host synchronisation inside. */
+ * The image is cut into 8x8 tiles T = ty * tiles_x + tx (tiles_x = ceil(W/8),
+ * row j = 0 at the bottom); rank `rank` of `nranks` renders the tiles
+ * T = rank, rank + nranks, ... (a fine interleave: every rank samples the
+ * whole image, so the ranks' costs match).  d_out receives them packed: a
+ * device buffer of rtw_tiles_for_rank(W, H, rank, nranks) * 64 * 3 elements of
+ * the context's precision (float or double), the rank's k-th tile at
+ * d_out[(k * 64 + ly * 8 + lx) * 3 + c] (pixels outside the image: 0).
+ * d_out may be NULL when the rank has no tiles.  Asynchronous on `stream`
+ * (a hipStream_t; NULL = the context's own stream).  No host synchronisation
+ * inside. */
 int rtw_render_device(rtw_ctx *ctx, const rtw_camera *cam, uint64_t seed,
                       uint32_t rank, uint32_t nranks, void *d_out, size_t out_bytes,
                       void *stream);
-uint32_t rtw_tile_rows(void);                        /* rows per tile row (8) */
-uint32_t rtw_rows_for_rank(uint32_t image_height, uint32_t rank, uint32_t nranks);
+uint32_t rtw_tile_size(void);                        /* tile edge in pixels (8) */
+uint32_t rtw_tiles_for_rank(uint32_t image_width, uint32_t image_height, uint32_t rank,
+                            uint32_t nranks);
+/* The gathered packed tiles of all ranks -> the image [H][W][3] (sums, j = 0
+ * bottom row), on the device: d_ranks holds nranks rank buffers, each
+ * rank_stride_bytes apart (>= rank 0's packed size; equal-size buffers as an
+ * RCCL gather delivers them).  Asynchronous on `stream`. */
+int rtw_assemble_tiles(rtw_ctx *ctx, const void *d_ranks, size_t rank_stride_bytes, uint32_t nranks,
+                       uint32_t image_width, uint32_t image_height, void *d_image, void *stream);
 /* Counters of the last render (waits for it to finish).  Returns
  * RTW_E_NO_LIGHTS / RTW_E_PANIC (stats still filled) when a sample reached a
  * reference panic. */
@@ -278,6 +288,12 @@ int rtw_encode_rgb8(const double *sums, uint32_t width, uint32_t height, uint32_
 /* Writes the reference's P3 "image.ppm" text; returns bytes written or < 0. */
 int rtw_write_ppm(const char *path, const double *sums, uint32_t width, uint32_t height,
                   uint32_t spp);
+/* The same for the f32 sums of a speed-mode render (each sum widened to f64
+ * exactly, then encoded as above). */
+int rtw_encode_rgb8_f32(const float *sums, uint32_t width, uint32_t height, uint32_t spp,
+                        uint8_t *out_rgb);
+int rtw_write_ppm_f32(const char *path, const float *sums, uint32_t width, uint32_t height,
+                      uint32_t spp);
 
 #ifdef __cplusplus
 }

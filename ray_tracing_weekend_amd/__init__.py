@@ -532,12 +532,28 @@ class Renderer:
         return out
 
     def render_device(self, cam: Camera, seed: int, out_ptr: int, out_bytes: int, *,
-                      rank: int = 0, nranks: int = 1, stream: int = 0):
-        """Asynchronous render of this rank's tile rows into device memory."""
+                      rank: int = 0, nranks: int = 1, stream: int | None = None):
+        """Asynchronous render of this rank's 8x8 tiles (T = rank mod nranks),
+        packed, into device memory (rtw_render_device).  `stream` defaults to
+        torch's current stream, so that the render is ordered after the torch
+        work that prepared `out_ptr` and before the work that reads it."""
+        if stream is None:
+            stream = _torch_stream()
         self._check(_lib.rtw_render_device(self.ctx, C.byref(cam.raw), C.c_uint64(seed), rank,
-                                           nranks, C.c_void_p(out_ptr), out_bytes,
+                                           nranks, C.c_void_p(out_ptr) if out_ptr else None, out_bytes,
                                            C.c_void_p(stream) if stream else None),
                     "rtw_render_device")
+
+    def assemble_tiles(self, ranks_ptr: int, rank_stride_bytes: int, nranks: int, width: int,
+                       height: int, image_ptr: int, *, stream: int | None = None):
+        """The ranks' gathered packed tiles -> the image [H, W, 3] on the device
+        (rtw_assemble_tiles), on torch's current stream by default."""
+        if stream is None:
+            stream = _torch_stream()
+        self._check(_lib.rtw_assemble_tiles(self.ctx, C.c_void_p(ranks_ptr), rank_stride_bytes, nranks,
+                                            width, height, C.c_void_p(image_ptr),
+                                            C.c_void_p(stream) if stream else None),
+                    "rtw_assemble_tiles")
 
     def get_timings(self, n: int = 64):
         """(render_ms, total_ms) lists for the last n renders (HIP events)."""
@@ -552,12 +568,24 @@ class Renderer:
         return self.stats
 
 
-def rows_for_rank(height: int, rank: int, nranks: int) -> int:
-    return int(_lib.rtw_rows_for_rank(height, rank, nranks))
+def tiles_for_rank(width: int, height: int, rank: int, nranks: int) -> int:
+    """8x8 tiles rank `rank` of `nranks` renders (rtw_tiles_for_rank)."""
+    return int(_lib.rtw_tiles_for_rank(width, height, rank, nranks))
 
 
-def tile_rows() -> int:
-    return int(_lib.rtw_tile_rows())
+def tile_size() -> int:
+    return int(_lib.rtw_tile_size())
+
+
+def _torch_stream() -> int:
+    """hipStream_t of torch's current stream (0 when torch has no GPU)."""
+    try:
+        import torch
+        if torch.cuda.is_available():
+            return int(torch.cuda.current_stream().cuda_stream)
+    except ImportError:
+        pass
+    return 0
 
 
 # ---------------------------------------------------------------- scenes
@@ -619,21 +647,31 @@ def _mat(soa, m):
 
 
 # ---------------------------------------------------------------- output
-def encode_rgb8(sums: np.ndarray, spp: int) -> np.ndarray:
-    """SampledColour Display (colour.rs:14-36), rows flipped top-first: uint8 [H, W, 3]."""
+def _sums(sums: np.ndarray):
+    """(contiguous array, ctypes pointer, f32?) of float32 or float64 sums."""
+    if np.asarray(sums).dtype == np.float32:
+        s = np.ascontiguousarray(sums, np.float32)
+        return s, s.ctypes.data_as(_capi._f32p), True
     s = np.ascontiguousarray(sums, np.float64)
+    return s, s.ctypes.data_as(_capi._f64p), False
+
+
+def encode_rgb8(sums: np.ndarray, spp: int) -> np.ndarray:
+    """SampledColour Display (colour.rs:14-36), rows flipped top-first: uint8 [H, W, 3].
+    float32 sums (a speed-mode render) are widened to f64 exactly first."""
+    s, ptr, f32 = _sums(sums)
     H, W = s.shape[:2]
     out = np.zeros((H, W, 3), np.uint8)
-    _lib.rtw_encode_rgb8(s.ctypes.data_as(_capi._f64p), W, H, spp,
-                         out.ctypes.data_as(C.POINTER(C.c_uint8)))
+    fn = _lib.rtw_encode_rgb8_f32 if f32 else _lib.rtw_encode_rgb8
+    fn(ptr, W, H, spp, out.ctypes.data_as(C.POINTER(C.c_uint8)))
     return out
 
 
 def write_ppm(path: str, sums: np.ndarray, spp: int) -> int:
     """The reference's P3 image.ppm (bin/src/main.rs:89-104)."""
-    s = np.ascontiguousarray(sums, np.float64)
+    s, ptr, f32 = _sums(sums)
     H, W = s.shape[:2]
-    n = _lib.rtw_write_ppm(path.encode(), s.ctypes.data_as(_capi._f64p), W, H, spp)
+    n = (_lib.rtw_write_ppm_f32 if f32 else _lib.rtw_write_ppm)(path.encode(), ptr, W, H, spp)
     if n < 0:
         raise RenderError(n, f"cannot write {path}")
     return n

@@ -26,6 +26,7 @@ RTW_LIGHTS_BVH_LEAF = 1
 
 _f64p = C.POINTER(C.c_double)
 _u32p = C.POINTER(C.c_uint32)
+_f32p = C.POINTER(C.c_float)
 
 
 class rtw_camera_builder(C.Structure):
@@ -66,7 +67,7 @@ class rtw_scene(C.Structure):
     ]
 
 
-ABI_VERSION = 5     # RTW_ABI_VERSION of include/rtw.h
+ABI_VERSION = 6     # RTW_ABI_VERSION of include/rtw.h
 
 
 class rtw_stats(C.Structure):
@@ -96,8 +97,10 @@ PROTOTYPES = [
                              _f64p, C.POINTER(rtw_stats)]),
     ("rtw_render_device", C.c_int, [C.c_void_p, C.POINTER(rtw_camera), C.c_uint64, C.c_uint32,
                                     C.c_uint32, C.c_void_p, C.c_size_t, C.c_void_p]),
-    ("rtw_tile_rows", C.c_uint32, []),
-    ("rtw_rows_for_rank", C.c_uint32, [C.c_uint32, C.c_uint32, C.c_uint32]),
+    ("rtw_tile_size", C.c_uint32, []),
+    ("rtw_tiles_for_rank", C.c_uint32, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32]),
+    ("rtw_assemble_tiles", C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_uint32, C.c_uint32,
+                                     C.c_uint32, C.c_void_p, C.c_void_p]),
     ("rtw_get_stats", C.c_int, [C.c_void_p, C.POINTER(rtw_stats)]),
     ("rtw_get_timings", C.c_int, [C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_float), C.c_int]),
     ("rtw_scene_simple", C.c_void_p, [C.c_uint64, C.c_int]),
@@ -109,6 +112,9 @@ PROTOTYPES = [
     ("rtw_encode_rgb8", C.c_int, [_f64p, C.c_uint32, C.c_uint32, C.c_uint32,
                                   C.POINTER(C.c_uint8)]),
     ("rtw_write_ppm", C.c_int, [C.c_char_p, _f64p, C.c_uint32, C.c_uint32, C.c_uint32]),
+    ("rtw_encode_rgb8_f32", C.c_int, [_f32p, C.c_uint32, C.c_uint32, C.c_uint32,
+                                      C.POINTER(C.c_uint8)]),
+    ("rtw_write_ppm_f32", C.c_int, [C.c_char_p, _f32p, C.c_uint32, C.c_uint32, C.c_uint32]),
 ]
 
 _lib = None

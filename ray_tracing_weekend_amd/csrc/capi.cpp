@@ -40,14 +40,12 @@ struct rtw_ctx {
     uint32_t bvh_leaf = 0;            // spheres per BVH leaf (set before rtw_set_scene); 0 = auto:
                                       // 4, or 8 for scenes of >= 100k spheres (C5: +12 %)
     uint32_t persist = 2048;          // workgroups of persistent waves (tasks from a counter);
-                                      // 0: one task per wave (then "xcd" maps blocks to tasks)
+                                      // 0: one task per wave
     uint32_t light_leaf = 0;          // light spheres per light-BVH leaf; 0 = 4
     uint32_t light_grid = 4;          // light pdf through the light grid at light_grid / 16
                                       // cells per light (set before rtw_set_scene); 0: light BVH
+    uint32_t hit64 = 1;               // f32: f64 hit points (the reference's self-intersection odds)
     uint32_t item_order = 1;          // wave item pool: 1 sample-major (C2 +1.3 %, C3 +5 %, C5 +2 %), 0 pixel-major
-    uint32_t xcd = 0;                 // 1: contiguous task runs per XCD (measured 2x SLOWER on C2,
-                                      // C3 and C5: each XCD gets an image band, sky bands finish
-                                      // early -- the round-robin default balances), 0: off
     uint32_t light_bvh_min = 64;      // light lists at least this long use the light BVH
                                       // (C2, 19 lights: the linear masked loop is faster)
     hipStream_t stream = nullptr;
@@ -65,8 +63,10 @@ struct rtw_ctx {
     // work buffers
     void* d_partial = nullptr;
     size_t partial_cap = 0;
-    void* d_out = nullptr;
+    void* d_out = nullptr;        // rtw_render: the packed tiles, then the image
     size_t out_cap = 0;
+    void* d_img = nullptr;
+    size_t img_cap = 0;
     static constexpr int kCounters = 7;   // rtw_kernels.h KParams::counters
     unsigned long long* d_counters = nullptr;
     std::vector<unsigned char> h_out;
@@ -237,6 +237,7 @@ std::vector<unsigned char> stage_scene(const rtw_scene* s, rtw::DevScene<R>* ds,
         return o;
     };
     const size_t o_sph = reserve(sizeof(R4) * s->n_spheres);
+    const size_t o_s64 = reserve(sizeof(double) * 4 * s->n_spheres);
     const size_t o_r = reserve(sizeof(R) * s->n_spheres);
     const size_t o_smat = reserve(sizeof(uint32_t) * s->n_spheres);
     const size_t o_sshade = reserve(sizeof(R4) * s->n_spheres);
@@ -298,6 +299,7 @@ std::vector<unsigned char> stage_scene(const rtw_scene* s, rtw::DevScene<R>* ds,
         // passes (sphere.rs:42-45): r^2 = -inf makes the discriminant -inf
         reinterpret_cast<R4*>(b + o_sph)[k] = R4{(R)p[0], (R)p[1], (R)p[2], p[3] < 0 ? (R)-INFINITY : r * r};
         reinterpret_cast<R*>(b + o_r)[k] = r;
+        for (int a = 0; a < 4; ++a) reinterpret_cast<double*>(b + o_s64)[4 * k + a] = p[a];
         const uint32_t m = s->sphere_mat[k], t = s->mat_type[m];
         reinterpret_cast<uint32_t*>(b + o_smat)[k] = m | (t << 24);
         const double* mp = s->mat_params + 5 * m;
@@ -413,6 +415,7 @@ std::vector<unsigned char> stage_scene(const rtw_scene* s, rtw::DevScene<R>* ds,
     }
     ds->sph = reinterpret_cast<const R4*>(base + o_sph);
     ds->sph_r = reinterpret_cast<const R*>(base + o_r);
+    ds->sph64 = reinterpret_cast<const rtw::R4<double>*>(base + o_s64);
     ds->sph_mat = reinterpret_cast<const uint32_t*>(base + o_smat);
     ds->sph_shade = reinterpret_cast<const R4*>(base + o_sshade);
     ds->planes = reinterpret_cast<const R*>(base + o_pl);
@@ -617,8 +620,16 @@ int ensure(rtw_ctx* c, void** buf, size_t* cap, size_t bytes) {
     return RTW_OK;
 }
 
-uint32_t local_tile_rows(uint32_t tiles_y, uint32_t rank, uint32_t nranks) {
-    return rank < tiles_y ? (tiles_y - rank + nranks - 1) / nranks : 0;
+// pixels inside the image of the tiles T = rank (mod nranks)
+uint64_t rank_pixels(uint32_t W, uint32_t H, uint32_t rank, uint32_t nranks) {
+    const uint32_t tiles_x = (W + rtw::kTile - 1) / rtw::kTile, tiles_y = (H + rtw::kTile - 1) / rtw::kTile;
+    const uint64_t n = (uint64_t)tiles_x * tiles_y;
+    uint64_t px = 0;
+    for (uint64_t T = rank; T < n; T += nranks) {
+        const uint32_t tx = (uint32_t)(T % tiles_x), ty = (uint32_t)(T / tiles_x);
+        px += (uint64_t)std::min(rtw::kTile, W - tx * rtw::kTile) * std::min(rtw::kTile, H - ty * rtw::kTile);
+    }
+    return px;
 }
 
 template <typename R>
@@ -655,10 +666,10 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
     p.rank = rank;
     p.nranks = nranks;
     p.tiles_x = (p.W + rtw::kTile - 1) / rtw::kTile;
-    const uint32_t tiles_y = (p.H + rtw::kTile - 1) / rtw::kTile;
-    p.n_local_tiles = local_tile_rows(tiles_y, rank, nranks) * p.tiles_x;
-    const size_t need_out = (size_t)rtw_rows_for_rank(p.H, rank, nranks) * p.W * 3 * sizeof(R);
-    if (out_bytes < need_out) return fail(c, RTW_E_INVALID, "d_out is smaller than rows_for_rank*W*3");
+    p.n_local_tiles = rtw_tiles_for_rank(p.W, p.H, rank, nranks);
+    const size_t need_out = (size_t)p.n_local_tiles * 64 * 3 * sizeof(R);
+    if (out_bytes < need_out) return fail(c, RTW_E_INVALID, "d_out is smaller than tiles_for_rank*64*3");
+    if (need_out && !d_out) return fail(c, RTW_E_INVALID, "d_out is NULL");
     // Work decomposition: ITEM = (pixel, chunk of `chunk` samples) -- the unit
     // a lane folds in sample order; TASK = (8x8 tile, group of chunks) -- one
     // wavefront's dynamic item pool.  Small chunks balance the lanes of a
@@ -689,7 +700,6 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
     p.group = std::max<uint32_t>(1, std::min<uint32_t>(group, std::max<uint32_t>(p.n_chunks, 1)));
     p.n_groups = p.n_chunks ? (p.n_chunks + p.group - 1) / p.group : 0;
     p.n_tasks = p.n_local_tiles * p.n_groups;
-    p.xcd = c->xcd;
     p.item_order = c->item_order;
     p.persist = c->persist;
     const size_t partial_bytes = std::max<size_t>((size_t)p.n_chunks * p.n_local_tiles * 64 * 3 * sizeof(R), 64);
@@ -761,11 +771,16 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
         p.stack = std::max(p.sc.bvh_depth + 1, p.light_bvh == 1 ? p.sc.lbvh_depth + 1 : 1u);
         if (p.stack > rtw::kBvhStack) return fail(c, RTW_E_UNSUPPORTED, "BVH deeper than the kernel's traversal stack");
     }
+    // f64 hit points: the f32 kernels of sphere + plane scenes (the launch
+    // routes textured / quad / cuboid scenes to kernels without them)
+    p.hit64 = c->hit64 ? 1u : 0u;
     hipEvent_t* ev = c->ring[c->n_renders % rtw_ctx::kRing];
     HIP_TRY(c, hipEventRecord(c->ev0, stream));
     HIP_TRY(c, hipEventRecord(ev[0], stream));
     int lrc = 0;
-    if (p.spp == 0 || p.max_depth == 0) {
+    if (need_out == 0) {
+        HIP_TRY(c, hipEventRecord(ev[1], stream));
+    } else if (p.spp == 0 || p.max_depth == 0) {
         // depth == 0: every sample is Colour::default() + res = 0 (camera.rs:470-472)
         HIP_TRY(c, hipMemsetAsync(d_out, 0, need_out, stream));
         HIP_TRY(c, hipEventRecord(ev[1], stream));
@@ -779,7 +794,7 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
     HIP_TRY(c, hipEventRecord(ev[2], stream));
     ++c->n_renders;
     c->last = rtw_stats{};
-    c->last.samples = (uint64_t)rtw_rows_for_rank(p.H, rank, nranks) * p.W * p.spp;
+    c->last.samples = rank_pixels(p.W, p.H, rank, nranks) * p.spp;
     c->last.accel = (uint32_t)accel;
     c->last.bvh_width = bvh_width;
     c->last.kernel = (uint32_t)world;
@@ -826,6 +841,7 @@ void rtw_destroy(rtw_ctx* c) {
     if (c->d_scene) (void)hipFree(c->d_scene);
     if (c->d_partial) (void)hipFree(c->d_partial);
     if (c->d_out) (void)hipFree(c->d_out);
+    if (c->d_img) (void)hipFree(c->d_img);
     if (c->d_counters) (void)hipFree(c->d_counters);
     for (auto& tri : c->ring)
         for (auto& e : tri)
@@ -855,8 +871,8 @@ int rtw_set_tuning(rtw_ctx* c, const char* key, int64_t value) {
     else if (k == "light_leaf") c->light_leaf = (uint32_t)std::min<int64_t>(value, 15);
     else if (k == "persist") c->persist = (uint32_t)std::min<int64_t>(value, 1 << 20);
     else if (k == "light_grid") c->light_grid = (uint32_t)std::min<int64_t>(value, 1024);
-    else if (k == "xcd") c->xcd = (uint32_t)std::min<int64_t>(value, 2);
     else if (k == "item_order") c->item_order = value ? 1u : 0u;
+    else if (k == "hit64") c->hit64 = value ? 1u : 0u;
     else if (k == "light_bvh_min") c->light_bvh_min = (uint32_t)std::min<int64_t>(value, 1u << 30);
     else if (k == "partial_max") c->partial_max = std::max<size_t>(1 << 20, (size_t)value);
     else if (k == "group") c->group = (uint32_t)value;
@@ -1004,13 +1020,13 @@ int rtw_set_scene(rtw_ctx* c, const rtw_scene* s) {
         fix(ds.sph); fix(ds.sph_r); fix(ds.sph_mat); fix(ds.sph_shade); fix(ds.planes); fix(ds.plane_mat);
         fix(ds.mat_type); fix(ds.mat_p); fix(ds.lights); fix(ds.bvh); fix(ds.bsph); fix(ds.bid);
         fix(ds.bvh4); fix(ds.lbvh); fix(ds.lsph); fix(ds.lid); fix(ds.lg_start); fix(ds.lg_sph); fix(ds.lg_id);
-        fix(ds.quads); fix(ds.quad_mat); fix(ds.lquads);
+        fix(ds.quads); fix(ds.quad_mat); fix(ds.lquads); fix(ds.sph64);
         if (ds.lref) fix(ds.lref);
         fix(ds.boxes); fix(ds.box_mat);
         if (ds.mat_tex) fix(ds.mat_tex);
         fix(ds.tex_type); fix(ds.tex_p); fix(ds.tex_refs); fix(ds.perlin_vec); fix(ds.perlin_perm);
     };
-    static_assert(offsetof(rtw::DevScene<float>, n_sph) == 31 * sizeof(void*),
+    static_assert(offsetof(rtw::DevScene<float>, n_sph) == 32 * sizeof(void*),
                   "DevScene gained a pointer: update rebase");
     if (c->precision == RTW_F32) {
         rebase(tmp32);
@@ -1024,19 +1040,38 @@ int rtw_set_scene(rtw_ctx* c, const rtw_scene* s) {
     return RTW_OK;
 }
 
-uint32_t rtw_tile_rows(void) { return rtw::kTile; }
+uint32_t rtw_tile_size(void) { return rtw::kTile; }
 
-uint32_t rtw_rows_for_rank(uint32_t H, uint32_t rank, uint32_t nranks) {
-    if (nranks == 0) return 0;
-    const uint32_t tiles_y = (H + rtw::kTile - 1) / rtw::kTile;
-    uint32_t rows = 0;
-    for (uint32_t t = rank; t < tiles_y; t += nranks) rows += std::min(rtw::kTile, H - t * rtw::kTile);
-    return rows;
+uint32_t rtw_tiles_for_rank(uint32_t W, uint32_t H, uint32_t rank, uint32_t nranks) {
+    if (nranks == 0 || rank >= nranks) return 0;
+    const uint64_t n = (uint64_t)((W + rtw::kTile - 1) / rtw::kTile) * ((H + rtw::kTile - 1) / rtw::kTile);
+    return rank < n ? (uint32_t)((n - rank + nranks - 1) / nranks) : 0u;
+}
+
+int rtw_assemble_tiles(rtw_ctx* c, const void* d_ranks, size_t rank_stride_bytes, uint32_t nranks, uint32_t W,
+                       uint32_t H, void* d_image, void* stream) {
+    if (!c || nranks == 0) return fail(c, RTW_E_INVALID, "bad argument");
+    const size_t esz = c->precision == RTW_F32 ? sizeof(float) : sizeof(double);
+    if ((uint64_t)W * H == 0) return RTW_OK;
+    if (!d_ranks || !d_image || rank_stride_bytes % esz)
+        return fail(c, RTW_E_INVALID, "bad assemble buffers");
+    if (rank_stride_bytes < (size_t)rtw_tiles_for_rank(W, H, 0, nranks) * 64 * 3 * esz)
+        return fail(c, RTW_E_INVALID, "rank stride is smaller than tiles_for_rank(rank 0)*64*3");
+    HIP_TRY(c, hipSetDevice(c->device));
+    hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : c->stream;
+    const size_t stride = rank_stride_bytes / esz;
+    const int rc = c->precision == RTW_F32
+                       ? rtw::launch_assemble_f32(reinterpret_cast<const float*>(d_ranks), stride, nranks, W, H,
+                                                  reinterpret_cast<float*>(d_image), s)
+                       : rtw::launch_assemble_f64(reinterpret_cast<const double*>(d_ranks), stride, nranks, W, H,
+                                                  reinterpret_cast<double*>(d_image), s);
+    if (rc) return fail(c, RTW_E_DEVICE, std::string("assemble launch failed: ") + hipGetErrorString(hipGetLastError()));
+    return RTW_OK;
 }
 
 int rtw_render_device(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t rank, uint32_t nranks,
                       void* d_out, size_t out_bytes, void* stream) {
-    if (!c || !cam || !d_out || nranks == 0 || rank >= nranks) return fail(c, RTW_E_INVALID, "bad argument");
+    if (!c || !cam || nranks == 0 || rank >= nranks) return fail(c, RTW_E_INVALID, "bad argument");
     if (!c->has_scene) return fail(c, RTW_E_NO_SCENE, "rtw_set_scene was not called");
     HIP_TRY(c, hipSetDevice(c->device));
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
@@ -1096,12 +1131,17 @@ int rtw_render(rtw_ctx* c, const rtw_camera* cam, const rtw_scene* scene, uint64
     if (!c->has_scene) return fail(c, RTW_E_NO_SCENE, "no scene");
     const size_t esz = c->precision == RTW_F32 ? sizeof(float) : sizeof(double);
     const size_t n = (size_t)cam->image_width * cam->image_height * 3;
-    int rc = ensure(c, &c->d_out, &c->out_cap, std::max<size_t>(n * esz, 64));
+    const size_t tiles = (size_t)rtw_tiles_for_rank(cam->image_width, cam->image_height, 0, 1) * 64 * 3;
+    int rc = ensure(c, &c->d_out, &c->out_cap, std::max<size_t>(tiles * esz, 64));
+    if (rc) return rc;
+    rc = ensure(c, &c->d_img, &c->img_cap, std::max<size_t>(n * esz, 64));
     if (rc) return rc;
     rc = rtw_render_device(c, cam, seed, 0, 1, c->d_out, c->out_cap, nullptr);
     if (rc) return rc;
+    rc = rtw_assemble_tiles(c, c->d_out, c->out_cap, 1, cam->image_width, cam->image_height, c->d_img, nullptr);
+    if (rc) return rc;
     c->h_out.resize(n * esz);
-    if (n) HIP_TRY(c, hipMemcpyAsync(c->h_out.data(), c->d_out, n * esz, hipMemcpyDeviceToHost, c->stream));
+    if (n) HIP_TRY(c, hipMemcpyAsync(c->h_out.data(), c->d_img, n * esz, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     if (c->precision == RTW_F32) {
         const float* f = reinterpret_cast<const float*>(c->h_out.data());
@@ -1183,23 +1223,30 @@ static uint8_t to_u8(double x) {
     return (uint8_t)v;
 }
 
-int rtw_encode_rgb8(const double* sums, uint32_t W, uint32_t H, uint32_t spp, uint8_t* out) {
+}  // extern "C"
+
+namespace {
+// write_colour, colour.rs:14-36: scale = (spp as f64).recip(); sqrt(c * scale),
+// on the f64 value of each sum (an f32 sum is widened exactly first); rows in
+// reverse, main.rs:97-104
+template <typename S>
+int encode_rgb8(const S* sums, uint32_t W, uint32_t H, uint32_t spp, uint8_t* out) {
     if ((!sums || !out) && W && H) return RTW_E_INVALID;
-    // write_colour, colour.rs:14-36: scale = (spp as f64).recip(); sqrt(c * scale)
     const double scale = 1.0 / (double)(int32_t)spp;
     for (uint32_t r = 0; r < H; ++r) {
-        const uint32_t j = H - 1 - r;   // main.rs:97-104 writes rows in reverse
+        const uint32_t j = H - 1 - r;
         for (uint32_t i = 0; i < W; ++i)
             for (int k = 0; k < 3; ++k)
-                out[((size_t)r * W + i) * 3 + k] = to_u8(sqrt(sums[((size_t)j * W + i) * 3 + k] * scale));
+                out[((size_t)r * W + i) * 3 + k] = to_u8(sqrt((double)sums[((size_t)j * W + i) * 3 + k] * scale));
     }
     return RTW_OK;
 }
 
-int rtw_write_ppm(const char* path, const double* sums, uint32_t W, uint32_t H, uint32_t spp) {
+template <typename S>
+int write_ppm(const char* path, const S* sums, uint32_t W, uint32_t H, uint32_t spp) {
     if (!path) return RTW_E_INVALID;
     std::vector<uint8_t> rgb((size_t)W * H * 3);
-    int rc = rtw_encode_rgb8(sums, W, H, spp, rgb.data());
+    int rc = encode_rgb8(sums, W, H, spp, rgb.data());
     if (rc) return rc;
     FILE* f = fopen(path, "wb");
     if (!f) return RTW_E_INVALID;
@@ -1208,6 +1255,22 @@ int rtw_write_ppm(const char* path, const double* sums, uint32_t W, uint32_t H, 
         n += fprintf(f, "%u %u %u\n", rgb[3 * p], rgb[3 * p + 1], rgb[3 * p + 2]);
     fclose(f);
     return n;
+}
+}  // namespace
+
+extern "C" {
+
+int rtw_encode_rgb8(const double* sums, uint32_t W, uint32_t H, uint32_t spp, uint8_t* out) {
+    return encode_rgb8(sums, W, H, spp, out);
+}
+int rtw_encode_rgb8_f32(const float* sums, uint32_t W, uint32_t H, uint32_t spp, uint8_t* out) {
+    return encode_rgb8(sums, W, H, spp, out);
+}
+int rtw_write_ppm(const char* path, const double* sums, uint32_t W, uint32_t H, uint32_t spp) {
+    return write_ppm(path, sums, W, H, spp);
+}
+int rtw_write_ppm_f32(const char* path, const float* sums, uint32_t W, uint32_t H, uint32_t spp) {
+    return write_ppm(path, sums, W, H, spp);
 }
 
 }  // extern "C"

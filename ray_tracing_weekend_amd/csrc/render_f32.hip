@@ -10,4 +10,9 @@ int launch_render_f32(const KParams<float>& p, int world, size_t lds_bytes, floa
     return launch_render_impl<float>(p, world, lds_bytes, out, stream, mid);
 }
 
+int launch_assemble_f32(const float* ranks, size_t rank_stride, uint32_t nranks, uint32_t W, uint32_t H,
+                        float* img, hipStream_t stream) {
+    return launch_assemble_impl<float>(ranks, rank_stride, nranks, W, H, img, stream);
+}
+
 }  // namespace rtw

@@ -10,4 +10,9 @@ int launch_render_f64(const KParams<double>& p, int world, size_t lds_bytes, dou
     return launch_render_impl<double>(p, world, lds_bytes, out, stream, mid);
 }
 
+int launch_assemble_f64(const double* ranks, size_t rank_stride, uint32_t nranks, uint32_t W, uint32_t H,
+                        double* img, hipStream_t stream) {
+    return launch_assemble_impl<double>(ranks, rank_stride, nranks, W, H, img, stream);
+}
+
 }  // namespace rtw

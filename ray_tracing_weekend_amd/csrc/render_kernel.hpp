@@ -220,6 +220,25 @@ __device__ __forceinline__ void sweep_spheres(const R4<float>* __restrict__ sph,
     tb = __uint_as_float(ub + tminb);
 }
 
+// The same with one sphere id excluded (kOptHit64: the sphere the ray starts on)
+template <bool kRobust>
+__device__ __forceinline__ void sweep_spheres_excl(const R4<float>* __restrict__ sph, uint32_t n, int32_t base,
+                                                   V3<float> o, V3<float> d, float tmin, float& tb, int32_t& best,
+                                                   int32_t excl) {
+    const float a = len2_f32(d);
+    const float ia = __builtin_amdgcn_rcpf(a);
+    const uint32_t tminb = __float_as_uint(tmin);
+    uint32_t ub = __float_as_uint(tb) - tminb;
+#pragma unroll 8
+    for (uint32_t k = 0; k < n; ++k) {
+        const uint32_t u = sphere_u<kRobust>(sph[k], o, d, a, ia, tminb);
+        const bool h = u < ub && base + (int32_t)k != excl;
+        ub = h ? u : ub;
+        best = h ? base + (int32_t)k : best;
+    }
+    tb = __uint_as_float(ub + tminb);
+}
+
 // Sum of Sphere::pdf_value over the light list in list order
 // (HittableList::pdf_value, hittable_list.rs:408-412; sphere.rs:101-111).
 // f64: the reference's arithmetic, light by light.
@@ -685,6 +704,153 @@ __device__ __forceinline__ void bvh_closest(const DevScene<float>& sc, int32_t b
     best = T.best;
 }
 
+// ---------------------------------------------------------------------------
+// f64 hit points for the f32 kernels (kOptHit64).  The reference's t_min =
+// f64::EPSILON (camera.rs:473) makes the bounce after a hit re-hit its own
+// sphere ("acne") exactly when the rounded f64 hit point r.at(t) lies inside
+// it -- a coin flip decided by f64 rounding that shapes the image (paths
+// trapped inside spheres, NaN samples from Lambertian points inside light
+// spheres).  f32 arithmetic flips that coin with other odds, so the f32 image
+// drifts from the reference's region by region.  With kOptHit64 the f32
+// kernel keeps the ray origin in f64 and computes, in f64 with the
+// reference's operation order and no FMA contraction: the re-hit test of the
+// sphere the ray starts on, the t of the sphere the f32 traversal picked, and
+// the hit point o + d t.  Traversal, shading and sampling stay f32.
+// ---------------------------------------------------------------------------
+// Sphere::hit's roots, sphere.rs:61-80, with t in [EPSILON, inf] (f64, no FMA)
+// on the sphere as given (DevScene::sph64: {c, radius})
+__device__ __forceinline__ bool sphere_t_ref64(const R4<double>& S, V3<double> o, V3<double> d, double& t) {
+#pragma clang fp contract(off)
+    const double ocx = o.x - S.x, ocy = o.y - S.y, ocz = o.z - S.z, r = S.w;
+    const double a = d.x * d.x + d.y * d.y + d.z * d.z;
+    const double half_b = ocx * d.x + ocy * d.y + ocz * d.z;
+    const double c = (ocx * ocx + ocy * ocy + ocz * ocz) - r * r;
+    const double disc = half_b * half_b - a * c;
+    if (!(disc > 0.0)) return false;
+    const double sq = __builtin_sqrt(disc);
+    double root = (-half_b - sq) / a;
+    if (!(P<double>::kEps <= root && root <= (double)INFINITY)) {
+        root = (-half_b + sq) / a;
+        if (!(P<double>::kEps <= root && root <= (double)INFINITY)) return false;
+    }
+    t = root;
+    return true;
+}
+// Ray::at, o + d t (f64, no FMA)
+__device__ __forceinline__ V3<double> ray_at64(V3<double> o, V3<double> d, double t) {
+#pragma clang fp contract(off)
+    return V3<double>{o.x + d.x * t, o.y + d.y * t, o.z + d.z * t};
+}
+__device__ __forceinline__ V3<double> to64(V3<float> v) { return V3<double>{v.x, v.y, v.z}; }
+// An f32 direction as a GENERIC f64 value: the f32 value with pseudo-random
+// bits below its 24-bit mantissa (a relative change < 2^-25: the same f32
+// value).  The reference's directions are f64 results with rounding noise in
+// every bit; a 24-bit value makes d.d exact and the products of d.(o - c)
+// nearly so, which changes the odds of the ulp-level decisions above (the
+// re-hit of a perfect mirror from inside, measured: tools/trace_paths.py).
+// The bits come from a hash of the f32 bits (no RNG draw).
+__device__ __forceinline__ uint32_t mix32(uint32_t h) {
+    h ^= h >> 16;
+    h *= 0x7feb352du;
+    h ^= h >> 15;
+    h *= 0x846ca68bu;
+    h ^= h >> 16;
+    return h;
+}
+__device__ __forceinline__ V3<double> dither64(V3<float> v) {
+    const uint32_t h0 = mix32(__float_as_uint(v.x) ^ mix32(__float_as_uint(v.y) ^ mix32(__float_as_uint(v.z))));
+    const uint32_t h1 = mix32(h0 + 0x9e3779b9u), h2 = mix32(h1 + 0x9e3779b9u);
+    constexpr double kScale = 0x1p-25 / 4294967296.0;        // (h - 2^31) * 2^-57: |rel| < 2^-26
+    return V3<double>{(double)v.x * (1.0 + ((double)h0 - 2147483648.0) * kScale),
+                      (double)v.y * (1.0 + ((double)h1 - 2147483648.0) * kScale),
+                      (double)v.z * (1.0 + ((double)h2 - 2147483648.0) * kScale)};
+}
+
+__device__ __forceinline__ V3<double> dither64(V3<double> v) { return v; }   // (R = double: unused)
+template <typename R>
+__device__ __forceinline__ V3<R> from64(V3<double> v) { return mk((R)v.x, (R)v.y, (R)v.z); }
+
+// Metal::scatter's direction (material.rs:407-421) in f64, no FMA:
+// reflect(d / |d|, n) + us * fuzz, with reflect(v, n) = v - (n * 2) (v . n)
+// (vec.rs); its dot with n decides absorption (returned in `keep`)
+__device__ __forceinline__ V3<double> metal_dir64(V3<double> d, V3<double> n, double fuzz, V3<double> us,
+                                                  bool& keep) {
+#pragma clang fp contract(off)
+    const double l = __builtin_sqrt(d.x * d.x + d.y * d.y + d.z * d.z);
+    const double ux = d.x / l, uy = d.y / l, uz = d.z / l;
+    const double vn = ux * n.x + uy * n.y + uz * n.z;
+    const double rx = ux - (n.x * 2.0) * vn, ry = uy - (n.y * 2.0) * vn, rz = uz - (n.z * 2.0) * vn;
+    const V3<double> out = {rx + us.x * fuzz, ry + us.y * fuzz, rz + us.z * fuzz};
+    keep = out.x * n.x + out.y * n.y + out.z * n.z > 0.0;
+    return out;
+}
+// Dialectric::scatter's direction (material.rs:458-487) in f64, no FMA; the
+// Open01 word is drawn only when refraction is possible (the || short circuit)
+__device__ __forceinline__ V3<double> dielectric_dir64(V3<double> d, V3<double> n, bool front, double ior,
+                                                       Rng& g) {
+#pragma clang fp contract(off)
+    const double ratio = front ? 1.0 / ior : ior;
+    const double l = __builtin_sqrt(d.x * d.x + d.y * d.y + d.z * d.z);
+    const double ux = d.x / l, uy = d.y / l, uz = d.z / l;
+    const double cos_t = __builtin_fmin(ux * -n.x + uy * -n.y + uz * -n.z, 1.0);
+    const double sin_t = __builtin_sqrt(1.0 - cos_t * cos_t);
+    bool refl = ratio * sin_t > 1.0;
+    if (!refl) {
+        double r0 = (1.0 - ratio) / (1.0 + ratio);       // Dialectric::reflectance, powi(5) as LLVM expands it
+        r0 = r0 * r0;
+        const double x = 1.0 - cos_t, x2 = x * x;
+        refl = r0 + (1.0 - r0) * (x * (x2 * x2)) > P<double>::u_open01(g.next());
+    }
+    if (refl) {
+        const double vn = ux * n.x + uy * n.y + uz * n.z;
+        return V3<double>{ux - (n.x * 2.0) * vn, uy - (n.y * 2.0) * vn, uz - (n.z * 2.0) * vn};
+    }
+    // refract(v, n, eta), vec.rs: perp = (v + n cos) eta, par = n * -sqrt(1 - perp.perp)
+    const double c2 = __builtin_fmin(ux * -n.x + uy * -n.y + uz * -n.z, 1.0);
+    const double px = (ux + n.x * c2) * ratio, py = (uy + n.y * c2) * ratio, pz = (uz + n.z * c2) * ratio;
+    const double q = -__builtin_sqrt(1.0 - (px * px + py * py + pz * pz));
+    return V3<double>{px + n.x * q, py + n.y * q, pz + n.z * q};
+}
+// the outward normal (p - c) / radius, sphere.rs:82-83 (f64, no FMA)
+__device__ __forceinline__ V3<double> sphere_normal64(V3<double> p, const R4<double>& S) {
+#pragma clang fp contract(off)
+    return V3<double>{(p.x - S.x) / S.w, (p.y - S.y) / S.w, (p.z - S.z) / S.w};
+}
+__device__ __forceinline__ bool front64(V3<double> d, V3<double> n) {
+#pragma clang fp contract(off)
+    return d.x * n.x + d.y * n.y + d.z * n.z < 0.0;
+}
+
+// The f32 sphere test with one sphere id excluded (kOptHit64: the sphere the
+// ray starts on, whose re-hit is decided in f64).
+template <bool kRobust>
+struct SphereTesterX : SphereTester<float, kRobust> {
+    int32_t excl;
+    __device__ __forceinline__ void test(const R4<float>& s, int32_t id) {
+        const uint32_t u = sphere_u<kRobust>(s, this->o, this->d, this->a, this->ia, this->tminb);
+        const bool upd = (u < this->ub || (u == this->ub && id < this->best)) && id != excl;
+        this->ub = upd ? u : this->ub;
+        this->best = upd ? id : this->best;
+    }
+};
+template <int kKind, bool kRobust>
+__device__ __forceinline__ void bvh_closest_excl(const DevScene<float>& sc, int32_t base, V3<float> o,
+                                                 V3<float> d, float tmin, float& tb, int32_t& best,
+                                                 int32_t* stk, uint32_t& nvis, uint32_t& ntest, int32_t excl) {
+    SphereTesterX<kRobust> T;
+    T.o = o;
+    T.d = d;
+    T.a = len2_f32(d);
+    T.ia = __builtin_amdgcn_rcpf(T.a);
+    T.tminb = __float_as_uint(tmin);
+    T.ub = __float_as_uint(tb) - T.tminb;
+    T.best = best;
+    T.excl = excl;
+    bvh_dispatch<kKind>(sc, base, o, d, T, stk, nvis, ntest, -1);
+    tb = T.bound();
+    best = T.best;
+}
+
 // Light pdf through the light BVH (KParams::light_bvh): every light sphere the
 // ray (o, d) hits with t in [0, inf] contributes its solid-angle pdf
 // (HittableList::pdf_value, hittable_list.rs:408-412; sphere.rs:101-111).
@@ -935,13 +1101,18 @@ __device__ V3<R> tex_colour(const DevScene<R>& sc, uint32_t tid, R u, R v, V3<R>
     return mk((R)NAN, (R)NAN, (R)NAN);
 }
 
-// RTW_EXP (profiling builds only, tools/exp_cost.sh): repeat one part of the
-// per-segment work so that the time difference prices it.  1 = closest-hit
-// query, 2 = light pdf sum, 3 = stream seeding, 4 = Lambertian direction
-// sampling, 5 = plane tests, 6 = closest-hit query along another direction,
-// 7 = light pdf sum along the same direction.
-#ifndef RTW_EXP
-#define RTW_EXP 0
+// Experiment hooks: every RTW_PROBE_* below expands to nothing in the product
+// build; the profiling builds of tools/exp_cost.sh (RTW_EXP) and
+// tools/trace_paths.py (RTW_TRACE) define them in rtw_probes.hpp.
+#if defined(RTW_EXP) || defined(RTW_TRACE)
+#include "rtw_probes.hpp"
+#else
+#define RTW_PROBE_PLANES()
+#define RTW_PROBE_CLOSEST()
+#define RTW_PROBE_SEGMENT()
+#define RTW_PROBE_LAMBERT_DIR()
+#define RTW_PROBE_LIGHT_PDF()
+#define RTW_PROBE_SEED()
 #endif
 
 // kOpt: compile-time options, chosen per launch by the host
@@ -951,7 +1122,9 @@ __device__ V3<R> tex_colour(const DevScene<R>& sc, uint32_t tid, R u, R v, V3<R>
 //   kOptPrims    quads, transformed cuboids and mixed light lists (DevScene::lref); without
 //                it the kernel is spheres + planes only (the Book-1 scenes) and carries none
 //                of that code -- fewer live registers across the segment loop
-enum : int { kOptRobust = 1, kOptLightBvh = 2, kOptTex = 4, kOptPrims = 8 };
+//   kOptHit64    (f32 kernels of sphere + plane scenes) f64 ray origin, own-sphere re-hit test,
+//                hit t and hit point (sphere_t_ref64): the reference's self-intersection odds
+enum : int { kOptRobust = 1, kOptLightBvh = 2, kOptTex = 4, kOptPrims = 8, kOptHit64 = 16 };
 
 template <typename R, int kWorld, int kOpt>
 // f32: ask for 5 waves per SIMD (<= 96 VGPRs; the kernel fits without
@@ -959,12 +1132,17 @@ template <typename R, int kWorld, int kOpt>
 #ifndef RTW_WAVES
 #define RTW_WAVES 5
 #endif
-__global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? RTW_WAVES : 1) render_kernel(const KParams<R> p) {
+#ifndef RTW_WAVES_H64
+#define RTW_WAVES_H64 4
+#endif
+__global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ? RTW_WAVES_H64 : RTW_WAVES) : 1)
+    render_kernel(const KParams<R> p) {
     using PR = P<R>;
     constexpr bool kRobust = (kOpt & kOptRobust) != 0;
     constexpr bool kLightBvh = (kOpt & kOptLightBvh) != 0 && kWorld >= kWorldBvh;
     constexpr bool kTex = (kOpt & kOptTex) != 0;
     constexpr bool kPrims = (kOpt & kOptPrims) != 0;
+    constexpr bool kHit64 = (kOpt & kOptHit64) != 0 && sizeof(R) == 4 && !kTex && !kPrims;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     R4<R>* s_sph = reinterpret_cast<R4<R>*>(smem);
     R4<R>* s_li = s_sph + p.sc.n_sph;
@@ -1022,25 +1200,17 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? RTW_WAVES : 1) render
     if constexpr (kWorld == kWorldBvhLds) li = l_li;
 
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    // Workgroups are dispatched round-robin over the 8 XCDs (block b -> XCD
-    // b % 8), each with its own L2.  With p.xcd the block -> task map hands
-    // every XCD one contiguous run of tasks (neighbouring tiles: similar rays,
-    // the same BVH nodes and spheres) instead of every 8th task; the work of
-    // a task is unchanged, so the image is too.  Measured 2x slower (C2, C3,
-    // C5): an XCD then owns an image band, and the sky bands finish first --
-    // off by default.
-    // p.xcd == 2: XCD x = blockIdx % 8 takes the tile rows tr = x (mod 8) --
-    // every XCD still samples the whole image (balanced, like the multi-GPU
-    // interleave), and all tasks of a tile, and of its row, share one L2.
-    // the wave's current task (wave-uniform): tile lt at (tx, ty), chunks
-    // [c_begin, c_begin + glen), a pool of n_items (pixel, chunk) items
+    // the wave's current task (wave-uniform): local tile lt = global 8x8 tile
+    // T = lt * nranks + rank at (tx, ty) -- the ranks take the image's tiles
+    // round-robin (rtw_tiles_for_rank) -- and chunks [c_begin, c_begin +
+    // glen): a pool of n_items (pixel, chunk) items
     uint32_t lt = 0, tx = 0, ty = 0, c_begin = 0, glen = 0, n_items = 0;
     auto set_task = [&](uint32_t t) {
         lt = t / p.n_groups;
         const uint32_t cg = t - lt * p.n_groups;
-        const uint32_t tr = lt / p.tiles_x;
-        tx = lt - tr * p.tiles_x;
-        ty = tr * p.nranks + p.rank;
+        const uint32_t T = lt * p.nranks + p.rank;
+        ty = T / p.tiles_x;
+        tx = T - ty * p.tiles_x;
         c_begin = cg * p.group;
         glen = min(c_begin + p.group, p.n_chunks) - c_begin;
         n_items = 64u * glen;
@@ -1050,28 +1220,8 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? RTW_WAVES : 1) render
     // finish the last one -- no per-task drain, one workgroup setup (LDS
     // staging) per resident workgroup.  Else one task per wave (static map).
     bool more = p.persist != 0;       // wave-uniform: the counter may hold tasks
-    uint32_t blk = blockIdx.x;
-    uint32_t task = 0;
-    if (p.persist) {
-    } else if (p.xcd == 2) {
-        const uint32_t x = blk & 7u, k = blk >> 3;
-        const uint32_t per_row = p.tiles_x * p.n_groups;          // tasks of one tile row
-        const uint32_t ltr = p.n_local_tiles / p.tiles_x;          // this rank's tile rows
-        const uint32_t rows_x = x < ltr ? (ltr - x + 7u) / 8u : 0u;
-        const uint32_t i = k * kWavesPerBlock + wave;              // index in XCD x's task list
-        if (i >= rows_x * per_row) return;
-        const uint32_t r = i / per_row;
-        task = (x + 8u * r) * per_row + (i - r * per_row);
-    } else {
-        if (p.xcd == 1) {
-            const uint32_t nb = gridDim.x, per = nb / 8u, rem = nb % 8u;
-            const uint32_t x = blk % 8u, k = blk / 8u;
-            // XCD x runs blocks x, x + 8, ...: (per + (x < rem)) of them
-            blk = x * per + min(x, rem) + k;
-        }
-        task = blk * kWavesPerBlock + wave;
-    }
     if (!p.persist) {
+        const uint32_t task = blockIdx.x * kWavesPerBlock + wave;
         if (task >= p.n_tasks) return;
         set_task(task);
     }
@@ -1110,7 +1260,12 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? RTW_WAVES : 1) render
     Rng g;
     V3<R> o = zero, d = zero, mult = zero, res = zero;
     uint32_t depth = 0;
-    int32_t self_s = -1;          // isolated sphere the current ray starts on (else -1)
+    int32_t self_s = -1;          // isolated sphere the current ray starts on (else -1); kHit64:
+                                  // the sphere it starts on, isolated or not
+    bool self_iso = false;        // kHit64: self_s is isolated
+    V3<double> o64 = {0.0, 0.0, 0.0};   // kHit64: the ray origin in f64
+    V3<double> d64 = {0.0, 0.0, 0.0};   // kHit64: the ray direction in f64 (a Metal / Dielectric
+                                        // scatter's own f64 result, else dither64 of the f32 one)
     uint32_t segs = 0, lambs = 0, nvis = 0, ntest = 0;
     bool active = false, need = true;
 
@@ -1127,10 +1282,15 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? RTW_WAVES : 1) render
         }
         o = origin;
         d = ps - origin;
+        if constexpr (kHit64) {
+            o64 = to64(origin);
+            d64 = dither64(d);
+        }
         mult = mk<R>(1, 1, 1);
         res = zero;
         depth = p.max_depth;
         self_s = -1;
+        self_iso = false;
     };
     // Give every lane that needs one a valid item: from the current pool, then
     // (p.persist) from the next task's; none once no task is left.
@@ -1183,18 +1343,17 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? RTW_WAVES : 1) render
 
     while (__ballot(active) != 0) {
         if (active) {
+            if constexpr (kHit64) {
+                // the f32 ray is the f64 one rounded (dither64 stays within half an
+                // f32 ulp): o, d are not kept live across segments
+                o = from64<R>(o64);
+                d = from64<R>(d64);
+            }
             // ---- world.hit(&r, EPSILON..=INFINITY): closest over all primitives
             R tb = (R)INFINITY;
             int32_t best = -1;
-#if RTW_EXP == 5
-            for (int32_t k = 0; k < nplanes; ++k) {
-                R t;
-                const R* pl = p.sc.planes + kPlaneR * k;
-                if (aabb_hit_ref(pl + 6, pl + 9, o, mk(d.y, d.x, d.z), tmin) &&
-                    plane_t(pl, o, mk(d.y, d.x, d.z), tmin, t, nullptr) && t == (R)-7)
-                    ++segs;
-            }
-#endif
+            double tb64 = 0.0;            // kHit64: the closest hit's t in f64
+            RTW_PROBE_PLANES();
             for (int32_t k = 0; k < nplanes; ++k) {
                 R t;
                 const R* pl = p.sc.planes + kPlaneR * k;
@@ -1226,27 +1385,44 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? RTW_WAVES : 1) render
                     best = bbase + k;
                 }
             }
-            if constexpr (kWorld >= kWorldBvh) {
-#if RTW_EXP == 1 || RTW_EXP == 6
-                {
-                    // 1: the same query again (warm caches); 6: a query along a
-                    // permuted direction (cold nodes: prices memory latency)
-                    R tb2 = tb;
-                    int32_t best2 = best;
-                    const V3<R> d2 = RTW_EXP == 6 ? mk(d.z, d.x, d.y) : d;
-                    bvh_closest<kWorld == kWorldBvhLds ? kWorldBvhWW : kWorld, kRobust>(scw, sbase, o, d2, tmin, tb2, best2,
-                                        reinterpret_cast<int32_t*>(smem) + wave * p.stack * 64 + lane, nvis,
-                                        ntest, self_s);
-                    segs += best2 == -7 ? 1u : 0u;
+            if constexpr (kHit64) {
+                // the own sphere's re-hit in f64, the others in f32 (it excluded), the
+                // winner's t again in f64
+                tb64 = best >= 0 ? (double)tb : (double)INFINITY;
+                bool skip = false;
+                if (self_s >= 0) {
+                    ++ntest;
+                    double ts;
+                    if (sphere_t_ref64(p.sc.sph64[self_s], o64, d64, ts) && ts < tb64) {
+                        tb64 = ts;
+                        tb = (float)ts;
+                        best = sbase + self_s;
+                        skip = self_iso;          // isolated: provably the closest sphere hit
+                    }
                 }
-#endif
-                bvh_closest<kWorld == kWorldBvhLds ? kWorldBvhWW : kWorld, kRobust>(scw, sbase, o, d, tmin, tb, best,
-                                    reinterpret_cast<int32_t*>(smem) + wave * p.stack * 64 + lane, nvis,
-                                    ntest, self_s);
+                if (!skip) {
+                    const int32_t prev = best, excl = self_s >= 0 ? sbase + self_s : -1;
+                    if constexpr (kWorld >= kWorldBvh) {
+                        int32_t* stk = reinterpret_cast<int32_t*>(smem) + wave * p.stack * 64 + lane;
+                        constexpr int kKind = kWorld == kWorldBvhLds ? kWorldBvhWW : kWorld;
+                        bvh_closest_excl<kKind, kRobust>(scw, sbase, o, d, tmin, tb, best, stk, nvis, ntest, excl);
+                    } else {
+                        sweep_spheres_excl<kRobust>(sph, p.sc.n_sph, sbase, o, d, tmin, tb, best, excl);
+                    }
+                    if (best != prev && best >= sbase) {
+                        if (!sphere_t_ref64(p.sc.sph64[best - sbase], o64, d64, tb64)) tb64 = (double)tb;
+                    }
+                }
+            } else if constexpr (kWorld >= kWorldBvh) {
+                RTW_PROBE_CLOSEST();
+                int32_t* stk = reinterpret_cast<int32_t*>(smem) + wave * p.stack * 64 + lane;
+                constexpr int kKind = kWorld == kWorldBvhLds ? kWorldBvhWW : kWorld;
+                bvh_closest<kKind, kRobust>(scw, sbase, o, d, tmin, tb, best, stk, nvis, ntest, self_s);
             } else {
                 sweep_spheres<kRobust>(sph, p.sc.n_sph, sbase, o, d, tmin, tb, best);
             }
             ++segs;
+            RTW_PROBE_SEGMENT();
 
             bool done = false;
             V3<R> col = zero;
@@ -1256,10 +1432,18 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? RTW_WAVES : 1) render
             } else {
                 // HitRecord::new, hittable.rs:101-129
                 V3<R> pnt = o + d * tb;
+                V3<double> pnt64 = {0.0, 0.0, 0.0};
+                if constexpr (kHit64) {
+                    pnt64 = ray_at64(o64, d64, tb64);
+                    pnt = mk((float)pnt64.x, (float)pnt64.y, (float)pnt64.z);
+                }
                 V3<R> outward;
                 uint32_t m, mtype;
                 R4<R> mp;
                 int32_t next_self = -1;
+                bool next_iso = false;
+                V3<double> n64 = {0.0, 0.0, 0.0};   // kHit64, sphere hits: the f64 outward normal
+                bool sph_hit = false;
                 bool box_hit = false;
                 bool box_front = false;
                 R hu = (R)0, hv = (R)0;                            // HitRecord u, v (kTex)
@@ -1317,9 +1501,26 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? RTW_WAVES : 1) render
                     mtype = (mw >> 24) & 0x7fu;
                     mp = p.sc.sph_shade[k];
                     next_self = (mw >> 31) ? (int32_t)k : -1;   // bit 31: isolated sphere
+                    if constexpr (kHit64) {
+                        next_self = (int32_t)k;
+                        next_iso = (mw >> 31) != 0;
+                        // Metal / Dielectric scatter in f64 from the f64 normal: their
+                        // directions decide the next re-hit at the ulp level
+                        if (mtype == kMatMetal || mtype == kMatDielectric) {
+                            n64 = sphere_normal64(pnt64, p.sc.sph64[k]);
+                            outward = mk((float)n64.x, (float)n64.y, (float)n64.z);
+                            sph_hit = true;
+                        }
+                    }
                     if constexpr (kTex) sphere_uv(outward, hu, hv);
                 }
-                const bool front = box_hit ? box_front : dot(d, outward) < (R)0;
+                bool front = box_hit ? box_front : dot(d, outward) < (R)0;
+                if constexpr (kHit64) {
+                    if (sph_hit) {                                 // the f64 front face and normal
+                        front = front64(d64, n64);
+                        if (!front) n64 = -n64;
+                    }
+                }
                 const V3<R> nrm = front ? outward : -outward;
                 // Material::emitted: DiffuseLight's colour (material.rs:508-514),
                 // black for every other material (material.rs:42-44)
@@ -1332,32 +1533,52 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? RTW_WAVES : 1) render
                 const V3<R> emitted = mtype == kMatDiffuseLight ? colour : zero;
                 if (mtype == kMatMetal) {
                     // Metal::scatter, material.rs:407-421
-                    V3<R> refl = reflect(PR::normalize(d), nrm);
-                    V3<R> dir = refl + unit_sphere<R>(g) * mp.w;
-                    if (!(dot(dir, nrm) > (R)0)) {
+                    V3<R> dir;
+                    bool keep;
+                    if (kHit64 && sph_hit) {
+                        const V3<R> us = unit_sphere<R>(g);
+                        d64 = metal_dir64(d64, n64, (double)mp.w, dither64(us), keep);
+                        dir = from64<R>(d64);
+                    } else {
+                        V3<R> refl = reflect(PR::normalize(d), nrm);
+                        dir = refl + unit_sphere<R>(g) * mp.w;
+                        keep = dot(dir, nrm) > (R)0;
+                        if constexpr (kHit64) d64 = dither64(dir);
+                    }
+                    if (!keep) {
                         col = mult * emitted + res;
                         done = true;
                     } else {
                         mult = mult * mk(mp.x, mp.y, mp.z);            // Reflect, camera.rs:488-500
                         o = pnt;
                         self_s = next_self;
+                        self_iso = next_iso;
+                        if constexpr (kHit64) o64 = pnt64;
                         d = dir;
                     }
                 } else if (mtype == kMatDielectric) {
                     // Dialectric::scatter, material.rs:458-487
-                    R ratio = front ? PR::div_((R)1, mp.w) : mp.w;
-                    V3<R> unit = PR::normalize(d);
-                    R cos_t = PR::min_(dot(unit, -nrm), (R)1);
-                    R sin_t = PR::sqrt_((R)1 - cos_t * cos_t);
-                    bool cannot = ratio * sin_t > (R)1;
                     V3<R> dir;
-                    if (cannot || reflectance(cos_t, ratio) > PR::u_open01(g.next()))
-                        dir = reflect(unit, nrm);
-                    else
-                        dir = refract(unit, nrm, ratio);
+                    if (kHit64 && sph_hit) {
+                        d64 = dielectric_dir64(d64, n64, front, (double)mp.w, g);
+                        dir = from64<R>(d64);
+                    } else {
+                        R ratio = front ? PR::div_((R)1, mp.w) : mp.w;
+                        V3<R> unit = PR::normalize(d);
+                        R cos_t = PR::min_(dot(unit, -nrm), (R)1);
+                        R sin_t = PR::sqrt_((R)1 - cos_t * cos_t);
+                        bool cannot = ratio * sin_t > (R)1;
+                        if (cannot || reflectance(cos_t, ratio) > PR::u_open01(g.next()))
+                            dir = reflect(unit, nrm);
+                        else
+                            dir = refract(unit, nrm, ratio);
+                        if constexpr (kHit64) d64 = dither64(dir);
+                    }
                     // mult * Colour(1, 1, 1) is the identity on every value
                     o = pnt;
                     self_s = next_self;
+                    self_iso = next_iso;
+                    if constexpr (kHit64) o64 = pnt64;
                     d = dir;
                 } else if (mtype == kMatLambertian) {
                     // Lambertian + MixturePdf(HittablePdf(lights), CosinePdf):
@@ -1392,19 +1613,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? RTW_WAVES : 1) render
                     } else {
                         dir = uvw.transform(cosine_hemisphere<R>(g));
                     }
-#if RTW_EXP == 4
-                    {
-                        Rng g2 = g;
-                        V3<R> dir2;
-                        if (PR::u_std(g2.next()) < (R)0.5) {
-                            const R4<R> L = li[g2.index(p.sc.n_lights)];
-                            dir2 = sphere_random(mk(L.x, L.y, L.z), L.w, pnt, g2);
-                        } else {
-                            dir2 = uvw.transform(cosine_hemisphere<R>(g2));
-                        }
-                        segs += dir2.x == (R)-7 ? 1u : 0u;
-                    }
-#endif
+                    RTW_PROBE_LAMBERT_DIR();
                     const V3<R> ndir = PR::normalize(dir);
                     const R cos_w = PR::over_pi(dot(ndir, uvw.w));
                     R acc;                                                // hittable_list.rs:408-412
@@ -1419,17 +1628,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? RTW_WAVES : 1) render
                         acc = lights_pdf_sum_pk<kRobust>(li, l_lp, p.sc.n_lights, pnt, dir);
                     else
                         acc = lights_pdf_sum<kRobust>(li, p.sc.n_lights, pnt, dir);
-#if RTW_EXP == 2 || RTW_EXP == 7
-                    // 2: along a permuted direction; 7: the same direction again
-                    if constexpr (kLightBvh)
-                        segs += (p.light_bvh == 2
-                                     ? lights_pdf_grid<kRobust>(p.sc, pnt, RTW_EXP == 7 ? dir : mk(dir.y, dir.z, dir.x))
-                                     : lights_pdf_bvh<kRobust>(p.sc, pnt, RTW_EXP == 7 ? dir : mk(dir.y, dir.z, dir.x),
-                                                               reinterpret_cast<int32_t*>(smem) + wave * p.stack * 64 +
-                                                                   lane)) == (R)-7 ? 1u : 0u;
-                    else
-                        segs += lights_pdf_sum<kRobust>(li, p.sc.n_lights, pnt, mk(dir.y, dir.z, dir.x)) == (R)-7 ? 1u : 0u;
-#endif
+                    RTW_PROBE_LIGHT_PDF();
                     // / len; a BVH leaf list multiplies by len and divides again (bvh.rs:67-76, 191-194)
                     R lpdf = PR::div_(acc, (R)p.sc.n_list);
                     if (p.sc.light_flags & 1u) lpdf = PR::div_(lpdf * (R)p.sc.n_list, (R)p.sc.n_list);
@@ -1441,6 +1640,11 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? RTW_WAVES : 1) render
                     mult = new_mult;
                     o = pnt;
                     self_s = next_self;
+                    self_iso = next_iso;
+                    if constexpr (kHit64) {
+                        o64 = pnt64;
+                        d64 = dither64(dir);
+                    }
                     d = dir;
                 } else {
                     // Invisible (material.rs:321-325): scatter() == None
@@ -1459,13 +1663,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? RTW_WAVES : 1) render
                 part = part + col;
                 ++s;
                 if (s < s_end) {
-#if RTW_EXP == 3
-                    {
-                        Rng g2;
-                        g2.seed(p.seed ^ 0x55u, pix, s);
-                        segs += (g2.next() & 0xfffu) == 7u ? 1u : 0u;
-                    }
-#endif
+                    RTW_PROBE_SEED();
                     start_sample();
                 } else {
                     R* dst = p.partial + (((size_t)c * p.n_local_tiles + my_lt) * 64 + px) * 3;
@@ -1496,29 +1694,55 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? RTW_WAVES : 1) render
 }
 
 // Fold the chunk sums of every pixel in chunk order and write the rank's
-// packed rows: out[(tr * 8 + ly) * W + i][3].
+// packed tiles: out[(lt * 64 + px) * 3], px = ly * 8 + lx (pixels outside the
+// image: 0).  The fold accumulates in double whatever R is: with many chunks
+// (C4: 4096 spp) an f32 running sum would lose low bits; in f64 mode this is
+// the reference's sequential f64 fold (camera.rs:323-335).
 template <typename R>
 __global__ void __launch_bounds__(256) reduce_chunks_kernel(const KParams<R> p, R* __restrict__ out) {
     const uint32_t gid = blockIdx.x * 256 + threadIdx.x;
     const uint32_t lt = gid >> 6, lane = gid & 63;
     if (lt >= p.n_local_tiles) return;
-    const uint32_t tr = lt / p.tiles_x, tx = lt - tr * p.tiles_x;
-    const uint32_t ty = tr * p.nranks + p.rank;
-    const uint32_t i = tx * kTile + (lane & 7), ly = lane >> 3, j = ty * kTile + ly;
-    if (i >= p.W || j >= p.H) return;
-    R sx = 0, sy = 0, sz = 0;
-    const size_t stride = (size_t)p.n_local_tiles * 64 * 3;
-    const R* src = p.partial + ((size_t)lt * 64 + lane) * 3;
-    for (uint32_t c = 0; c < p.n_chunks; ++c) {
-        sx = sx + src[0];
-        sy = sy + src[1];
-        sz = sz + src[2];
-        src += stride;
+    const uint32_t T = lt * p.nranks + p.rank;
+    const uint32_t ty = T / p.tiles_x, tx = T - ty * p.tiles_x;
+    const uint32_t i = tx * kTile + (lane & 7), j = ty * kTile + (lane >> 3);
+    double sx = 0, sy = 0, sz = 0;
+    if (i < p.W && j < p.H) {
+        const size_t stride = (size_t)p.n_local_tiles * 64 * 3;
+        const R* src = p.partial + ((size_t)lt * 64 + lane) * 3;
+        for (uint32_t c = 0; c < p.n_chunks; ++c) {
+            sx = sx + (double)src[0];
+            sy = sy + (double)src[1];
+            sz = sz + (double)src[2];
+            src += stride;
+        }
     }
-    R* dst = out + ((size_t)(tr * kTile + ly) * p.W + i) * 3;
-    dst[0] = sx;
-    dst[1] = sy;
-    dst[2] = sz;
+    R* dst = out + ((size_t)lt * 64 + lane) * 3;
+    dst[0] = (R)sx;
+    dst[1] = (R)sy;
+    dst[2] = (R)sz;
+}
+
+// Un-interleave the ranks' packed tiles into the image [H][W][3]: one thread
+// per pixel slot of every global tile T (rank T % nranks, its local tile
+// T / nranks).  ranks = nranks buffers, rank_stride elements apart.
+template <typename R>
+__global__ void __launch_bounds__(256) assemble_tiles_kernel(const R* __restrict__ ranks, size_t rank_stride,
+                                                             uint32_t nranks, uint32_t W, uint32_t H,
+                                                             uint32_t tiles_x, uint32_t n_tiles,
+                                                             R* __restrict__ img) {
+    const uint32_t gid = blockIdx.x * 256 + threadIdx.x;
+    const uint32_t T = gid >> 6, lane = gid & 63;
+    if (T >= n_tiles) return;
+    const uint32_t ty = T / tiles_x, tx = T - ty * tiles_x;
+    const uint32_t i = tx * kTile + (lane & 7), j = ty * kTile + (lane >> 3);
+    if (i >= W || j >= H) return;
+    const uint32_t k = T % nranks, lt = T / nranks;
+    const R* src = ranks + k * rank_stride + ((size_t)lt * 64 + lane) * 3;
+    R* dst = img + ((size_t)j * W + i) * 3;
+    dst[0] = src[0];
+    dst[1] = src[1];
+    dst[2] = src[2];
 }
 
 }  // namespace dev
@@ -1579,14 +1803,7 @@ template <typename R>
 inline int launch_render_impl(const KParams<R>& p, int world, size_t lds_bytes, R* out,
                               hipStream_t stream, hipEvent_t mid) {
     uint32_t blocks = (p.n_tasks + kWavesPerBlock - 1) / kWavesPerBlock;
-    if (p.persist) {
-        blocks = blocks < p.persist ? blocks : p.persist;   // resident-size grid, tasks from the counter
-    } else if (p.xcd == 2 && p.tiles_x) {
-        // 8 XCD lanes of blocks, each as long as the longest XCD task list
-        const uint32_t ltr = p.n_local_tiles / p.tiles_x;
-        const uint32_t longest = (ltr + 7u) / 8u * p.tiles_x * p.n_groups;
-        blocks = 8u * ((longest + kWavesPerBlock - 1) / kWavesPerBlock);
-    }
+    if (p.persist) blocks = blocks < p.persist ? blocks : p.persist;   // resident-size grid, tasks from the counter
     if (blocks) {
         const bool robust = sizeof(R) == 4 && p.sc.robust;
         const bool lbvh = p.light_bvh != 0;
@@ -1611,10 +1828,18 @@ inline int launch_render_impl(const KParams<R>& p, int world, size_t lds_bytes, 
                 else if (lbvh) launch_world<R, Pr | dev::kOptLightBvh>(p, world, lds_bytes, blocks, stream);
                 else launch_world<R, Pr>(p, world, lds_bytes, blocks, stream);
             } else {
-                if (robust && lbvh) launch_world<R, dev::kOptRobust | dev::kOptLightBvh>(p, world, lds_bytes, blocks, stream);
-                else if (robust) launch_world<R, dev::kOptRobust>(p, world, lds_bytes, blocks, stream);
-                else if (lbvh) launch_world<R, dev::kOptLightBvh>(p, world, lds_bytes, blocks, stream);
-                else launch_world<R, 0>(p, world, lds_bytes, blocks, stream);
+                constexpr int H = dev::kOptHit64;
+                if (p.hit64) {
+                    if (robust && lbvh) launch_world<R, H | dev::kOptRobust | dev::kOptLightBvh>(p, world, lds_bytes, blocks, stream);
+                    else if (robust) launch_world<R, H | dev::kOptRobust>(p, world, lds_bytes, blocks, stream);
+                    else if (lbvh) launch_world<R, H | dev::kOptLightBvh>(p, world, lds_bytes, blocks, stream);
+                    else launch_world<R, H>(p, world, lds_bytes, blocks, stream);
+                } else {
+                    if (robust && lbvh) launch_world<R, dev::kOptRobust | dev::kOptLightBvh>(p, world, lds_bytes, blocks, stream);
+                    else if (robust) launch_world<R, dev::kOptRobust>(p, world, lds_bytes, blocks, stream);
+                    else if (lbvh) launch_world<R, dev::kOptLightBvh>(p, world, lds_bytes, blocks, stream);
+                    else launch_world<R, 0>(p, world, lds_bytes, blocks, stream);
+                }
             }
         } else {
             (void)robust;
@@ -1629,6 +1854,19 @@ inline int launch_render_impl(const KParams<R>& p, int world, size_t lds_bytes, 
     if (rblocks) {
         hipLaunchKernelGGL((dev::reduce_chunks_kernel<R>), dim3(rblocks), dim3(256), 0, stream, p,
                            out);
+        if (hipGetLastError() != hipSuccess) return -1;
+    }
+    return 0;
+}
+
+template <typename R>
+inline int launch_assemble_impl(const R* ranks, size_t rank_stride, uint32_t nranks, uint32_t W, uint32_t H,
+                                R* img, hipStream_t stream) {
+    const uint32_t tiles_x = (W + kTile - 1) / kTile, n_tiles = tiles_x * ((H + kTile - 1) / kTile);
+    const uint32_t blocks = (uint32_t)(((uint64_t)n_tiles * 64 + 255) / 256);
+    if (blocks) {
+        hipLaunchKernelGGL((dev::assemble_tiles_kernel<R>), dim3(blocks), dim3(256), 0, stream, ranks, rank_stride,
+                           nranks, W, H, tiles_x, n_tiles, img);
         if (hipGetLastError() != hipSuccess) return -1;
     }
     return 0;

@@ -98,6 +98,8 @@ struct DevScene {
     const R* quads;                   // n_quads x kQuadR (see quad layout below)
     const uint32_t* quad_mat;
     const R* lquads;                  // the light list's quads, n_lquads x kQuadR
+    const R4<double>* sph64;          // spheres {cx, cy, cz, radius} as given (f64): the f32
+                                      // kernels' f64 hit points (kOptHit64)
     const uint32_t* lref;             // light list in order (kLref* bits | index; null when the
                                       // list is spheres only)
     const R* boxes;                   // n_boxes x kBoxR (transformed cuboids, layout below)
@@ -161,12 +163,12 @@ struct KParams {
     uint32_t W, H, spp, max_depth;
     uint32_t chunk, n_chunks;         // samples per item, items per pixel
     uint32_t group, n_groups;         // chunks per wave task, tasks per tile
-    uint32_t tiles_x, n_local_tiles, rank, nranks;
+    uint32_t tiles_x, n_local_tiles, rank, nranks;   // local tile lt = global tile lt * nranks + rank
     uint32_t n_tasks;                 // n_local_tiles * n_groups
     uint32_t stack;                   // BVH traversal stack entries per lane (LDS)
     uint32_t light_bvh;               // light pdf (BVH kernels only): 1 through sc.lbvh, 2 the light grid
-    uint32_t xcd;                     // 1: XCD-aware workgroup -> task mapping
     uint32_t item_order;              // 0: pixel-major item pool, 1: sample-major
+    uint32_t hit64;                   // f32 BVH kernels: f64 ray origin / own-sphere re-hit / hit point
     uint32_t persist;                 // > 0: workgroups launched (waves take tasks from
                                       // counters[6]); 0: one task per wave
 };
@@ -179,5 +181,11 @@ int launch_render_f32(const KParams<float>& p, int world, size_t lds_bytes, floa
                       hipStream_t stream, hipEvent_t mid);
 int launch_render_f64(const KParams<double>& p, int world, size_t lds_bytes, double* out,
                       hipStream_t stream, hipEvent_t mid);
+// The ranks' packed tiles (nranks buffers, rank_stride elements apart) -> the
+// image [H][W][3] (rtw_assemble_tiles).
+int launch_assemble_f32(const float* ranks, size_t rank_stride, uint32_t nranks, uint32_t W, uint32_t H,
+                        float* img, hipStream_t stream);
+int launch_assemble_f64(const double* ranks, size_t rank_stride, uint32_t nranks, uint32_t W, uint32_t H,
+                        double* img, hipStream_t stream);
 
 }  // namespace rtw

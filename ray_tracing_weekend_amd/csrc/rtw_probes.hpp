@@ -1,0 +1,137 @@
+// rtw_probes.hpp -- experiment-only hooks of the render kernel (never in the
+// product build: render_kernel.hpp includes this file only when RTW_EXP or
+// RTW_TRACE is defined; otherwise every RTW_PROBE_* hook is empty).
+//
+// RTW_EXP (tools/exp_cost.sh): repeat one part of the per-segment work so that
+// the time difference prices it.  1 = closest-hit query, 2 = light pdf sum,
+// 3 = stream seeding, 4 = Lambertian direction sampling, 5 = plane tests,
+// 6 = closest-hit query along another direction, 7 = light pdf sum along the
+// same direction.  The repeated work feeds a comparison that never holds, so
+// the compiler keeps it.
+//
+// RTW_TRACE (tools/trace_paths.py): record every segment of the first
+// kTraceSamples samples of one pixel -- the ray (origin, direction) and the
+// closest hit (object id, t) -- into a device array the tool reads back with
+// rtw_probe_trace_read_f32 / _f64 (exported by the trace build only).
+#pragma once
+
+#ifndef RTW_EXP
+#define RTW_EXP 0
+#endif
+
+#if RTW_EXP == 5
+#define RTW_PROBE_PLANES() \
+    do { \
+        for (int32_t k = 0; k < nplanes; ++k) { \
+            R t; \
+            const R* pl = p.sc.planes + kPlaneR * k; \
+            if (aabb_hit_ref(pl + 6, pl + 9, o, mk(d.y, d.x, d.z), tmin) && \
+                plane_t(pl, o, mk(d.y, d.x, d.z), tmin, t, nullptr) && t == (R)-7) \
+                ++segs; \
+        } \
+    } while (0)
+#else
+#define RTW_PROBE_PLANES()
+#endif
+
+#if RTW_EXP == 1 || RTW_EXP == 6
+#define RTW_PROBE_CLOSEST() \
+    do { \
+        { \
+            R tb2 = tb; \
+            int32_t best2 = best; \
+            const V3<R> d2 = RTW_EXP == 6 ? mk(d.z, d.x, d.y) : d; \
+            bvh_closest<kWorld == kWorldBvhLds ? kWorldBvhWW : kWorld, kRobust>(scw, sbase, o, d2, tmin, tb2, best2, \
+                                reinterpret_cast<int32_t*>(smem) + wave * p.stack * 64 + lane, nvis, \
+                                ntest, self_s); \
+            segs += best2 == -7 ? 1u : 0u; \
+        } \
+    } while (0)
+#else
+#define RTW_PROBE_CLOSEST()
+#endif
+
+#if RTW_EXP == 4
+#define RTW_PROBE_LAMBERT_DIR() \
+    do { \
+        { \
+            Rng g2 = g; \
+            V3<R> dir2; \
+            if (PR::u_std(g2.next()) < (R)0.5) { \
+                const R4<R> L = li[g2.index(p.sc.n_lights)]; \
+                dir2 = sphere_random(mk(L.x, L.y, L.z), L.w, pnt, g2); \
+            } else { \
+                dir2 = uvw.transform(cosine_hemisphere<R>(g2)); \
+            } \
+            segs += dir2.x == (R)-7 ? 1u : 0u; \
+        } \
+    } while (0)
+#else
+#define RTW_PROBE_LAMBERT_DIR()
+#endif
+
+#if RTW_EXP == 2 || RTW_EXP == 7
+#define RTW_PROBE_LIGHT_PDF() \
+    do { \
+        if constexpr (kLightBvh) \
+            segs += (p.light_bvh == 2 \
+                         ? lights_pdf_grid<kRobust>(p.sc, pnt, RTW_EXP == 7 ? dir : mk(dir.y, dir.z, dir.x)) \
+                         : lights_pdf_bvh<kRobust>(p.sc, pnt, RTW_EXP == 7 ? dir : mk(dir.y, dir.z, dir.x), \
+                                                   reinterpret_cast<int32_t*>(smem) + wave * p.stack * 64 + \
+                                                       lane)) == (R)-7 ? 1u : 0u; \
+        else \
+            segs += lights_pdf_sum<kRobust>(li, p.sc.n_lights, pnt, mk(dir.y, dir.z, dir.x)) == (R)-7 ? 1u : 0u; \
+    } while (0)
+#else
+#define RTW_PROBE_LIGHT_PDF()
+#endif
+
+#if RTW_EXP == 3
+#define RTW_PROBE_SEED() \
+    do { \
+        { \
+            Rng g2; \
+            g2.seed(p.seed ^ 0x55u, pix, s); \
+            segs += (g2.next() & 0xfffu) == 7u ? 1u : 0u; \
+        } \
+    } while (0)
+#else
+#define RTW_PROBE_SEED()
+#endif
+
+#ifdef RTW_TRACE
+// build with -DRTW_TRACE=f32 (render_f32.hip) / -DRTW_TRACE=f64 (render_f64.hip):
+// each instantiation unit keeps its own trace array and exports its reader
+// (this header is included inside namespace rtw::dev)
+constexpr uint32_t kTraceSamples = 64, kTraceSegs = 64, kTraceRec = 8;
+static __device__ double g_trace[kTraceSamples * kTraceSegs * kTraceRec];
+static __device__ unsigned long long g_trace_pix = ~0ull;
+#define RTW_CAT2(a, b) a##b
+#define RTW_CAT(a, b) RTW_CAT2(a, b)
+// set the traced pixel (j * W + i) and clear the array / copy it out (n doubles)
+extern "C" int RTW_CAT(rtw_probe_trace_set_, RTW_TRACE)(unsigned long long pix) {
+    static double zero[kTraceSamples * kTraceSegs * kTraceRec];
+    for (auto& z : zero) z = -2.0;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_trace), zero, sizeof zero) != hipSuccess) return -1;
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_trace_pix), &pix, sizeof pix) == hipSuccess ? 0 : -1;
+}
+extern "C" int RTW_CAT(rtw_probe_trace_read_, RTW_TRACE)(double* out, size_t n) {
+    n = n < (size_t)kTraceSamples * kTraceSegs * kTraceRec
+            ? n : (size_t)kTraceSamples * kTraceSegs * kTraceRec;
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_trace), n * sizeof(double)) == hipSuccess ? (int)n : -1;
+}
+// {object id (-1 miss), t, origin xyz, direction xyz} of segment max_depth - depth
+#define RTW_PROBE_SEGMENT() \
+    do { \
+        if (pix == g_trace_pix && s < kTraceSamples && p.max_depth - depth < kTraceSegs) { \
+            double* rec = g_trace + ((size_t)s * kTraceSegs + (p.max_depth - depth)) * kTraceRec; \
+            double t64 = (double)tb, ox = (double)o.x, oy = (double)o.y, oz = (double)o.z; \
+            if constexpr (kHit64) { t64 = tb64; ox = o64.x; oy = o64.y; oz = o64.z; } \
+            rec[0] = (double)best; rec[1] = t64; rec[2] = ox; rec[3] = oy; rec[4] = oz; \
+            rec[5] = (double)d.x; rec[6] = (double)d.y; rec[7] = (double)d.z; \
+        } \
+    } while (0)
+#else
+#define RTW_PROBE_SEGMENT()
+#endif

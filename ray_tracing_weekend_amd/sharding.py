@@ -1,13 +1,17 @@
-"""Row-tile sharding of one image over ranks.
+"""Tile sharding of one image over ranks.
 
-The image is cut into 8-row tile rows; tile row ``t`` belongs to rank
-``t % nranks`` (sky rows are cheap and sphere rows expensive, so interleaving
-balances the ranks).  Each rank's ``rtw_render_device`` output holds its rows
-packed in increasing order; rank 0 gathers the packed buffers (one RCCL
-gather) and scatters them back into image rows with one indexed copy per rank.
+The image is cut into 8x8 tiles T = ty * tiles_x + tx (row j = 0 at the
+bottom); tile T belongs to rank T % nranks.  The interleave is fine-grained, so
+every rank samples the image's whole cost profile (sky tiles are cheap, tiles
+over the sphere field expensive) and the ranks' shares cost the same.  Each
+rank's ``rtw_render_device`` output holds its tiles packed (the k-th tile at
+``[k * 64 + ly * 8 + lx]``); rank 0 gathers the equal-size packed buffers (one
+RCCL gather) and un-interleaves them on the device with ``rtw_assemble_tiles``.
 
-This is the host side of the only exchange step of the path -- the reference
-renders on one host (``camera.rs:315-388``), so it has no counterpart there.
+This module is the torch restatement of that layout: the index maps, and an
+``assemble`` that the CPU tests (gloo) and the GPU test of the native
+assembler use as the reference.  The reference renders on one host
+(``camera.rs:315-388``), so this exchange step has no counterpart there.
 """
 from __future__ import annotations
 
@@ -15,30 +19,61 @@ import functools
 
 import torch
 
-TILE_ROWS = 8      # == rtw_tile_rows() == kTile in csrc/rtw_kernels.h
+TILE = 8      # == rtw_tile_size() == kTile in csrc/rtw_kernels.h
 
 
-def rank_rows(height: int, rank: int, nranks: int, tile: int = TILE_ROWS) -> list[int]:
-    """Image rows (j index, 0 = bottom) that ``rank`` renders, in the order
-    they are packed in its output buffer."""
+def n_tiles(width: int, height: int, tile: int = TILE) -> int:
+    return ((width + tile - 1) // tile) * ((height + tile - 1) // tile)
+
+
+def tiles_for_rank(width: int, height: int, rank: int, nranks: int) -> int:
+    """Number of tiles ``rank`` renders (== rtw_tiles_for_rank)."""
     if nranks < 1 or not 0 <= rank < nranks:
         raise ValueError(f"bad rank {rank} of {nranks}")
-    rows = []
-    for t in range(rank, (height + tile - 1) // tile, nranks):
-        rows.extend(range(t * tile, min(height, (t + 1) * tile)))
-    return rows
+    n = n_tiles(width, height)
+    return (n - rank + nranks - 1) // nranks if rank < n else 0
+
+
+def rank_tiles(width: int, height: int, rank: int, nranks: int) -> list[int]:
+    """Global tile ids of ``rank`` in the order they are packed."""
+    return list(range(rank, n_tiles(width, height), nranks)) if tiles_for_rank(width, height, rank, nranks) else []
 
 
 @functools.lru_cache(maxsize=64)
-def _index(height: int, rank: int, nranks: int, device: str) -> torch.Tensor:
-    return torch.tensor(rank_rows(height, rank, nranks), dtype=torch.long, device=device)
+def _maps(width: int, height: int, rank: int, nranks: int, device: str):
+    """(slots, pixels): for every in-image pixel of the rank's packed tiles,
+    its slot in the packed buffer and its index in the flattened image."""
+    tiles_x = (width + TILE - 1) // TILE
+    t = torch.tensor(rank_tiles(width, height, rank, nranks), dtype=torch.long)
+    lane = torch.arange(64, dtype=torch.long)
+    i = (t % tiles_x)[:, None] * TILE + (lane % TILE)[None, :]
+    j = (t // tiles_x)[:, None] * TILE + (lane // TILE)[None, :]
+    slot = torch.arange(t.numel() * 64, dtype=torch.long).view(-1, 64)
+    ok = (i < width) & (j < height)
+    return slot[ok].to(device), (j * width + i)[ok].to(device)
 
 
-def assemble(image: torch.Tensor, gathered, height: int) -> torch.Tensor:
-    """Scatter the ranks' packed row buffers ``gathered[k]`` (shape
-    ``[>= rows of rank k, W, 3]``) into ``image`` (``[height, W, 3]``)."""
+def pack(image: torch.Tensor, rank: int, nranks: int) -> torch.Tensor:
+    """The rank's packed tile buffer ``[tiles * 64, 3]`` cut out of a full
+    image ``[H, W, 3]`` (pixels outside the image: 0) -- what
+    rtw_render_device writes for that rank."""
+    height, width = image.shape[:2]
+    slots, pix = _maps(width, height, rank, nranks, str(image.device))
+    out = torch.zeros((tiles_for_rank(width, height, rank, nranks) * 64, 3), dtype=image.dtype,
+                      device=image.device)
+    out[slots] = image.reshape(-1, 3)[pix]
+    return out
+
+
+def assemble(image: torch.Tensor, gathered, height: int | None = None) -> torch.Tensor:
+    """Scatter the ranks' packed tile buffers ``gathered[k]`` (each at least
+    ``tiles_for_rank(W, H, k, N) * 64 * 3`` elements) into ``image``
+    (``[H, W, 3]``); the torch restatement of rtw_assemble_tiles."""
+    h, width = image.shape[:2]
+    height = h if height is None else height
     nranks = len(gathered)
+    flat = image.view(-1, 3)
     for k, buf in enumerate(gathered):
-        idx = _index(height, k, nranks, str(image.device))
-        image.index_copy_(0, idx, buf[: idx.numel()])
+        slots, pix = _maps(width, height, k, nranks, str(image.device))
+        flat.index_copy_(0, pix, buf.reshape(-1, 3)[slots])
     return image

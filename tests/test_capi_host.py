@@ -4,6 +4,7 @@ scenes::simple, output encoding) agrees with the oracle restatement; nothing
 here launches a kernel."""
 import ctypes as C
 import os
+import math
 import re
 
 import numpy as np
@@ -32,7 +33,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert rtw._lib.rtw_abi_version() == rtw._capi.ABI_VERSION == 5
+    assert rtw._lib.rtw_abi_version() == rtw._capi.ABI_VERSION == 6
 
 
 def test_camera_builder_defaults_match_reference():
@@ -141,6 +142,67 @@ def test_encode_rgb8_matches_write_colour():
         j = 1 - r
         for i in range(2):
             assert list(out[r, i]) == [ref(x) for x in sums[j, i]]
+
+
+def _write_colour(x, spp):
+    """colour.rs:14-36 restated in Python floats (IEEE f64): scale =
+    (spp as f64).recip(); (256 * sqrt(x * scale).clamp(0, 1)) as u8 (Rust's
+    float -> u8 cast saturates, NaN -> 0)."""
+    scale = 1.0 / float(spp)
+    v = math.sqrt(x * scale) if x * scale >= 0 else math.nan
+    if v != v:
+        return 0
+    t = 256.0 * min(max(v, 0.0), 1.0)
+    return 255 if t >= 255 else int(t)
+
+
+def _boundary_cases(spp, limit=40):
+    """sums next to an encoder step k/256 where x * (1/spp) and x / spp round
+    to different u8 -- they pin the reciprocal multiply of colour.rs:24."""
+    out = []
+    for k in range(1, 256):
+        x0 = spp * (k / 256) ** 2
+        for direction in (-np.inf, np.inf):
+            x = x0
+            for _ in range(limit):
+                x = float(np.nextafter(x, direction))
+                if _write_colour(x, spp) != min(255, int(256 * min(1.0, math.sqrt(x / spp)))):
+                    out.append(x)
+    return out
+
+
+@pytest.mark.parametrize("spp", [3, 100, 500])
+def test_encode_rgb8_values_pin_the_recip_multiply(spp):
+    """Random sums and sums at the u8 step boundaries, at spp 3 / 100 / 500;
+    at spp 3 and 500 there are sums where sum * (1/spp) and sum / spp encode
+    differently, and the encoder must follow the reference's recip."""
+    rng = np.random.default_rng(spp)
+    vals = list(rng.uniform(0, 1.2 * spp, 3000)) + list(rng.uniform(0, 0.01 * spp, 3000))
+    edge = _boundary_cases(spp)
+    if spp in (3, 500):
+        assert edge, "expected sums that tell x*(1/spp) from x/spp apart"
+    vals = np.array((vals + edge + [0.0, -1.0, np.nan, np.inf, spp * 1.0])[: 3 * ((len(vals) + len(edge) + 5) // 3)])
+    vals = np.concatenate([vals, np.zeros((-len(vals)) % 3)])
+    sums = vals.reshape(1, -1, 3)
+    out = rtw.encode_rgb8(sums, spp)
+    want = np.array([_write_colour(x, spp) for x in vals], np.uint8).reshape(1, -1, 3)
+    np.testing.assert_array_equal(out, want)
+
+
+def test_encode_rgb8_f32_sums_widen_exactly():
+    """A speed-mode (f32) framebuffer encodes as its exact f64 values would."""
+    rng = np.random.default_rng(5)
+    sums = rng.uniform(-1, 600, (7, 9, 3)).astype(np.float32)
+    sums[0, 0] = [np.nan, np.inf, 0.0]
+    np.testing.assert_array_equal(rtw.encode_rgb8(sums, 500), rtw.encode_rgb8(sums.astype(np.float64), 500))
+
+
+def test_write_ppm_f32_matches_f64(tmp_path):
+    sums = np.random.default_rng(6).uniform(0, 120, (5, 4, 3)).astype(np.float32)
+    a, b = tmp_path / "a.ppm", tmp_path / "b.ppm"
+    rtw.write_ppm(str(a), sums, 100)
+    rtw.write_ppm(str(b), sums.astype(np.float64), 100)
+    assert a.read_bytes() == b.read_bytes()
 
 
 def test_write_ppm_layout(tmp_path):

@@ -174,30 +174,48 @@ def test_mixed_materials_custom_scene():
 
 
 def test_rank_sharding_reassembles_the_image():
-    """rtw_render_device over 3 ranks (interleaved 8-row tile rows) == one full render."""
+    """rtw_render_device over 3 ranks (8x8 tiles, T -> rank T % 3), gathered
+    into one buffer and un-interleaved by rtw_assemble_tiles == one full render
+    (f64, ragged edge tiles: 50x45); the torch restatement
+    (sharding.assemble) gives the same image."""
     import torch
+    from ray_tracing_weekend_amd import sharding
     soa, b = _scene()
     cam = b.with_image_width(50).with_image_height(45).with_samples_per_pixel(3).with_max_depth(20).build()
-    H, W = 45, 50
+    H, W, N = 45, 50, 3
     full, _, _ = _render_gpu(soa, cam, 9, rtw.RTW_F64)
-    parts = []
     with rtw.Renderer(precision=rtw.RTW_F64) as r:
         r.set_scene(soa)
-        for rank in range(3):
-            rows = rtw.rows_for_rank(H, rank, 3)
-            buf = torch.zeros((rows, W, 3), dtype=torch.float64, device="cuda:0")
-            r.render_device(cam, 9, buf.data_ptr(), buf.numel() * 8, rank=rank, nranks=3)
-            torch.cuda.synchronize()
-            parts.append(buf.cpu().numpy())
-    img = np.zeros((H, W, 3))
-    t = rtw.tile_rows()
-    for rank in range(3):
-        pos = 0
-        for ty in range(rank, (H + t - 1) // t, 3):
-            n = min(t, H - ty * t)
-            img[ty * t: ty * t + n] = parts[rank][pos: pos + n]
-            pos += n
-    assert np.array_equal(np.nan_to_num(img, nan=-7), np.nan_to_num(full, nan=-7))
+        per = rtw.tiles_for_rank(W, H, 0, N) * 64 * 3
+        ranks = torch.full((N, per), -5.0, dtype=torch.float64, device="cuda:0")
+        for rank in range(N):
+            n = rtw.tiles_for_rank(W, H, rank, N) * 64 * 3
+            r.render_device(cam, 9, ranks[rank].data_ptr(), n * 8, rank=rank, nranks=N)
+        img = torch.full((H, W, 3), -9.0, dtype=torch.float64, device="cuda:0")
+        r.assemble_tiles(ranks.data_ptr(), per * 8, N, W, H, img.data_ptr())
+        ref = torch.full_like(img, -9.0)
+        sharding.assemble(ref, list(ranks.unbind(0)))
+        torch.cuda.synchronize()
+    assert np.array_equal(np.nan_to_num(img.cpu().numpy(), nan=-7), np.nan_to_num(full, nan=-7))
+    assert torch.equal(torch.nan_to_num(img, nan=-7.0), torch.nan_to_num(ref, nan=-7.0))
+    # the packed buffers are what sharding.pack cuts out of the image (padding 0)
+    for rank in range(N):
+        p = sharding.pack(torch.from_numpy(full), rank, N).reshape(-1)
+        got = ranks[rank, : p.numel()].cpu()
+        assert torch.equal(torch.nan_to_num(got, nan=-7.0), torch.nan_to_num(p, nan=-7.0))
+
+
+def test_rank_without_tiles_renders_nothing():
+    """More ranks than tiles: a rank with no tiles accepts a NULL d_out and
+    renders nothing (a 0-element torch buffer has data_ptr 0)."""
+    soa, b = _scene()
+    cam = b.with_image_width(8).with_image_height(8).with_samples_per_pixel(2).with_max_depth(5).build()
+    assert rtw.tiles_for_rank(8, 8, 1, 2) == 0
+    with rtw.Renderer(precision=rtw.RTW_F32) as r:
+        r.set_scene(soa)
+        r.render_device(cam, 3, 0, 0, rank=1, nranks=2)
+        assert r.get_stats().samples == 0
+
 
 
 def test_f32_statistically_matches_f64_oracle():
@@ -684,24 +702,28 @@ def test_c2_full_frame_f64_rows_match_oracle():
 
 @pytest.mark.parametrize("nranks", [2, 8])
 def test_c2_full_frame_rank_split_is_the_single_render(nranks):
-    """rtw_render_device over nranks (the multi-GPU row-tile split, DESIGN.md
-    §7) reassembles the one-rank C2-size image bit for bit (f32)."""
+    """rtw_render_device over nranks (the multi-GPU tile interleave, DESIGN.md
+    §7) + rtw_assemble_tiles reassembles the one-rank C2-size image bit for
+    bit (f32).  Every render runs on torch's current stream, the stream the
+    buffers were filled on."""
     import torch
-    from ray_tracing_weekend_amd import sharding
     soa, b = _scene()
     H, W = 800, 1200
     cam = b.with_image_width(W).with_image_height(H).with_samples_per_pixel(2).with_max_depth(50).build()
+    s = torch.cuda.current_stream().cuda_stream
     with rtw.Renderer(precision=rtw.RTW_F32) as r:
         r.set_scene(soa)
+        one = torch.zeros((rtw.tiles_for_rank(W, H, 0, 1) * 64 * 3,), dtype=torch.float32, device="cuda:0")
+        r.render_device(cam, 109, one.data_ptr(), one.numel() * 4, stream=s)
         full = torch.zeros((H, W, 3), dtype=torch.float32, device="cuda:0")
-        r.render_device(cam, 109, full.data_ptr(), full.numel() * 4)
-        rows_max = max(rtw.rows_for_rank(H, k, nranks) for k in range(nranks))
-        bufs = [torch.zeros((rows_max, W, 3), dtype=torch.float32, device="cuda:0") for _ in range(nranks)]
+        r.assemble_tiles(one.data_ptr(), one.numel() * 4, 1, W, H, full.data_ptr(), stream=s)
+        per = rtw.tiles_for_rank(W, H, 0, nranks) * 64 * 3
+        ranks = torch.zeros((nranks, per), dtype=torch.float32, device="cuda:0")
         for k in range(nranks):
-            r.render_device(cam, 109, bufs[k].data_ptr(), bufs[k].numel() * 4, rank=k, nranks=nranks)
-        torch.cuda.synchronize()
+            r.render_device(cam, 109, ranks[k].data_ptr(), per * 4, rank=k, nranks=nranks, stream=s)
         img = torch.empty_like(full)
-        sharding.assemble(img, bufs, H)
+        r.assemble_tiles(ranks.data_ptr(), per * 4, nranks, W, H, img.data_ptr(), stream=s)
+        torch.cuda.synchronize()
     assert torch.equal(torch.nan_to_num(img, nan=-7.0), torch.nan_to_num(full, nan=-7.0))
 
 
@@ -709,13 +731,12 @@ def test_c2_full_frame_rank_split_is_the_single_render(nranks):
 def test_scheduling_knobs_do_not_change_the_image(prec):
     """The wave item pool order (pixel- / sample-major), persistent waves (one
     workgroup draining every task from the counter, or many) or one task per
-    wave with its XCD task mappings, and the task size only move work between
-    lanes: same image bit for bit."""
+    wave, and the task size only move work between lanes: same image bit for
+    bit."""
     soa, b = _scene()
     cam = b.with_image_width(40).with_image_height(24).with_samples_per_pixel(9).with_max_depth(50).build()
     base, _, cb = _render_gpu(soa, cam, 113, prec)
     for t in ({"item_order": 0}, {"persist": 1}, {"persist": 3, "group": 1}, {"persist": 0},
-              {"persist": 0, "xcd": 1}, {"persist": 0, "xcd": 2}, {"persist": 0, "xcd": 2, "target_tasks": 1000},
-              {"item_order": 0, "target_tasks": 1000}):
+              {"persist": 0, "target_tasks": 1000}, {"item_order": 0, "target_tasks": 1000}):
         img, _, cv = _render_gpu(soa, cam, 113, prec, tuning=t)
         assert _same(base, img) and cb == cv, t

@@ -1,14 +1,18 @@
-"""N > 1 path on CPU: row-tile sharding, the gather to rank 0 and the
-reassembly, with world_size 2 over gloo.
+"""N > 1 path on CPU: tile sharding, the gather to rank 0 and the
+reassembly, over gloo.
 
-Each rank "renders" its rows with a deterministic stand-in f(j, i) (the
-kernel's own sharding is covered on the GPU by
-test_gpu_parity.py::test_rank_sharding_reassembles_the_image); what is tested
-here is the host logic bench.py runs: which rows a rank owns, the packed
-buffer sized by rtw_rows_for_rank, dist.gather, sharding.assemble.
+Each rank "renders" its tiles with a deterministic stand-in f(j, i) packed the
+way rtw_render_device packs them (the kernel's own sharding and the native
+assembler are covered on the GPU by test_gpu_parity.py); what runs here is the
+host logic of bench.py itself -- bench.make_step (render into the packed
+buffer, dist.gather into the rows of one [N, numel] tensor, assemble on rank
+0) and bench.run_steps (warm-up, barriers, timed steps, max over ranks) --
+with sharding.assemble, the torch restatement of rtw_assemble_tiles, in place
+of the device kernel.
 """
 import os
 import socket
+import time
 
 import numpy as np
 import pytest
@@ -26,30 +30,45 @@ def _image(h, w):
     return j * 1000.0 + i + c / 8.0
 
 
-def _tile_owner_rows(h, rank, n, tile=8):
-    # independent statement of the assignment: tile row t -> rank t % n
-    return [j for j in range(h) if (j // tile) % n == rank]
+def _owner(h, w, n):
+    """independent statement of the assignment: pixel (i, j) lies in tile
+    T = (j // 8) * ceil(w / 8) + i // 8, which rank T % n renders"""
+    tx = (w + 7) // 8
+    j, i = np.meshgrid(np.arange(h), np.arange(w), indexing="ij")
+    return ((j // 8) * tx + i // 8) % n
 
 
 def _worker(rank, world, port, h, w, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
+        import bench
         full = torch.from_numpy(_image(h, w))
-        mine = sharding.rank_rows(h, rank, world)
-        max_rows = max(len(sharding.rank_rows(h, k, world)) for k in range(world))
-        buf = torch.full((max_rows, w, 3), -1.0, dtype=torch.float64)
-        buf[: len(mine)] = full[mine]
-        gathered = [torch.empty_like(buf) for _ in range(world)] if rank == 0 else None
-        dist.gather(buf, gathered, dst=0)
-        ok = True
+        max_tiles = sharding.tiles_for_rank(w, h, 0, world)
+        buf = torch.full((max_tiles * 64 * 3,), -1.0, dtype=torch.float64)
+        gathered = torch.empty((world, buf.numel()), dtype=torch.float64) if rank == 0 else None
+        image = torch.full((h, w, 3), np.nan, dtype=torch.float64) if rank == 0 else None
+        seeds = []
+
+        def render(seed, out):          # stand-in for rtw_render_device: this rank's tiles, packed
+            seeds.append(seed)
+            packed = sharding.pack(full, rank, world).reshape(-1)
+            out[: packed.numel()] = packed
+            time.sleep(0.01 * (rank + 1))
+
+        def assemble(ranks, img):       # stand-in for rtw_assemble_tiles
+            sharding.assemble(img, list(ranks.unbind(0)))
+
+        step = bench.make_step(render, assemble, dist, rank, world, buf, gathered, image)
+        elapsed = bench.run_steps(step, 3, 2, dist, lambda: None, device="cpu")
+        ok = seeds == [1000, 1001, 0, 1, 2]
+        # the timed region is the slowest rank's: >= 3 steps x 10 ms x world
+        ok = ok and elapsed >= 0.03 * world * 0.99
         if rank == 0:
-            image = torch.full((h, w, 3), np.nan, dtype=torch.float64)
-            sharding.assemble(image, gathered, h)
-            ok = bool(torch.equal(image, full))
-        t = torch.tensor([len(mine)], dtype=torch.int64)
+            ok = ok and bool(torch.equal(image, full))
+        t = torch.tensor([sharding.tiles_for_rank(w, h, rank, world)], dtype=torch.int64)
         dist.all_reduce(t)
-        ok = ok and int(t) == h
+        ok = ok and int(t) == sharding.n_tiles(w, h)
         q.put((rank, ok))
     finally:
         dist.destroy_process_group()
@@ -61,52 +80,71 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("h,w", [(27, 5), (800, 4), (8, 3)])
-def test_gather_reassembles_image_world2(h, w):
+@pytest.mark.parametrize("world,h,w", [(2, 27, 5), (2, 800, 12), (2, 8, 3), (3, 41, 30)])
+def test_bench_step_gathers_and_reassembles(world, h, w):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, h, w, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, h, w, q)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
         p.join(timeout=120)
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     res = dict(q.get(timeout=5) for _ in procs)
-    assert res == {0: True, 1: True}
+    assert res == {r: True for r in range(world)}
 
 
-@pytest.mark.parametrize("h", [0, 1, 7, 8, 9, 27, 225, 800])
+@pytest.mark.parametrize("h,w", [(0, 5), (1, 1), (7, 9), (8, 8), (9, 17), (27, 5), (225, 400), (800, 1200)])
 @pytest.mark.parametrize("n", [1, 2, 3, 8])
-def test_rank_rows_partition(h, n):
-    rows = [sharding.rank_rows(h, k, n) for k in range(n)]
+def test_rank_tiles_partition(h, w, n):
+    own = _owner(h, w, n)
+    full = torch.from_numpy(_image(h, w))
     for k in range(n):
-        assert rows[k] == _tile_owner_rows(h, k, n)
-    assert sorted(sum(rows, [])) == list(range(h))
+        assert sharding.tiles_for_rank(w, h, k, n) == len(sharding.rank_tiles(w, h, k, n))
+        if h and w:
+            # rank k's packed buffer holds exactly the pixels it owns
+            packed = sharding.pack(full, k, n)
+            vals = set(map(tuple, packed[(packed != 0).any(-1)].tolist()))
+            mine = set(map(tuple, full[torch.from_numpy(own == k)].tolist()))
+            assert vals == mine - {(0.0, 0.125, 0.25)} or vals == mine
+    assert sum(sharding.tiles_for_rank(w, h, k, n) for k in range(n)) == sharding.n_tiles(w, h)
 
 
-@pytest.mark.parametrize("h", [1, 27, 225, 800])
+@pytest.mark.parametrize("h,w", [(1, 1), (27, 5), (225, 400), (800, 1200), (2160, 3840)])
 @pytest.mark.parametrize("n", [1, 2, 3, 8])
-def test_rank_rows_match_c_abi(h, n):
-    from ray_tracing_weekend_amd import rows_for_rank, tile_rows
-    assert tile_rows() == sharding.TILE_ROWS
+def test_tiles_for_rank_match_c_abi(h, w, n):
+    from ray_tracing_weekend_amd import tile_size, tiles_for_rank
+    assert tile_size() == sharding.TILE
     for k in range(n):
-        assert rows_for_rank(h, k, n) == len(sharding.rank_rows(h, k, n))
+        assert tiles_for_rank(w, h, k, n) == sharding.tiles_for_rank(w, h, k, n)
 
 
-def test_assemble_three_ranks_single_process():
-    h, w, n = 41, 6, 3
+def test_pack_assemble_round_trip_single_process():
+    h, w, n = 41, 30, 3
     full = torch.from_numpy(_image(h, w))
     bufs = []
     for k in range(n):
-        r = sharding.rank_rows(h, k, n)
-        b = torch.zeros((24, w, 3), dtype=torch.float64)
-        b[: len(r)] = full[r]
+        p = sharding.pack(full, k, n).reshape(-1)
+        b = torch.zeros(sharding.tiles_for_rank(w, h, 0, n) * 64 * 3, dtype=torch.float64)
+        b[: p.numel()] = p
         bufs.append(b)
     img = torch.empty_like(full)
-    assert torch.equal(sharding.assemble(img, bufs, h), full)
+    assert torch.equal(sharding.assemble(img, bufs), full)
+
+
+def test_c4_shares_balance():
+    """C4 (3840x2160) over 8 ranks: 16 200 tiles each, every rank's tiles spread
+    over the whole image height (the cost profile of the image is sampled)."""
+    w, h, n = 3840, 2160, 8
+    tx = w // 8
+    for k in range(n):
+        t = np.array(sharding.rank_tiles(w, h, k, n))
+        assert len(t) == 16200
+        rows = np.bincount(t // tx, minlength=h // 8)
+        assert rows.min() == rows.max() == tx // n
 
 
 def test_bad_rank_rejected():
     with pytest.raises(ValueError):
-        sharding.rank_rows(10, 2, 2)
+        sharding.tiles_for_rank(10, 10, 2, 2)

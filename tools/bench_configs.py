@@ -51,7 +51,7 @@ def main():
         t0 = time.perf_counter()
         r.set_scene(scene)
         t_stage = time.perf_counter() - t0
-        buf = torch.empty((cfg["h"], cfg["w"], 3), dtype=torch.float32, device="cuda:0")
+        buf = torch.empty((rtw.tiles_for_rank(cfg["w"], cfg["h"], 0, 1) * 64 * 3,), dtype=torch.float32, device="cuda:0")
         r.render_device(cam, 1, buf.data_ptr(), buf.numel() * 4)      # warm-up
         torch.cuda.synchronize()
         t0 = time.perf_counter()

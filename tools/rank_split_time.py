@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""Per-rank render time of the C2 headline split over N ranks, measured on ONE
+"""Per-rank render time of an image split over N ranks (C2 headline by
+default; --size 3840x2160 --spp 4096 for C4 shares), measured on ONE
 GPU (each rank's share rendered in turn with rtw_render_device(rank, nranks)):
 the compute part of the strong-scaling curve the driver's N-GPU bench measures
 (it adds the barrier and the one RCCL gather).  Prints one JSON line per N.
@@ -25,8 +26,12 @@ def main():
     ap.add_argument("--ns", default="1,2,4,8")
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--tuning", default="", help="k=v,... (rtw_set_tuning)")
+    ap.add_argument("--size", default="1200x800", help="WxH (C4: 3840x2160)")
+    ap.add_argument("--spp", type=int, default=500)
+    ap.add_argument("--ranks", default="", help="only these ranks of each N (e.g. 0 for one C4 share)")
     a = ap.parse_args()
-    W, H, SPP = 1200, 800, 500
+    W, H = (int(x) for x in a.size.split("x"))
+    SPP = a.spp
     scene, b = rtw.scenes.simple_soa()
     cam = b.with_image_width(W).with_image_height(H).with_samples_per_pixel(SPP).with_max_depth(50).build()
     r = rtw.Renderer(precision=rtw.RTW_F32)
@@ -34,13 +39,15 @@ def main():
         k, v = kv.split("=")
         r.set_tuning(k, int(v))
     r.set_scene(scene)
-    buf = torch.empty((H, W, 3), dtype=torch.float32, device="cuda:0")
-    r.render_device(cam, 1, buf.data_ptr(), buf.numel() * 4)     # warm-up
+    buf = torch.empty((rtw.tiles_for_rank(W, H, 0, 1) * 64 * 3,), dtype=torch.float32, device="cuda:0")
+    if W * H * SPP <= 2_000_000_000:
+        r.render_device(cam, 1, buf.data_ptr(), buf.numel() * 4)     # warm-up
     torch.cuda.synchronize()
     base = None
     for n in (int(x) for x in a.ns.split(",")):
         per_rank, kern = [], []
-        for rank in range(n):
+        only = [int(x) for x in a.ranks.split(",")] if a.ranks else range(n)
+        for rank in only:
             best = float("inf")
             for _ in range(a.reps):
                 torch.cuda.synchronize()
@@ -52,7 +59,9 @@ def main():
             per_rank.append(best * 1e3)
         slowest = max(per_rank)
         base = base or slowest
-        print(json.dumps({"tuning": a.tuning, "nranks": n, "max_rank_ms": round(slowest, 2), "min_rank_ms": round(min(per_rank), 2),
+        st = r.get_stats()
+        print(json.dumps({"size": a.size, "spp": SPP, "tuning": a.tuning, "nranks": n, "ranks": list(only),
+                          "chunk": int(st.chunk), "max_rank_ms": round(slowest, 2), "min_rank_ms": round(min(per_rank), 2),
                           "speedup_vs_1": round(base / slowest, 2), "max_rank_launch_ms": round(max(kern), 2),
                           "msamples_s_if_parallel": round(W * H * SPP / (slowest * 1e-3) / 1e6, 1),
                           "per_rank_ms": [round(x, 2) for x in per_rank]}), flush=True)
