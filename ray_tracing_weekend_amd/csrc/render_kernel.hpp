@@ -32,6 +32,24 @@ namespace rtw {
 
 namespace dev {
 
+// Experiment hooks: every RTW_PROBE_* below expands to nothing in the product
+// build; the profiling builds of tools/exp_cost.sh (RTW_EXP) and
+// tools/trace_paths.py (RTW_TRACE) and tools/lane_profile.py (RTW_PROF)
+// define them in rtw_probes.hpp.
+#if defined(RTW_EXP) || defined(RTW_TRACE) || defined(RTW_PROF)
+#include "rtw_probes.hpp"
+#else
+#define RTW_PROBE_PLANES()
+#define RTW_PROBE_CLOSEST()
+#define RTW_PROBE_SEGMENT()
+#define RTW_PROBE_LAMBERT_DIR()
+#define RTW_PROBE_LIGHT_PDF()
+#define RTW_PROBE_SEED()
+#define RTW_PROBE_LANES(id)
+#define RTW_PROBE_H64()
+#define RTW_PROBE_SCATTER64(expr)
+#endif
+
 template <typename R>
 __device__ __forceinline__ V3<R> v3of(const R* a) { return mk(a[0], a[1], a[2]); }
 
@@ -529,6 +547,7 @@ __device__ __forceinline__ void bvh_traverse_ww(const DevScene<R>& sc, int32_t b
             const bool inner = node >= 0 && node != kDone;
             if (!__any(inner) || __all(leaf != 0 || node == kDone)) break;
             if (inner) {
+                RTW_PROBE_LANES(1);
                 ++nvis;
                 const BvhNode<R>& nd = nodes[node];
                 const R tb = T.bound();
@@ -557,6 +576,7 @@ __device__ __forceinline__ void bvh_traverse_ww(const DevScene<R>& sc, int32_t b
         }
         if (!__any(leaf != 0)) break;   // no parked leaves: every lane is done
         if (leaf != 0) {
+            RTW_PROBE_LANES(2);
             test_leaf(sc, base, leaf, T, ntest);
             leaf = 0;
         }
@@ -1101,19 +1121,6 @@ __device__ V3<R> tex_colour(const DevScene<R>& sc, uint32_t tid, R u, R v, V3<R>
     return mk((R)NAN, (R)NAN, (R)NAN);
 }
 
-// Experiment hooks: every RTW_PROBE_* below expands to nothing in the product
-// build; the profiling builds of tools/exp_cost.sh (RTW_EXP) and
-// tools/trace_paths.py (RTW_TRACE) define them in rtw_probes.hpp.
-#if defined(RTW_EXP) || defined(RTW_TRACE)
-#include "rtw_probes.hpp"
-#else
-#define RTW_PROBE_PLANES()
-#define RTW_PROBE_CLOSEST()
-#define RTW_PROBE_SEGMENT()
-#define RTW_PROBE_LAMBERT_DIR()
-#define RTW_PROBE_LIGHT_PDF()
-#define RTW_PROBE_SEED()
-#endif
 
 // kOpt: compile-time options, chosen per launch by the host
 //   kOptRobust   (f32) closest-approach sphere and light tests (far geometry)
@@ -1342,7 +1349,9 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
     acquire();
 
     while (__ballot(active) != 0) {
+        RTW_PROBE_LANES(3);
         if (active) {
+            RTW_PROBE_LANES(4);
             if constexpr (kHit64) {
                 // the f32 ray is the f64 one rounded (dither64 stays within half an
                 // f32 ulp): o, d are not kept live across segments
@@ -1391,6 +1400,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                 tb64 = best >= 0 ? (double)tb : (double)INFINITY;
                 bool skip = false;
                 if (self_s >= 0) {
+                    RTW_PROBE_LANES(5);
                     ++ntest;
                     double ts;
                     if (sphere_t_ref64(p.sc.sph64[self_s], o64, d64, ts) && ts < tb64) {
@@ -1401,6 +1411,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                     }
                 }
                 if (!skip) {
+                    RTW_PROBE_LANES(6);
                     const int32_t prev = best, excl = self_s >= 0 ? sbase + self_s : -1;
                     if constexpr (kWorld >= kWorldBvh) {
                         int32_t* stk = reinterpret_cast<int32_t*>(smem) + wave * p.stack * 64 + lane;
@@ -1413,6 +1424,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                         if (!sphere_t_ref64(p.sc.sph64[best - sbase], o64, d64, tb64)) tb64 = (double)tb;
                     }
                 }
+                RTW_PROBE_H64();
             } else if constexpr (kWorld >= kWorldBvh) {
                 RTW_PROBE_CLOSEST();
                 int32_t* stk = reinterpret_cast<int32_t*>(smem) + wave * p.stack * 64 + lane;
@@ -1532,11 +1544,13 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                 }
                 const V3<R> emitted = mtype == kMatDiffuseLight ? colour : zero;
                 if (mtype == kMatMetal) {
+                    RTW_PROBE_LANES(7);
                     // Metal::scatter, material.rs:407-421
                     V3<R> dir;
                     bool keep;
                     if (kHit64 && sph_hit) {
                         const V3<R> us = unit_sphere<R>(g);
+                        RTW_PROBE_SCATTER64(metal_dir64(d64, n64, (double)mp.w, dither64(us), keep2).y);
                         d64 = metal_dir64(d64, n64, (double)mp.w, dither64(us), keep);
                         dir = from64<R>(d64);
                     } else {
@@ -1557,9 +1571,11 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                         d = dir;
                     }
                 } else if (mtype == kMatDielectric) {
+                    RTW_PROBE_LANES(8);
                     // Dialectric::scatter, material.rs:458-487
                     V3<R> dir;
                     if (kHit64 && sph_hit) {
+                        RTW_PROBE_SCATTER64(dielectric_dir64(d64, n64, !front, (double)mp.w, g2).y);
                         d64 = dielectric_dir64(d64, n64, front, (double)mp.w, g);
                         dir = from64<R>(d64);
                     } else {
@@ -1581,6 +1597,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                     if constexpr (kHit64) o64 = pnt64;
                     d = dir;
                 } else if (mtype == kMatLambertian) {
+                    RTW_PROBE_LANES(9);
                     // Lambertian + MixturePdf(HittablePdf(lights), CosinePdf):
                     // material.rs:357-376, pdf.rs:33-101, camera.rs:504-521
                     ++lambs;
@@ -1665,6 +1682,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                 if (s < s_end) {
                     RTW_PROBE_SEED();
                     start_sample();
+                RTW_PROBE_LANES(10);
                 } else {
                     R* dst = p.partial + (((size_t)c * p.n_local_tiles + my_lt) * 64 + px) * 3;
                     dst[0] = part.x;

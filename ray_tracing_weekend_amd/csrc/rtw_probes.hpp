@@ -6,8 +6,17 @@
 // the time difference prices it.  1 = closest-hit query, 2 = light pdf sum,
 // 3 = stream seeding, 4 = Lambertian direction sampling, 5 = plane tests,
 // 6 = closest-hit query along another direction, 7 = light pdf sum along the
-// same direction.  The repeated work feeds a comparison that never holds, so
-// the compiler keeps it.
+// same direction; f32 kernels with f64 hit points (kOptHit64): 8 = the
+// own-sphere f64 test, 9 = the f32 closest-hit query, 10 = the winner's f64 t,
+// 11 = the Metal / Dielectric f64 scatter (each along a permuted direction).
+// The repeated work feeds a comparison that never holds, so the compiler
+// keeps it.
+//
+// RTW_PROF (tools/lane_profile.py): at each RTW_PROBE_LANES(id) site, count
+// the wave passes and the lanes active in them (1 = BVH inner-node step,
+// 2 = parked-leaf tests, 3 = segment loop, 4 = active lanes of a trip, 5 =
+// own-sphere f64 test, 6 = closest-hit query, 7 = Metal, 8 = Dielectric,
+// 9 = Lambertian, 10 = next sample), read back with rtw_probe_lanes_read.
 //
 // RTW_TRACE (tools/trace_paths.py): record every segment of the first
 // kTraceSamples samples of one pixel -- the ray (origin, direction) and the
@@ -99,6 +108,44 @@
 #define RTW_PROBE_SEED()
 #endif
 
+#if RTW_EXP == 8 || RTW_EXP == 9 || RTW_EXP == 10
+#define RTW_PROBE_H64() \
+    do { \
+        const V3<double> dp_ = {d64.y, d64.z, d64.x}; \
+        double t2_ = 0.0; \
+        if (RTW_EXP == 8 && self_s >= 0) { \
+            if (sphere_t_ref64(p.sc.sph64[self_s], o64, dp_, t2_) && t2_ == -7.0) ++segs; \
+        } \
+        if (RTW_EXP == 9) { \
+            float tb2_ = (float)INFINITY; \
+            int32_t b2_ = -1; \
+            if constexpr (kWorld >= kWorldBvh) { \
+                int32_t* stk2_ = reinterpret_cast<int32_t*>(smem) + wave * p.stack * 64 + lane; \
+                bvh_closest_excl<kWorld == kWorldBvhLds ? kWorldBvhWW : kWorld, kRobust>( \
+                    scw, sbase, o, mk(d.y, d.z, d.x), tmin, tb2_, b2_, stk2_, nvis, ntest, -1); \
+            } \
+            if (b2_ == -7) ++segs; \
+        } \
+        if (RTW_EXP == 10 && best >= sbase) { \
+            if (sphere_t_ref64(p.sc.sph64[best - sbase], o64, dp_, t2_) && t2_ == -7.0) ++segs; \
+        } \
+    } while (0)
+#else
+#define RTW_PROBE_H64()
+#endif
+
+#if RTW_EXP == 11
+#define RTW_PROBE_SCATTER64(expr) \
+    do { \
+        bool keep2; \
+        Rng g2 = g; \
+        (void)keep2; \
+        if ((expr) == -7.0) ++segs; \
+    } while (0)
+#else
+#define RTW_PROBE_SCATTER64(expr)
+#endif
+
 #ifdef RTW_TRACE
 // build with -DRTW_TRACE=f32 (render_f32.hip) / -DRTW_TRACE=f64 (render_f64.hip):
 // each instantiation unit keeps its own trace array and exports its reader
@@ -134,4 +181,27 @@ extern "C" int RTW_CAT(rtw_probe_trace_read_, RTW_TRACE)(double* out, size_t n) 
     } while (0)
 #else
 #define RTW_PROBE_SEGMENT()
+#endif
+
+#ifdef RTW_PROF
+static __device__ unsigned long long g_lanes[2 * 16];
+#define RTW_PROBE_LANES(id) \
+    do { \
+        const uint64_t m_ = __ballot(true); \
+        if ((uint32_t)__lane_id() == (uint32_t)__builtin_ctzll(m_)) { \
+            atomicAdd(&g_lanes[2 * (id)], (unsigned long long)__popcll(m_)); \
+            atomicAdd(&g_lanes[2 * (id) + 1], 1ull); \
+        } \
+    } while (0)
+extern "C" int rtw_probe_lanes_read(unsigned long long* out, int reset) {
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_lanes), sizeof g_lanes) != hipSuccess) return -1;
+    if (reset) {
+        static unsigned long long zero[2 * 16];
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_lanes), zero, sizeof zero) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#else
+#define RTW_PROBE_LANES(id)
 #endif
