@@ -1,0 +1,121 @@
+"""BASELINE configs[3], C4: scenes::simple at 3840x2160, 4096 spp, depth 50,
+split over 8 GPUs by 8x8 tiles (tile T -> rank T % 8) and gathered.
+
+The full C4 render is 34 G samples; on one GPU these tests run
+  * the full 3840x2160 frame at 2 spp in f64, rows pinned to the oracle;
+  * rank 0's 1/8 share (16 200 tiles) at the full 4096 spp in f32 -- the
+    chunk sums of that share (4096 x 1.04 M pixels x 12 B = 51 GB at one
+    sample per item) exceed partial_max (8 GiB), so the auto chunk grows
+    and the chunk sums are folded in double (reduce_chunks_kernel);
+  * the same share's first tile in f64 at 4096 spp against the oracle with
+    the same chunk (bit for bit), and rank 7's share in f32 against rank 0's
+    cost (balance).
+"""
+import numpy as np
+import pytest
+
+import ray_tracing_weekend_amd as rtw
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+W, H, DEPTH, N = 3840, 2160, 50, 8
+
+
+def _cam(spp):
+    b = rtw.scenes.simple_soa(0x5EED0001)[1]
+    return b.with_image_width(W).with_image_height(H).with_samples_per_pixel(spp).with_max_depth(DEPTH).build()
+
+
+def _ocam(cam):
+    ocam = O.Camera()
+    for name, _ in O.Camera._fields_:
+        setattr(ocam, name, getattr(cam.raw, name))
+    return ocam
+
+
+def _share(prec, spp, rank, seed, tuning=None):
+    import torch
+    soa = rtw.scenes.simple_soa(0x5EED0001)[0]
+    cam = _cam(spp)
+    n = rtw.tiles_for_rank(W, H, rank, N) * 64 * 3
+    dt = torch.float32 if prec == rtw.RTW_F32 else torch.float64
+    buf = torch.zeros(n, dtype=dt, device="cuda:0")
+    with rtw.Renderer(precision=prec) as r:
+        for k, v in (tuning or {}).items():
+            r.set_tuning(k, v)
+        r.set_scene(soa)
+        r.render_device(cam, seed, buf.data_ptr(), n * buf.element_size(), rank=rank, nranks=N)
+        st = r.get_stats()
+        ms = r.get_timings(1)[0][0]
+    return buf.cpu().numpy().reshape(-1, 64, 3), st, ms
+
+
+def test_c4_full_frame_f64_rows_match_oracle():
+    soa = rtw.scenes.simple_soa(0x5EED0001)[0]
+    cam = _cam(2)
+    with rtw.Renderer(precision=rtw.RTW_F64) as r:
+        r.set_scene(soa)
+        img = r.render(cam, 41)
+        chunk = int(r.stats.chunk)
+    assert img.shape == (H, W, 3)
+    rows = (700, 1500, 400)
+    ref, _ = O.render(_ocam(cam), O.Scene(**soa.__dict__), 41, chunk=chunk, accel=O.ACCEL_BVH_CACHED, rows=rows)
+    sel = list(range(*rows))
+    g, o = img[sel], ref[sel]
+    assert np.array_equal(np.isnan(g).any(-1), np.isnan(o).any(-1))
+    ok = ~np.isnan(o).any(-1)
+    assert np.abs(g[ok] - o[ok]).mean() / 2 < 1e-5 and (g[ok] == o[ok]).all()
+
+
+@pytest.fixture(scope="module")
+def share0():
+    return _share(rtw.RTW_F32, 4096, 0, 7)
+
+
+def test_c4_share_at_4096_spp_grows_the_chunk(share0):
+    tiles, st, ms = share0
+    assert tiles.shape[0] == 16200
+    assert st.samples == 16200 * 64 * 4096
+    # 51 GB of one-sample chunk sums would exceed partial_max: the chunk grew
+    assert st.chunk > 1 and (4096 + st.chunk - 1) // st.chunk * 16200 * 64 * 12 <= 8 << 30
+    sums = tiles.reshape(-1, 3)
+    fin = np.isfinite(sums).all(-1)
+    assert fin.mean() > 0.5
+    means = sums[fin] / 4096
+    assert (means >= 0).all() and means.max() < 1.5 and 0.3 < means.mean() < 1.0
+    print(f"C4 rank-0 share: {ms:.1f} ms, chunk {st.chunk}, {st.samples / ms / 1e3:.0f} Msamples/s")
+
+
+def test_c4_share_chunk_does_not_change_the_samples(share0):
+    """Chunking only regroups the fold of each pixel's samples: the share's
+    sums with a 4x larger chunk agree with the auto-chunk sums to f32
+    summation rounding (the paths are the same RNG words)."""
+    tiles, st, _ = share0
+    other, st2, _ = _share(rtw.RTW_F32, 4096, 0, 7, tuning={"chunk": int(st.chunk) * 4})
+    assert st2.chunk == st.chunk * 4
+    a, b = tiles.reshape(-1, 3), other.reshape(-1, 3)
+    ok = np.isfinite(a).all(-1) & np.isfinite(b).all(-1)
+    assert np.array_equal(np.isfinite(a).all(-1), np.isfinite(b).all(-1))
+    rel = np.abs(a[ok] - b[ok]) / np.maximum(np.abs(a[ok]), 1.0)
+    assert rel.max() < 1e-4, rel.max()
+
+
+def test_c4_share_first_tile_f64_matches_oracle_at_4096_spp():
+    tiles, st, _ = _share(rtw.RTW_F64, 4096, 0, 9)
+    cam = _cam(4096)
+    soa = rtw.scenes.simple_soa(0x5EED0001)[0]
+    # rank 0's first tile is global tile 0: pixels i 0..7, j 0..7; check row j = 0
+    ref, _ = O.render(_ocam(cam), O.Scene(**soa.__dict__), 9, chunk=int(st.chunk), accel=O.ACCEL_BVH_CACHED,
+                      rows=(0, 1, 1), cols=(0, 8))
+    g = tiles[0, 0:8]
+    o = ref[0, 0:8]
+    assert np.array_equal(np.nan_to_num(g, nan=-7), np.nan_to_num(o, nan=-7))
+
+
+def test_c4_shares_cost_alike():
+    """The tile interleave balances the ranks: rank 7's share costs within
+    10 % of rank 0's (the row-tile split of round 1 differed by 15 % at C2)."""
+    _, _, ms0 = _share(rtw.RTW_F32, 512, 0, 3)
+    _, _, ms7 = _share(rtw.RTW_F32, 512, 7, 3)
+    assert abs(ms7 / ms0 - 1) < 0.10, (ms0, ms7)

@@ -72,7 +72,7 @@ def main():
             "node_visits_per_segment": round(st.node_visits / max(st.segments, 1), 3),
             "sphere_tests_per_segment": round(st.sphere_tests / max(st.segments, 1), 3),
             "scene_gen_s": round(t_gen, 2), "scene_stage_s": round(t_stage, 2),
-            "finite_fraction": float(torch.isfinite(buf).all(-1).float().mean()),
+            "finite_fraction": float(torch.isfinite(buf.view(-1, 3)).all(-1).float().mean()),
         }), flush=True)
         r.close()
 
