@@ -34,7 +34,9 @@ struct rtw_ctx {
                                   // tree staged in LDS (falls back to 1 when it does not fit),
                                   // 1 = the same from L1/L2, 2 = 4-wide octant tree, 0 = binary
                                   // single loop
-    size_t bvh_lds_max = 32 * 1024;   // LDS per workgroup allowed for bvh_kind 3
+    // LDS per workgroup allowed for bvh_kind 3 (0: by precision -- f32 32 KiB, five
+    // 256-thread workgroups per CU at 5 waves/SIMD; f64 52 KiB, three at 3 waves/SIMD)
+    size_t bvh_lds_max = 0;
     int robust = 2;                   // f32 closest-approach tests: 1 on, 0 off, 2 by scene scale
     double scene_extent = 0.0, min_radius = 0.0;   // of the staged scene (robust = 2)
     uint32_t bvh_leaf = 0;            // spheres per BVH leaf (set before rtw_set_scene); 0 = auto:
@@ -238,6 +240,7 @@ std::vector<unsigned char> stage_scene(const rtw_scene* s, rtw::DevScene<R>* ds,
     };
     const size_t o_sph = reserve(sizeof(R4) * s->n_spheres);
     const size_t o_s64 = reserve(sizeof(double) * 4 * s->n_spheres);
+    const size_t o_pl64 = reserve(sizeof(double) * 8 * s->n_planes);
     const size_t o_r = reserve(sizeof(R) * s->n_spheres);
     const size_t o_smat = reserve(sizeof(uint32_t) * s->n_spheres);
     const size_t o_sshade = reserve(sizeof(R4) * s->n_spheres);
@@ -319,6 +322,10 @@ std::vector<unsigned char> stage_scene(const rtw_scene* s, rtw::DevScene<R>* ds,
                                fx ? 0.0 : INFINITY, fy ? 0.0 : INFINITY, fz ? 0.0 : INFINITY};
         R* dst = reinterpret_cast<R*>(b + o_pl) + rtw::kPlaneR * k;
         for (int q = 0; q < 6; ++q) dst[q] = (R)pl[q];
+        for (int q = 0; q < 3; ++q) {
+            reinterpret_cast<double*>(b + o_pl64)[8 * k + q] = pl[q];
+            reinterpret_cast<double*>(b + o_pl64)[8 * k + 4 + q] = pl[3 + q];
+        }
         for (int q = 0; q < 6; ++q) dst[6 + q] = (R)box[q];
         // Plane::get_plane_uv's constants (plane.rs:40-54), computed as the
         // oracle's plane_uv does: theta = atan2(|n x V|, n . V), V = (0, 1, 0)
@@ -416,6 +423,7 @@ std::vector<unsigned char> stage_scene(const rtw_scene* s, rtw::DevScene<R>* ds,
     ds->sph = reinterpret_cast<const R4*>(base + o_sph);
     ds->sph_r = reinterpret_cast<const R*>(base + o_r);
     ds->sph64 = reinterpret_cast<const rtw::R4<double>*>(base + o_s64);
+    ds->pl64 = reinterpret_cast<const rtw::R4<double>*>(base + o_pl64);
     ds->sph_mat = reinterpret_cast<const uint32_t*>(base + o_smat);
     ds->sph_shade = reinterpret_cast<const R4*>(base + o_sshade);
     ds->planes = reinterpret_cast<const R*>(base + o_pl);
@@ -754,7 +762,8 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
         } else if (bin_stack <= rtw::kBvhStack) {
             p.stack = bin_stack;
             bvh_width = 2;
-            if (c->bvh_kind == 3 && tree_lds <= c->bvh_lds_max) {
+            const size_t lds_max = c->bvh_lds_max ? c->bvh_lds_max : (sizeof(R) == 4 ? 32 * 1024 : 52 * 1024);
+            if (c->bvh_kind == 3 && tree_lds <= lds_max) {
                 world = rtw::kWorldBvhLds;
                 launch_lds = tree_lds;
             } else {
@@ -1020,13 +1029,13 @@ int rtw_set_scene(rtw_ctx* c, const rtw_scene* s) {
         fix(ds.sph); fix(ds.sph_r); fix(ds.sph_mat); fix(ds.sph_shade); fix(ds.planes); fix(ds.plane_mat);
         fix(ds.mat_type); fix(ds.mat_p); fix(ds.lights); fix(ds.bvh); fix(ds.bsph); fix(ds.bid);
         fix(ds.bvh4); fix(ds.lbvh); fix(ds.lsph); fix(ds.lid); fix(ds.lg_start); fix(ds.lg_sph); fix(ds.lg_id);
-        fix(ds.quads); fix(ds.quad_mat); fix(ds.lquads); fix(ds.sph64);
+        fix(ds.quads); fix(ds.quad_mat); fix(ds.lquads); fix(ds.sph64); fix(ds.pl64);
         if (ds.lref) fix(ds.lref);
         fix(ds.boxes); fix(ds.box_mat);
         if (ds.mat_tex) fix(ds.mat_tex);
         fix(ds.tex_type); fix(ds.tex_p); fix(ds.tex_refs); fix(ds.perlin_vec); fix(ds.perlin_perm);
     };
-    static_assert(offsetof(rtw::DevScene<float>, n_sph) == 32 * sizeof(void*),
+    static_assert(offsetof(rtw::DevScene<float>, n_sph) == 33 * sizeof(void*),
                   "DevScene gained a pointer: update rebase");
     if (c->precision == RTW_F32) {
         rebase(tmp32);

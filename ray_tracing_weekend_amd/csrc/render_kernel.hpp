@@ -756,6 +756,14 @@ __device__ __forceinline__ bool sphere_t_ref64(const R4<double>& S, V3<double> o
     t = root;
     return true;
 }
+// Plane::hit's t, plane.rs:64: -((o - p) . n) / (d . n) (f64, no FMA), on the
+// plane as given (DevScene::pl64: {point, 0}, {normal, 0})
+__device__ __forceinline__ double plane_t_ref64(const R4<double>* P, V3<double> o, V3<double> d) {
+#pragma clang fp contract(off)
+    const R4<double> pt = P[0], n = P[1];
+    const double denom = d.x * n.x + d.y * n.y + d.z * n.z;
+    return -(((o.x - pt.x) * n.x + (o.y - pt.y) * n.y + (o.z - pt.z) * n.z) / denom);
+}
 // Ray::at, o + d t (f64, no FMA)
 __device__ __forceinline__ V3<double> ray_at64(V3<double> o, V3<double> d, double t) {
 #pragma clang fp contract(off)
@@ -1424,6 +1432,9 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                         if (!sphere_t_ref64(p.sc.sph64[best - sbase], o64, d64, tb64)) tb64 = (double)tb;
                     }
                 }
+                // a plane's t in f64 too, so that its hit points lie within f64 rounding
+                // of the plane (the one-sided Book-1 ground is never hit from above)
+                if (best >= 0 && best < nplanes) tb64 = plane_t_ref64(p.sc.pl64 + 2 * best, o64, d64);
                 RTW_PROBE_H64();
             } else if constexpr (kWorld >= kWorldBvh) {
                 RTW_PROBE_CLOSEST();
@@ -1825,8 +1836,8 @@ inline int launch_render_impl(const KParams<R>& p, int world, size_t lds_bytes, 
     if (blocks) {
         const bool robust = sizeof(R) == 4 && p.sc.robust;
         const bool lbvh = p.light_bvh != 0;
-        // kOptPrims: always for textured and f64 kernels; the f32 Book-1
-        // kernels go without when the scene has no quads, cuboids or mixed list
+        // kOptPrims: always for textured kernels; the Book-1 kernels go
+        // without when the scene has no quads, cuboids or mixed list
         const bool prims = p.sc.n_quads || p.sc.n_boxes || p.sc.lref;
         constexpr int T = dev::kOptTex | dev::kOptPrims, Pr = dev::kOptPrims;
         if (p.sc.mat_tex) {
@@ -1860,10 +1871,16 @@ inline int launch_render_impl(const KParams<R>& p, int world, size_t lds_bytes, 
                 }
             }
         } else {
+            // f64: the sphere + plane scenes' kernels go without the quad / cuboid code
+            // too (156 instead of 176 VGPRs: 3 waves per SIMD instead of 2)
             (void)robust;
-            (void)prims;
-            if (lbvh) launch_world<R, Pr | dev::kOptLightBvh>(p, world, lds_bytes, blocks, stream);
-            else launch_world<R, Pr>(p, world, lds_bytes, blocks, stream);
+            if (prims) {
+                if (lbvh) launch_world<R, Pr | dev::kOptLightBvh>(p, world, lds_bytes, blocks, stream);
+                else launch_world<R, Pr>(p, world, lds_bytes, blocks, stream);
+            } else {
+                if (lbvh) launch_world<R, dev::kOptLightBvh>(p, world, lds_bytes, blocks, stream);
+                else launch_world<R, 0>(p, world, lds_bytes, blocks, stream);
+            }
         }
         if (hipGetLastError() != hipSuccess) return -1;
     }

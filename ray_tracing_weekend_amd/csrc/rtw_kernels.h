@@ -100,6 +100,7 @@ struct DevScene {
     const R* lquads;                  // the light list's quads, n_lquads x kQuadR
     const R4<double>* sph64;          // spheres {cx, cy, cz, radius} as given (f64): the f32
                                       // kernels' f64 hit points (kOptHit64)
+    const R4<double>* pl64;           // planes {point, 0}, {normal, 0} as given (f64): kOptHit64
     const uint32_t* lref;             // light list in order (kLref* bits | index; null when the
                                       // list is spheres only)
     const R* boxes;                   // n_boxes x kBoxR (transformed cuboids, layout below)
@@ -148,6 +149,7 @@ constexpr uint32_t kBoxRot = 144, kBoxInv = 153, kBoxT = 162, kBoxTi = 165, kBox
                    kBoxOk = 174;
 
 constexpr uint32_t kBvhStack = 32;    // per-lane traversal stack entries (LDS)
+
 
 template <typename R>
 struct KParams {
