@@ -192,8 +192,8 @@ int rtw_set_accel(rtw_ctx *ctx, int accel);
 /* scheduling knobs (benchmarking): "chunk" (samples per item, 0 = auto),
  * "auto_chunk", "group" (chunks per wave task, 0 = auto: 4..32), "target_tasks"
  * (auto group: about this many tasks; 0 = 2^19 with persistent waves, 2^17 without),
- * "persist" (workgroups of persistent waves that take tasks from a global counter,
- * default 2048; 0 = one task per wave),
+ * "persist" (workgroups of persistent waves that take tasks from a global counter;
+ * 1 = as many as are resident at once, the default; 0 = one task per wave),
  * "lds" (1 = stage the sphere list in LDS when it fits, 0 = read it from HBM),
  * "robust" (f32 ray-sphere tests in closest-approach form: 1 on, 0 off,
  * 2 = by the scene's distance-to-radius ratio, the default),

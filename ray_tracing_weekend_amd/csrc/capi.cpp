@@ -41,7 +41,8 @@ struct rtw_ctx {
     double scene_extent = 0.0, min_radius = 0.0;   // of the staged scene (robust = 2)
     uint32_t bvh_leaf = 0;            // spheres per BVH leaf (set before rtw_set_scene); 0 = auto:
                                       // 4, or 8 for scenes of >= 100k spheres (C5: +12 %)
-    uint32_t persist = 2048;          // workgroups of persistent waves (tasks from a counter);
+    uint32_t persist = rtw::kPersistResident;   // workgroups of persistent waves (tasks from a
+                                      // counter; default: as many as are resident at once);
                                       // 0: one task per wave
     uint32_t light_leaf = 0;          // light spheres per light-BVH leaf; 0 = 4
     uint32_t light_grid = 4;          // light pdf through the light grid at light_grid / 16
@@ -241,6 +242,7 @@ std::vector<unsigned char> stage_scene(const rtw_scene* s, rtw::DevScene<R>* ds,
     const size_t o_sph = reserve(sizeof(R4) * s->n_spheres);
     const size_t o_s64 = reserve(sizeof(double) * 4 * s->n_spheres);
     const size_t o_pl64 = reserve(sizeof(double) * 8 * s->n_planes);
+    const size_t o_m64 = reserve(sizeof(double) * 4 * s->n_materials);
     const size_t o_r = reserve(sizeof(R) * s->n_spheres);
     const size_t o_smat = reserve(sizeof(uint32_t) * s->n_spheres);
     const size_t o_sshade = reserve(sizeof(R4) * s->n_spheres);
@@ -412,6 +414,21 @@ std::vector<unsigned char> stage_scene(const rtw_scene* s, rtw::DevScene<R>* ds,
     for (uint32_t k = 0; k < s->n_materials; ++k) {
         const double* m = s->mat_params + 5 * k;
         const uint32_t t = s->mat_type[k];
+        // the f64 scatter constants of kOptHit64 (dielectric_dir64): Dialectric's
+        // index_of_refraction.recip() and reflectance's r0 for both faces, with the
+        // reference's operations (material.rs:450-454, 464-468); Metal's fuzz
+        double* m64 = reinterpret_cast<double*>(b + o_m64) + 4 * k;
+        if (t == RTW_DIELECTRIC) {
+            const double ior = m[4], rf = 1.0 / ior;
+            const double r0f = (1.0 - rf) / (1.0 + rf), r0b = (1.0 - ior) / (1.0 + ior);
+            m64[0] = rf;
+            m64[1] = r0f * r0f;
+            m64[2] = r0b * r0b;
+            m64[3] = ior;
+        } else {
+            m64[0] = m64[1] = m64[2] = 0.0;
+            m64[3] = t == RTW_METAL ? m[3] : 0.0;
+        }
         reinterpret_cast<uint32_t*>(b + o_mt)[k] = t;
         const double w = t == RTW_METAL ? m[3] : (t == RTW_DIELECTRIC ? m[4] : 0.0);
         reinterpret_cast<R4*>(b + o_mp)[k] = R4{(R)m[0], (R)m[1], (R)m[2], (R)w};
@@ -424,6 +441,7 @@ std::vector<unsigned char> stage_scene(const rtw_scene* s, rtw::DevScene<R>* ds,
     ds->sph_r = reinterpret_cast<const R*>(base + o_r);
     ds->sph64 = reinterpret_cast<const rtw::R4<double>*>(base + o_s64);
     ds->pl64 = reinterpret_cast<const rtw::R4<double>*>(base + o_pl64);
+    ds->mat64 = reinterpret_cast<const rtw::R4<double>*>(base + o_m64);
     ds->sph_mat = reinterpret_cast<const uint32_t*>(base + o_smat);
     ds->sph_shade = reinterpret_cast<const R4*>(base + o_sshade);
     ds->planes = reinterpret_cast<const R*>(base + o_pl);
@@ -878,7 +896,7 @@ int rtw_set_tuning(rtw_ctx* c, const char* key, int64_t value) {
     else if (k == "robust") c->robust = (int)std::min<int64_t>(value, 2);
     else if (k == "bvh_leaf") c->bvh_leaf = (uint32_t)std::min<int64_t>(value, 15);
     else if (k == "light_leaf") c->light_leaf = (uint32_t)std::min<int64_t>(value, 15);
-    else if (k == "persist") c->persist = (uint32_t)std::min<int64_t>(value, 1 << 20);
+    else if (k == "persist") c->persist = value == 1 ? rtw::kPersistResident : (uint32_t)std::min<int64_t>(value, 1 << 20);
     else if (k == "light_grid") c->light_grid = (uint32_t)std::min<int64_t>(value, 1024);
     else if (k == "item_order") c->item_order = value ? 1u : 0u;
     else if (k == "hit64") c->hit64 = value ? 1u : 0u;
@@ -1029,13 +1047,13 @@ int rtw_set_scene(rtw_ctx* c, const rtw_scene* s) {
         fix(ds.sph); fix(ds.sph_r); fix(ds.sph_mat); fix(ds.sph_shade); fix(ds.planes); fix(ds.plane_mat);
         fix(ds.mat_type); fix(ds.mat_p); fix(ds.lights); fix(ds.bvh); fix(ds.bsph); fix(ds.bid);
         fix(ds.bvh4); fix(ds.lbvh); fix(ds.lsph); fix(ds.lid); fix(ds.lg_start); fix(ds.lg_sph); fix(ds.lg_id);
-        fix(ds.quads); fix(ds.quad_mat); fix(ds.lquads); fix(ds.sph64); fix(ds.pl64);
+        fix(ds.quads); fix(ds.quad_mat); fix(ds.lquads); fix(ds.sph64); fix(ds.pl64); fix(ds.mat64);
         if (ds.lref) fix(ds.lref);
         fix(ds.boxes); fix(ds.box_mat);
         if (ds.mat_tex) fix(ds.mat_tex);
         fix(ds.tex_type); fix(ds.tex_p); fix(ds.tex_refs); fix(ds.perlin_vec); fix(ds.perlin_perm);
     };
-    static_assert(offsetof(rtw::DevScene<float>, n_sph) == 33 * sizeof(void*),
+    static_assert(offsetof(rtw::DevScene<float>, n_sph) == 34 * sizeof(void*),
                   "DevScene gained a pointer: update rebase");
     if (c->precision == RTW_F32) {
         rebase(tmp32);

@@ -36,9 +36,12 @@ namespace dev {
 // build; the profiling builds of tools/exp_cost.sh (RTW_EXP) and
 // tools/trace_paths.py (RTW_TRACE) and tools/lane_profile.py (RTW_PROF)
 // define them in rtw_probes.hpp.
-#if defined(RTW_EXP) || defined(RTW_TRACE) || defined(RTW_PROF)
+#if defined(RTW_EXP) || defined(RTW_TRACE) || defined(RTW_PROF) || defined(RTW_TIMELINE)
 #include "rtw_probes.hpp"
 #else
+#define RTW_PROBE_WAVE_BEGIN()
+#define RTW_PROBE_WAVE_TASK()
+#define RTW_PROBE_WAVE_END()
 #define RTW_PROBE_PLANES()
 #define RTW_PROBE_CLOSEST()
 #define RTW_PROBE_SEGMENT()
@@ -786,6 +789,9 @@ __device__ __forceinline__ uint32_t mix32(uint32_t h) {
     return h;
 }
 __device__ __forceinline__ V3<double> dither64(V3<float> v) {
+#if RTW_ABL == 4
+    return V3<double>{v.x, v.y, v.z};
+#endif
     const uint32_t h0 = mix32(__float_as_uint(v.x) ^ mix32(__float_as_uint(v.y) ^ mix32(__float_as_uint(v.z))));
     const uint32_t h1 = mix32(h0 + 0x9e3779b9u), h2 = mix32(h1 + 0x9e3779b9u);
     constexpr double kScale = 0x1p-25 / 4294967296.0;        // (h - 2^31) * 2^-57: |rel| < 2^-26
@@ -798,34 +804,42 @@ __device__ __forceinline__ V3<double> dither64(V3<double> v) { return v; }   // 
 template <typename R>
 __device__ __forceinline__ V3<R> from64(V3<double> v) { return mk((R)v.x, (R)v.y, (R)v.z); }
 
-// Metal::scatter's direction (material.rs:407-421) in f64, no FMA:
-// reflect(d / |d|, n) + us * fuzz, with reflect(v, n) = v - (n * 2) (v . n)
-// (vec.rs); its dot with n decides absorption (returned in `keep`)
-__device__ __forceinline__ V3<double> metal_dir64(V3<double> d, V3<double> n, double fuzz, V3<double> us,
-                                                  bool& keep) {
+// Vec3::normalize, self / self.length() (vec.rs), in f64, no FMA: the unit
+// incoming direction both Metal and Dialectric start from (material.rs:414, 469)
+__device__ __forceinline__ V3<double> unit64(V3<double> d) {
 #pragma clang fp contract(off)
     const double l = __builtin_sqrt(d.x * d.x + d.y * d.y + d.z * d.z);
-    const double ux = d.x / l, uy = d.y / l, uz = d.z / l;
+    return V3<double>{d.x / l, d.y / l, d.z / l};
+}
+// Metal::scatter's direction (material.rs:407-421) in f64, no FMA, from the
+// unit direction u: reflect(u, n) + us * fuzz, with reflect(v, n) = v - (n * 2)
+// (v . n) (vec.rs); its dot with n decides absorption (returned in `keep`)
+__device__ __forceinline__ V3<double> metal_dir64(V3<double> u, V3<double> n, double fuzz, V3<double> us,
+                                                  bool& keep) {
+#pragma clang fp contract(off)
+    const double ux = u.x, uy = u.y, uz = u.z;
     const double vn = ux * n.x + uy * n.y + uz * n.z;
     const double rx = ux - (n.x * 2.0) * vn, ry = uy - (n.y * 2.0) * vn, rz = uz - (n.z * 2.0) * vn;
     const V3<double> out = {rx + us.x * fuzz, ry + us.y * fuzz, rz + us.z * fuzz};
     keep = out.x * n.x + out.y * n.y + out.z * n.z > 0.0;
     return out;
 }
-// Dialectric::scatter's direction (material.rs:458-487) in f64, no FMA; the
-// Open01 word is drawn only when refraction is possible (the || short circuit)
-__device__ __forceinline__ V3<double> dielectric_dir64(V3<double> d, V3<double> n, bool front, double ior,
-                                                       Rng& g) {
+// Dialectric::scatter's direction (material.rs:458-487) in f64, no FMA, from
+// the unit direction u and the material's f64 record M = {1/ior, r0 at 1/ior,
+// r0 at ior, ior} (DevScene::mat64: the recip() and reflectance's r0 =
+// ((1 - ratio) / (1 + ratio))^2 of both faces, computed once on the host with
+// the same operations); the Open01 word is drawn only when refraction is
+// possible (the || short circuit)
+__device__ __forceinline__ V3<double> dielectric_dir64(V3<double> u, V3<double> n, bool front,
+                                                       const R4<double>& M, Rng& g) {
 #pragma clang fp contract(off)
-    const double ratio = front ? 1.0 / ior : ior;
-    const double l = __builtin_sqrt(d.x * d.x + d.y * d.y + d.z * d.z);
-    const double ux = d.x / l, uy = d.y / l, uz = d.z / l;
+    const double ratio = front ? M.x : M.w;
+    const double ux = u.x, uy = u.y, uz = u.z;
     const double cos_t = __builtin_fmin(ux * -n.x + uy * -n.y + uz * -n.z, 1.0);
     const double sin_t = __builtin_sqrt(1.0 - cos_t * cos_t);
     bool refl = ratio * sin_t > 1.0;
     if (!refl) {
-        double r0 = (1.0 - ratio) / (1.0 + ratio);       // Dialectric::reflectance, powi(5) as LLVM expands it
-        r0 = r0 * r0;
+        const double r0 = front ? M.y : M.z;             // Dialectric::reflectance, powi(5) as LLVM expands it
         const double x = 1.0 - cos_t, x2 = x * x;
         refl = r0 + (1.0 - r0) * (x * (x2 * x2)) > P<double>::u_open01(g.next());
     }
@@ -1140,6 +1154,9 @@ __device__ V3<R> tex_colour(const DevScene<R>& sc, uint32_t tid, R u, R v, V3<R>
 //   kOptHit64    (f32 kernels of sphere + plane scenes) f64 ray origin, own-sphere re-hit test,
 //                hit t and hit point (sphere_t_ref64): the reference's self-intersection odds
 enum : int { kOptRobust = 1, kOptLightBvh = 2, kOptTex = 4, kOptPrims = 8, kOptHit64 = 16 };
+#ifndef RTW_ABL
+#define RTW_ABL 0     // timing ablations of the kOptHit64 parts (experiment builds only)
+#endif
 
 template <typename R, int kWorld, int kOpt>
 // f32: ask for 5 waves per SIMD (<= 96 VGPRs; the kernel fits without
@@ -1283,6 +1300,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                                         // scatter's own f64 result, else dither64 of the f32 one)
     uint32_t segs = 0, lambs = 0, nvis = 0, ntest = 0;
     bool active = false, need = true;
+    RTW_PROBE_WAVE_BEGIN();
 
     auto start_sample = [&]() {
         // Camera::get_ray, camera.rs:274-293 + ray_colour_call, camera.rs:439-457
@@ -1327,6 +1345,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                     break;
                 }
                 set_task(t);
+                RTW_PROBE_WAVE_TASK();
                 next_q = 0;
                 continue;
             }
@@ -1411,7 +1430,11 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                     RTW_PROBE_LANES(5);
                     ++ntest;
                     double ts;
+#if RTW_ABL == 1
+                    if (sphere_t(mk(p.sc.sph[self_s].x, p.sc.sph[self_s].y, p.sc.sph[self_s].z), p.sc.sph[self_s].w, o, d, tmin, tb) && (double)tb < tb64) { ts = tb;
+#else
                     if (sphere_t_ref64(p.sc.sph64[self_s], o64, d64, ts) && ts < tb64) {
+#endif
                         tb64 = ts;
                         tb = (float)ts;
                         best = sbase + self_s;
@@ -1429,7 +1452,11 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                         sweep_spheres_excl<kRobust>(sph, p.sc.n_sph, sbase, o, d, tmin, tb, best, excl);
                     }
                     if (best != prev && best >= sbase) {
+#if RTW_ABL == 2
+                        tb64 = (double)tb;
+#else
                         if (!sphere_t_ref64(p.sc.sph64[best - sbase], o64, d64, tb64)) tb64 = (double)tb;
+#endif
                     }
                 }
                 // a plane's t in f64 too, so that its hit points lie within f64 rounding
@@ -1529,7 +1556,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                         next_iso = (mw >> 31) != 0;
                         // Metal / Dielectric scatter in f64 from the f64 normal: their
                         // directions decide the next re-hit at the ulp level
-                        if (mtype == kMatMetal || mtype == kMatDielectric) {
+                        if (RTW_ABL != 3 && (mtype == kMatMetal || mtype == kMatDielectric)) {
                             n64 = sphere_normal64(pnt64, p.sc.sph64[k]);
                             outward = mk((float)n64.x, (float)n64.y, (float)n64.z);
                             sph_hit = true;
@@ -1561,8 +1588,9 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                     bool keep;
                     if (kHit64 && sph_hit) {
                         const V3<R> us = unit_sphere<R>(g);
-                        RTW_PROBE_SCATTER64(metal_dir64(d64, n64, (double)mp.w, dither64(us), keep2).y);
-                        d64 = metal_dir64(d64, n64, (double)mp.w, dither64(us), keep);
+                        const double fuzz64 = p.sc.mat64[m].w;
+                        RTW_PROBE_SCATTER64(metal_dir64(unit64(d64), n64, fuzz64, dither64(us), keep2).y);
+                        d64 = metal_dir64(unit64(d64), n64, fuzz64, dither64(us), keep);
                         dir = from64<R>(d64);
                     } else {
                         V3<R> refl = reflect(PR::normalize(d), nrm);
@@ -1586,8 +1614,9 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                     // Dialectric::scatter, material.rs:458-487
                     V3<R> dir;
                     if (kHit64 && sph_hit) {
-                        RTW_PROBE_SCATTER64(dielectric_dir64(d64, n64, !front, (double)mp.w, g2).y);
-                        d64 = dielectric_dir64(d64, n64, front, (double)mp.w, g);
+                        const R4<double> m64 = p.sc.mat64[m];
+                        RTW_PROBE_SCATTER64(dielectric_dir64(unit64(d64), n64, !front, m64, g2).y);
+                        d64 = dielectric_dir64(unit64(d64), n64, front, m64, g);
                         dir = from64<R>(d64);
                     } else {
                         R ratio = front ? PR::div_((R)1, mp.w) : mp.w;
@@ -1707,6 +1736,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
         acquire();
     }
 
+    RTW_PROBE_WAVE_END();
     // wave-reduce the counters, one atomic per wave
     for (int off = 32; off > 0; off >>= 1) {
         segs += __shfl_xor(segs, off);
@@ -1784,10 +1814,30 @@ inline void allow_lds(size_t lds_bytes) {
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
 }
 
+// Grid of a persistent launch (KParams::persist == kPersistResident): the
+// workgroups that fit on the GPU at once for this kernel and LDS size (its
+// occupancy x CUs), no more than the tasks need.  More than that only adds
+// workgroups that start late and stretch the tail (C2 8-rank share: 2048
+// workgroups 15.3 ms, 1024 = resident at 4 waves/SIMD 14.9 ms); co-residency
+// is not required (no grid barrier: tasks come from a counter).
+template <typename R, int kWorld, int kOpt>
+inline uint32_t resident_blocks(uint32_t blocks, size_t lds_bytes) {
+    int per_cu = 0, dev = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &per_cu, reinterpret_cast<const void*>(&dev::render_kernel<R, kWorld, kOpt>), kBlock, lds_bytes) !=
+            hipSuccess ||
+        hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || per_cu < 1 ||
+        cus < 1)
+        return std::min<uint32_t>(blocks, 2048u);
+    return std::min<uint32_t>(blocks, (uint32_t)(per_cu * cus));
+}
+
 template <typename R, int kOpt>
 inline void launch_world(const KParams<R>& p, int world, size_t lds_bytes, uint32_t blocks,
                          hipStream_t stream) {
     const size_t stacks = (size_t)kWavesPerBlock * p.stack * 64 * sizeof(int32_t);
+    const bool resident = p.persist == kPersistResident;
     constexpr int kBrute = kOpt & ~dev::kOptLightBvh;   // the light BVH needs the BVH kernels' stack
     // textured scenes are small: their kernels exist for the brute-force and
     // binary while-while worlds only (launch_render_impl maps the others)
@@ -1797,29 +1847,37 @@ inline void launch_world(const KParams<R>& p, int world, size_t lds_bytes, uint3
     switch (world) {
     case kWorldLds:
         allow_lds<R, kWorldLds, kBrute>(lds_bytes);
+        if (resident) blocks = resident_blocks<R, kWorldLds, kBrute>(blocks, lds_bytes);
         hipLaunchKernelGGL((dev::render_kernel<R, kWorldLds, kBrute>), dim3(blocks), dim3(kBlock), lds_bytes,
                            stream, p);
         break;
     case kWorldBvhLds:
         allow_lds<R, kWorldBvhLds, kOpt>(lds_bytes);
+        if (resident) blocks = resident_blocks<R, kWorldBvhLds, kOpt>(blocks, lds_bytes);
         hipLaunchKernelGGL((dev::render_kernel<R, kWorldBvhLds, kOpt>), dim3(blocks), dim3(kBlock), lds_bytes,
                            stream, p);
         break;
     case kWorldBvh4:
-        if constexpr ((kOpt & dev::kOptTex) == 0)
+        if constexpr ((kOpt & dev::kOptTex) == 0) {
+            if (resident) blocks = resident_blocks<R, kWorldBvh4, kOpt>(blocks, stacks);
             hipLaunchKernelGGL((dev::render_kernel<R, kWorldBvh4, kOpt>), dim3(blocks), dim3(kBlock), stacks,
                                stream, p);
+        }
         break;
     case kWorldBvhWW:
+        if (resident) blocks = resident_blocks<R, kWorldBvhWW, kOpt>(blocks, stacks);
         hipLaunchKernelGGL((dev::render_kernel<R, kWorldBvhWW, kOpt>), dim3(blocks), dim3(kBlock), stacks,
                            stream, p);
         break;
     case kWorldBvh:
-        if constexpr ((kOpt & dev::kOptTex) == 0)
+        if constexpr ((kOpt & dev::kOptTex) == 0) {
+            if (resident) blocks = resident_blocks<R, kWorldBvh, kOpt>(blocks, stacks);
             hipLaunchKernelGGL((dev::render_kernel<R, kWorldBvh, kOpt>), dim3(blocks), dim3(kBlock), stacks,
                                stream, p);
+        }
         break;
     default:
+        if (resident) blocks = resident_blocks<R, kWorldGlobal, kBrute>(blocks, 0);
         hipLaunchKernelGGL((dev::render_kernel<R, kWorldGlobal, kBrute>), dim3(blocks), dim3(kBlock), 0, stream,
                            p);
         break;
@@ -1832,7 +1890,8 @@ template <typename R>
 inline int launch_render_impl(const KParams<R>& p, int world, size_t lds_bytes, R* out,
                               hipStream_t stream, hipEvent_t mid) {
     uint32_t blocks = (p.n_tasks + kWavesPerBlock - 1) / kWavesPerBlock;
-    if (p.persist) blocks = blocks < p.persist ? blocks : p.persist;   // resident-size grid, tasks from the counter
+    if (p.persist && p.persist != kPersistResident)
+        blocks = blocks < p.persist ? blocks : p.persist;   // fixed grid, tasks from the counter
     if (blocks) {
         const bool robust = sizeof(R) == 4 && p.sc.robust;
         const bool lbvh = p.light_bvh != 0;

@@ -101,6 +101,8 @@ struct DevScene {
     const R4<double>* sph64;          // spheres {cx, cy, cz, radius} as given (f64): the f32
                                       // kernels' f64 hit points (kOptHit64)
     const R4<double>* pl64;           // planes {point, 0}, {normal, 0} as given (f64): kOptHit64
+    const R4<double>* mat64;          // per material (f64, kOptHit64): {1/ior, r0 at 1/ior, r0 at ior,
+                                      // ior} (Dialectric), {-, -, -, fuzz} (Metal)
     const uint32_t* lref;             // light list in order (kLref* bits | index; null when the
                                       // list is spheres only)
     const R* boxes;                   // n_boxes x kBoxR (transformed cuboids, layout below)
@@ -149,6 +151,7 @@ constexpr uint32_t kBoxRot = 144, kBoxInv = 153, kBoxT = 162, kBoxTi = 165, kBox
                    kBoxOk = 174;
 
 constexpr uint32_t kBvhStack = 32;    // per-lane traversal stack entries (LDS)
+constexpr uint32_t kPersistResident = 0xFFFFFFFFu;   // KParams::persist: one resident grid
 
 
 template <typename R>
@@ -172,7 +175,8 @@ struct KParams {
     uint32_t item_order;              // 0: pixel-major item pool, 1: sample-major
     uint32_t hit64;                   // f32 BVH kernels: f64 ray origin / own-sphere re-hit / hit point
     uint32_t persist;                 // > 0: workgroups launched (waves take tasks from
-                                      // counters[6]); 0: one task per wave
+                                      // counters[6]; kPersistResident: as many as fit on the
+                                      // GPU at once); 0: one task per wave
 };
 
 // Host-side launch helpers (defined in render_f32.hip / render_f64.hip).

@@ -28,6 +28,43 @@
 #define RTW_EXP 0
 #endif
 
+#ifdef RTW_TIMELINE
+// tools/share_timeline.py: per wave {begin, end} wall-clock ticks (100 MHz) and
+// its task count, read back with rtw_probe_timeline_read
+constexpr uint32_t kTlWaves = 1 << 16;
+static __device__ unsigned long long g_tl[kTlWaves * 4];
+#define RTW_PROBE_WAVE_BEGIN() \
+    uint64_t tl_begin_ = wall_clock64(); \
+    uint32_t tl_tasks_ = 0, tl_last_ = 0
+#define RTW_PROBE_WAVE_TASK() (++tl_tasks_, tl_last_ = t)
+#define RTW_PROBE_WAVE_END() \
+    do { \
+        const uint32_t w_ = blockIdx.x * kWavesPerBlock + wave; \
+        if (lane == 0 && w_ < kTlWaves) { \
+            unsigned xcc_; \
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc_)); \
+            g_tl[4 * w_] = tl_begin_; \
+            g_tl[4 * w_ + 1] = wall_clock64(); \
+            g_tl[4 * w_ + 2] = tl_tasks_ | ((unsigned long long)tl_last_ << 32); \
+            g_tl[4 * w_ + 3] = xcc_ & 0xf; \
+        } \
+    } while (0)
+extern "C" int rtw_probe_timeline_read(unsigned long long* out, size_t n, int reset) {
+    n = n < (size_t)kTlWaves * 4 ? n : (size_t)kTlWaves * 4;
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tl), n * sizeof(unsigned long long)) != hipSuccess) return -1;
+    if (reset) {
+        static unsigned long long zero[kTlWaves * 4];
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_tl), zero, sizeof zero) != hipSuccess) return -1;
+    }
+    return (int)n;
+}
+#else
+#define RTW_PROBE_WAVE_BEGIN()
+#define RTW_PROBE_WAVE_TASK()
+#define RTW_PROBE_WAVE_END()
+#endif
+
 #if RTW_EXP == 5
 #define RTW_PROBE_PLANES() \
     do { \

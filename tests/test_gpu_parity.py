@@ -729,14 +729,15 @@ def test_c2_full_frame_rank_split_is_the_single_render(nranks):
 
 @pytest.mark.parametrize("prec", [rtw.RTW_F32, rtw.RTW_F64])
 def test_scheduling_knobs_do_not_change_the_image(prec):
-    """The wave item pool order (pixel- / sample-major), persistent waves (one
-    workgroup draining every task from the counter, or many) or one task per
-    wave, and the task size only move work between lanes: same image bit for
-    bit."""
+    """The wave item pool order (pixel- / sample-major), persistent waves (a
+    few workgroups draining every task from the counter, or a resident grid) or
+    one task per wave and the task size only move work between lanes: same
+    image bit for bit."""
     soa, b = _scene()
     cam = b.with_image_width(40).with_image_height(24).with_samples_per_pixel(9).with_max_depth(50).build()
     base, _, cb = _render_gpu(soa, cam, 113, prec)
-    for t in ({"item_order": 0}, {"persist": 1}, {"persist": 3, "group": 1}, {"persist": 0},
-              {"persist": 0, "target_tasks": 1000}, {"item_order": 0, "target_tasks": 1000}):
+    for t in ({"item_order": 0}, {"persist": 2}, {"persist": 3, "group": 1}, {"persist": 0},
+              {"persist": 0, "target_tasks": 1000}, {"item_order": 0, "target_tasks": 1000},
+              {"persist": 5, "group": 3}, {"persist": 1, "group": 2}):
         img, _, cv = _render_gpu(soa, cam, 113, prec, tuning=t)
         assert _same(base, img) and cb == cv, t
