@@ -723,7 +723,9 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
         group = (uint32_t)((p.n_chunks + n_groups - 1) / std::max<uint64_t>(n_groups, 1));
         group = std::max(kMinAutoGroup, std::min(group, kMaxAutoGroup));
     }
-    p.group = std::max<uint32_t>(1, std::min<uint32_t>(group, std::max<uint32_t>(p.n_chunks, 1)));
+    // at most 4096 chunks per task: the kernel divides item indices q < 64 * group
+    // by the group with a multiply-high by ceil(2^32 / group), exact while 64 group^2 < 2^32
+    p.group = std::max<uint32_t>(1, std::min<uint32_t>(std::min<uint32_t>(group, 4096u), std::max<uint32_t>(p.n_chunks, 1)));
     p.n_groups = p.n_chunks ? (p.n_chunks + p.group - 1) / p.group : 0;
     p.n_tasks = p.n_local_tiles * p.n_groups;
     p.item_order = c->item_order;

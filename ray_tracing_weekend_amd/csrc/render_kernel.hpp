@@ -1237,6 +1237,8 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
     // round-robin (rtw_tiles_for_rank) -- and chunks [c_begin, c_begin +
     // glen): a pool of n_items (pixel, chunk) items
     uint32_t lt = 0, tx = 0, ty = 0, c_begin = 0, glen = 0, n_items = 0;
+    uint32_t glen_m = 0;          // glen > 1: ceil(2^32 / glen), q / glen = umulhi(q, glen_m) for q < 64 glen
+                                  // (2^32 does not fit: glen == 1 is special-cased)
     auto set_task = [&](uint32_t t) {
         lt = t / p.n_groups;
         const uint32_t cg = t - lt * p.n_groups;
@@ -1246,6 +1248,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
         c_begin = cg * p.group;
         glen = min(c_begin + p.group, p.n_chunks) - c_begin;
         n_items = 64u * glen;
+        glen_m = glen > 1 ? (uint32_t)((0xFFFFFFFFull + glen) / glen) : 0u;
     };
     // p.persist: every wave takes tasks from a global counter until none are
     // left, and its lanes move on to the next task's items while others still
@@ -1265,7 +1268,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
     // kernel, so the image does not depend on it.
     auto decode = [&](uint32_t qq, uint32_t& px_out, uint32_t& c_out) {
         if (p.item_order) {
-            px_out = qq / glen;
+            px_out = glen > 1 ? __umulhi(qq, glen_m) : qq;   // qq / glen: exact, qq < 64 glen <= 2^18
             c_out = c_begin + (qq - px_out * glen);
         } else {
             px_out = qq & 63u;
