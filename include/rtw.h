@@ -198,6 +198,10 @@ int rtw_set_accel(rtw_ctx *ctx, int accel);
  * "robust" (f32 ray-sphere tests in closest-approach form: 1 on, 0 off,
  * 2 = by the scene's distance-to-radius ratio, the default),
  * "item_order" (wave item pool: 1 = sample-major, the default; 0 = pixel-major),
+ * "lpt" (1 = longest tiles first, the default: a blocking 2-spp pilot render of
+ * the rank's tiles counts each tile's segments and orders the tasks by it; cached
+ * until the scene, camera or rank split changes; 0 = tiles in index order),
+ * "lpt_min_spp" (renders of fewer samples per pixel skip the pilot, default 32),
  * "bvh_leaf" (spheres per BVH leaf, 1..15; 0 = auto, the default: 4, or 8 for
  * scenes of >= 100k spheres; takes effect at the
  * next rtw_set_scene), "light_bvh_min" (light lists this long or longer take the light grid
@@ -236,7 +240,9 @@ int rtw_render(rtw_ctx *ctx, const rtw_camera *cam, const rtw_scene *scene,
  * d_out[(k * 64 + ly * 8 + lx) * 3 + c] (pixels outside the image: 0).
  * d_out may be NULL when the rank has no tiles.  Asynchronous on `stream`
  * (a hipStream_t; NULL = the context's own stream).  No host synchronisation
- * inside. */
+ * inside, except once per (scene, camera, rank split) when tuning "lpt" is on
+ * and spp >= "lpt_min_spp": the pilot render whose tile costs order the tasks
+ * is read back (a 2-spp render of the rank's tiles, then cached). */
 int rtw_render_device(rtw_ctx *ctx, const rtw_camera *cam, uint64_t seed,
                       uint32_t rank, uint32_t nranks, void *d_out, size_t out_bytes,
                       void *stream);

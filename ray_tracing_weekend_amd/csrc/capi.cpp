@@ -49,6 +49,9 @@ struct rtw_ctx {
                                       // cells per light (set before rtw_set_scene); 0: light BVH
     uint32_t hit64 = 1;               // f32: f64 hit points (the reference's self-intersection odds)
     uint32_t item_order = 1;          // wave item pool: 1 sample-major (C2 +1.3 %, C3 +5 %, C5 +2 %), 0 pixel-major
+    uint32_t lpt = 1;                 // longest tiles first: task order from a pilot render's
+                                      // per-tile segment counts (cached per scene / camera / split)
+    uint32_t lpt_min_spp = 32;        // ... for renders of at least this many samples per pixel
     uint32_t light_bvh_min = 64;      // light lists at least this long use the light BVH
                                       // (C2, 19 lights: the linear masked loop is faster)
     hipStream_t stream = nullptr;
@@ -73,6 +76,15 @@ struct rtw_ctx {
     static constexpr int kCounters = 7;   // rtw_kernels.h KParams::counters
     unsigned long long* d_counters = nullptr;
     std::vector<unsigned char> h_out;
+    // longest-tiles-first order: one allocation [cost | order | pilot partial | pilot out]
+    uint64_t scene_serial = 0;        // ++ per rtw_upload_scene
+    void* d_lpt = nullptr;
+    size_t lpt_cap = 0;
+    bool lpt_valid = false;
+    rtw_camera lpt_cam{};
+    uint64_t lpt_serial = 0;
+    uint32_t lpt_rank = 0, lpt_nranks = 0, lpt_prec = 0;
+    std::vector<uint32_t> h_lpt_cost, h_lpt_order;
     rtw_stats last{};
     uint32_t last_n_sph = 0;
     std::string err;
@@ -681,6 +693,56 @@ void fill_camera(rtw::KParams<R>& p, const rtw_camera* cam) {
     p.max_depth = cam->max_depth;
 }
 
+// Longest tiles first: a 2-sample-per-pixel pilot render of the rank's tiles
+// counts each tile's segments; the tiles sorted by that count (descending,
+// ties by index) become the task order of the renders that follow, so the
+// launch does not end on a late-started tile whose samples bounce max_depth
+// times (a glass sphere's interior).  Only the order of tasks changes: every
+// item is still folded in sample order by the reduce, the image is the same
+// bit for bit.  Blocking (reads the counts back); cached by the caller.
+template <typename R>
+int lpt_pilot(rtw_ctx* c, const rtw::KParams<R>& p, int world, size_t launch_lds, hipStream_t stream) {
+    constexpr uint32_t kPilotSpp = 2;
+    const uint32_t nt = p.n_local_tiles;
+    rtw::KParams<R> q = p;
+    q.spp = std::min(p.spp, kPilotSpp);
+    q.chunk = 1;
+    q.n_chunks = q.spp;
+    q.group = q.n_chunks;
+    q.n_groups = 1;
+    q.n_tasks = nt;
+    q.seed = p.seed ^ 0x5851F42D4C957F2Dull;
+    q.tile_order = nullptr;
+    const size_t words = align_up((size_t)nt * 2, 64);
+    const size_t tile_bytes = (size_t)nt * 64 * 3 * sizeof(R);
+    const size_t bytes = words * sizeof(uint32_t) + (size_t)q.n_chunks * tile_bytes + tile_bytes;
+    int rc = ensure(c, &c->d_lpt, &c->lpt_cap, bytes);
+    if (rc) return rc;
+    uint32_t* d_cost = reinterpret_cast<uint32_t*>(c->d_lpt);
+    uint32_t* d_order = d_cost + nt;
+    R* d_part = reinterpret_cast<R*>(d_cost + words);
+    R* d_pout = d_part + (size_t)q.n_chunks * nt * 64 * 3;
+    q.partial = d_part;
+    q.tile_cost = d_cost;
+    HIP_TRY(c, hipMemsetAsync(d_cost, 0, (size_t)nt * sizeof(uint32_t), stream));
+    HIP_TRY(c, hipMemsetAsync(c->d_counters, 0, rtw_ctx::kCounters * sizeof(unsigned long long), stream));
+    int lrc;
+    if constexpr (std::is_same<R, float>::value) lrc = rtw::launch_render_f32(q, world, launch_lds, d_pout, stream, nullptr);
+    else lrc = rtw::launch_render_f64(q, world, launch_lds, d_pout, stream, nullptr);
+    if (lrc) return fail(c, RTW_E_DEVICE, std::string("pilot launch failed: ") + hipGetErrorString(hipGetLastError()));
+    c->h_lpt_cost.resize(nt);
+    c->h_lpt_order.resize(nt);
+    HIP_TRY(c, hipMemcpyAsync(c->h_lpt_cost.data(), d_cost, (size_t)nt * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+    HIP_TRY(c, hipStreamSynchronize(stream));
+    for (uint32_t k = 0; k < nt; ++k) c->h_lpt_order[k] = k;
+    const std::vector<uint32_t>& cost = c->h_lpt_cost;
+    std::stable_sort(c->h_lpt_order.begin(), c->h_lpt_order.end(),
+                     [&](uint32_t a, uint32_t b) { return cost[a] > cost[b]; });
+    HIP_TRY(c, hipMemcpyAsync(d_order, c->h_lpt_order.data(), (size_t)nt * sizeof(uint32_t), hipMemcpyHostToDevice, stream));
+    HIP_TRY(c, hipStreamSynchronize(stream));
+    return RTW_OK;
+}
+
 template <typename R>
 int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t rank, uint32_t nranks,
                     void* d_out, size_t out_bytes, hipStream_t stream) {
@@ -803,6 +865,26 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
     // f64 hit points: the f32 kernels of sphere + plane scenes (the launch
     // routes textured / quad / cuboid scenes to kernels without them)
     p.hit64 = c->hit64 ? 1u : 0u;
+    p.tile_order = nullptr;
+    p.tile_cost = nullptr;
+    if (c->lpt && need_out && p.spp >= std::max(c->lpt_min_spp, 1u) && p.max_depth && p.n_local_tiles > 1) {
+        const bool same = c->lpt_valid && c->lpt_serial == c->scene_serial && c->lpt_rank == rank &&
+                          c->lpt_nranks == nranks && c->lpt_prec == (uint32_t)sizeof(R) &&
+                          memcmp(&c->lpt_cam, cam, sizeof *cam) == 0;
+        if (!same) {
+            c->lpt_valid = false;
+            rc = lpt_pilot(c, p, world, launch_lds, stream);
+            if (rc) return rc;
+            c->lpt_valid = true;
+            c->lpt_cam = *cam;
+            c->lpt_serial = c->scene_serial;
+            c->lpt_rank = rank;
+            c->lpt_nranks = nranks;
+            c->lpt_prec = (uint32_t)sizeof(R);
+            HIP_TRY(c, hipMemsetAsync(c->d_counters, 0, rtw_ctx::kCounters * sizeof(unsigned long long), stream));
+        }
+        p.tile_order = reinterpret_cast<const uint32_t*>(c->d_lpt) + p.n_local_tiles;
+    }
     hipEvent_t* ev = c->ring[c->n_renders % rtw_ctx::kRing];
     HIP_TRY(c, hipEventRecord(c->ev0, stream));
     HIP_TRY(c, hipEventRecord(ev[0], stream));
@@ -872,6 +954,7 @@ void rtw_destroy(rtw_ctx* c) {
     if (c->d_out) (void)hipFree(c->d_out);
     if (c->d_img) (void)hipFree(c->d_img);
     if (c->d_counters) (void)hipFree(c->d_counters);
+    if (c->d_lpt) (void)hipFree(c->d_lpt);
     for (auto& tri : c->ring)
         for (auto& e : tri)
             if (e) (void)hipEventDestroy(e);
@@ -902,6 +985,8 @@ int rtw_set_tuning(rtw_ctx* c, const char* key, int64_t value) {
     else if (k == "light_grid") c->light_grid = (uint32_t)std::min<int64_t>(value, 1024);
     else if (k == "item_order") c->item_order = value ? 1u : 0u;
     else if (k == "hit64") c->hit64 = value ? 1u : 0u;
+    else if (k == "lpt") c->lpt = value ? 1u : 0u;
+    else if (k == "lpt_min_spp") c->lpt_min_spp = (uint32_t)std::min<int64_t>(value, 1u << 30);
     else if (k == "light_bvh_min") c->light_bvh_min = (uint32_t)std::min<int64_t>(value, 1u << 30);
     else if (k == "partial_max") c->partial_max = std::max<size_t>(1 << 20, (size_t)value);
     else if (k == "group") c->group = (uint32_t)value;
@@ -1066,6 +1151,7 @@ int rtw_set_scene(rtw_ctx* c, const rtw_scene* s) {
     }
     HIP_TRY(c, hipMemcpy(c->d_scene, blob.data(), blob.size(), hipMemcpyHostToDevice));
     c->has_scene = true;
+    ++c->scene_serial;
     return RTW_OK;
 }
 

@@ -1242,6 +1242,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
     auto set_task = [&](uint32_t t) {
         lt = t / p.n_groups;
         const uint32_t cg = t - lt * p.n_groups;
+        if (p.tile_order) lt = p.tile_order[lt];   // longest tiles first
         const uint32_t T = lt * p.nranks + p.rank;
         ty = T / p.tiles_x;
         tx = T - ty * p.tiles_x;
@@ -1731,6 +1732,8 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                     dst[0] = part.x;
                     dst[1] = part.y;
                     dst[2] = part.z;
+                    if (p.tile_cost)   // pilot render (chunk 1): this sample's segments
+                        atomicAdd(p.tile_cost + my_lt, p.max_depth - depth + 1u);
                     active = false;
                     need = true;
                 }

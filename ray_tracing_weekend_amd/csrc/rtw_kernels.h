@@ -177,6 +177,9 @@ struct KParams {
     uint32_t persist;                 // > 0: workgroups launched (waves take tasks from
                                       // counters[6]; kPersistResident: as many as fit on the
                                       // GPU at once); 0: one task per wave
+    const uint32_t* tile_order;       // non-null: task slot -> local tile (longest tiles first,
+                                      // from a pilot render's costs); null: identity
+    uint32_t* tile_cost;              // non-null (pilot render, chunk 1): += segments of each sample
 };
 
 // Host-side launch helpers (defined in render_f32.hip / render_f64.hip).

@@ -700,18 +700,22 @@ def test_c2_full_frame_f64_rows_match_oracle():
     assert mae < F64_MAE_TOL and exact == 1.0, (mae, exact)
 
 
-@pytest.mark.parametrize("nranks", [2, 8])
-def test_c2_full_frame_rank_split_is_the_single_render(nranks):
+@pytest.mark.parametrize("nranks,lpt", [(2, 0), (8, 0), (3, 1), (8, 1)])
+def test_c2_full_frame_rank_split_is_the_single_render(nranks, lpt):
     """rtw_render_device over nranks (the multi-GPU tile interleave, DESIGN.md
     §7) + rtw_assemble_tiles reassembles the one-rank C2-size image bit for
     bit (f32).  Every render runs on torch's current stream, the stream the
-    buffers were filled on."""
+    buffers were filled on.  lpt: every render (each rank's share, then the
+    one-rank frame again) takes its tiles longest first, the order of its own
+    pilot render."""
     import torch
     soa, b = _scene()
     H, W = 800, 1200
     cam = b.with_image_width(W).with_image_height(H).with_samples_per_pixel(2).with_max_depth(50).build()
     s = torch.cuda.current_stream().cuda_stream
     with rtw.Renderer(precision=rtw.RTW_F32) as r:
+        r.set_tuning("lpt", lpt)
+        r.set_tuning("lpt_min_spp", 1)
         r.set_scene(soa)
         one = torch.zeros((rtw.tiles_for_rank(W, H, 0, 1) * 64 * 3,), dtype=torch.float32, device="cuda:0")
         r.render_device(cam, 109, one.data_ptr(), one.numel() * 4, stream=s)
@@ -723,21 +727,26 @@ def test_c2_full_frame_rank_split_is_the_single_render(nranks):
             r.render_device(cam, 109, ranks[k].data_ptr(), per * 4, rank=k, nranks=nranks, stream=s)
         img = torch.empty_like(full)
         r.assemble_tiles(ranks.data_ptr(), per * 4, nranks, W, H, img.data_ptr(), stream=s)
+        again = torch.zeros_like(one)
+        r.render_device(cam, 109, again.data_ptr(), again.numel() * 4, stream=s)
         torch.cuda.synchronize()
     assert torch.equal(torch.nan_to_num(img, nan=-7.0), torch.nan_to_num(full, nan=-7.0))
+    assert torch.equal(torch.nan_to_num(again, nan=-7.0), torch.nan_to_num(one, nan=-7.0))
 
 
 @pytest.mark.parametrize("prec", [rtw.RTW_F32, rtw.RTW_F64])
 def test_scheduling_knobs_do_not_change_the_image(prec):
     """The wave item pool order (pixel- / sample-major), persistent waves (a
     few workgroups draining every task from the counter, or a resident grid) or
-    one task per wave and the task size only move work between lanes: same
-    image bit for bit."""
+    one task per wave and the task size only move work between lanes, and the
+    longest-tiles-first task order (a pilot render's tile costs) only moves
+    tiles between tasks: same image bit for bit."""
     soa, b = _scene()
     cam = b.with_image_width(40).with_image_height(24).with_samples_per_pixel(9).with_max_depth(50).build()
     base, _, cb = _render_gpu(soa, cam, 113, prec)
     for t in ({"item_order": 0}, {"persist": 2}, {"persist": 3, "group": 1}, {"persist": 0},
               {"persist": 0, "target_tasks": 1000}, {"item_order": 0, "target_tasks": 1000},
-              {"persist": 5, "group": 3}, {"persist": 1, "group": 2}):
+              {"persist": 5, "group": 3}, {"persist": 1, "group": 2},
+              {"lpt_min_spp": 1}, {"lpt_min_spp": 1, "persist": 0}, {"lpt_min_spp": 1, "persist": 2, "group": 1}):
         img, _, cv = _render_gpu(soa, cam, 113, prec, tuning=t)
         assert _same(base, img) and cb == cv, t
