@@ -191,16 +191,18 @@ int rtw_set_chunk(rtw_ctx *ctx, uint32_t chunk);
 int rtw_set_accel(rtw_ctx *ctx, int accel);
 /* scheduling knobs (benchmarking): "chunk" (samples per item, 0 = auto),
  * "auto_chunk", "group" (chunks per wave task, 0 = auto: 4..32), "target_tasks"
- * (auto group: about this many tasks; 0 = 2^19 with persistent waves, 2^17 without),
+ * (auto group: about this many tasks; 0 = 2^17),
  * "persist" (workgroups of persistent waves that take tasks from a global counter;
  * 1 = as many as are resident at once, the default; 0 = one task per wave),
  * "lds" (1 = stage the sphere list in LDS when it fits, 0 = read it from HBM),
  * "robust" (f32 ray-sphere tests in closest-approach form: 1 on, 0 off,
  * 2 = by the scene's distance-to-radius ratio, the default),
  * "item_order" (wave item pool: 1 = sample-major, the default; 0 = pixel-major),
- * "lpt" (1 = longest tiles first, the default: a blocking 2-spp pilot render of
- * the rank's tiles counts each tile's segments and orders the tasks by it; cached
- * until the scene, camera or rank split changes; 0 = tiles in index order),
+ * "lpt" (longest tiles first: a blocking 2-spp pilot render of the rank's tiles
+ * counts each tile's segments and orders the tasks by it, cached until the scene,
+ * camera or rank split changes; 1 = for worlds held in LDS or of at most 4 MiB
+ * (an XCD's L2), the default, 2 = for
+ * every world, 0 = tiles in index order),
  * "lpt_min_spp" (renders of fewer samples per pixel skip the pilot, default 32),
  * "bvh_leaf" (spheres per BVH leaf, 1..15; 0 = auto, the default: 4, or 8 for
  * scenes of >= 100k spheres; takes effect at the

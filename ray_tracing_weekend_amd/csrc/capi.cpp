@@ -50,7 +50,8 @@ struct rtw_ctx {
     uint32_t hit64 = 1;               // f32: f64 hit points (the reference's self-intersection odds)
     uint32_t item_order = 1;          // wave item pool: 1 sample-major (C2 +1.3 %, C3 +5 %, C5 +2 %), 0 pixel-major
     uint32_t lpt = 1;                 // longest tiles first: task order from a pilot render's
-                                      // per-tile segment counts (cached per scene / camera / split)
+                                      // per-tile segment counts (cached per scene / camera / split);
+                                      // 1: for worlds in LDS or within an L2, 2: always, 0: never
     uint32_t lpt_min_spp = 32;        // ... for renders of at least this many samples per pixel
     uint32_t light_bvh_min = 64;      // light lists at least this long use the light BVH
                                       // (C2, 19 lights: the linear masked loop is faster)
@@ -62,7 +63,8 @@ struct rtw_ctx {
     uint64_t n_renders = 0;
     // device scene (one allocation holding every array)
     void* d_scene = nullptr;
-    size_t scene_bytes = 0;
+    size_t scene_bytes = 0;           // allocation
+    size_t scene_used = 0;            // the current scene's bytes
     rtw::DevScene<float> sc32{};
     rtw::DevScene<double> sc64{};
     bool has_scene = false;
@@ -774,13 +776,15 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
     p.n_chunks = p.spp ? (p.spp + chunk - 1) / chunk : 0;
     uint32_t group = c->group;
     if (group == 0) {
-        // Persistent waves (default) have no per-task drain, only the launch's
-        // tail, which grows with the task size: ~2^19 tasks (C2 split over
-        // 1 / 2 / 4 / 8 ranks: 14 / 7 / 4 / 4 chunks per task, measured within
-        // 2 % of the best of 4..32 each).  One task per wave instead pays a
-        // drain per task: ~2^17 tasks.
+        // Persistent waves (default) have no per-task drain; a task boundary
+        // mixes two tiles' items in the wave (less coherent), the launch's tail
+        // grows with the task size.  Longest tiles first leaves cheap tiles
+        // for the end, so ~2^17 tasks (~32 per resident wave): C2 split over
+        // 1 / 2 / 4 / 8 ranks -> 32 / 28 / 15 / 8 chunks per task (N = 1:
+        // group 32 93.7 ms vs 16 94.4, 4 104.4; an 8-way share: 8 13.2 ms vs
+        // 4 13.6).  One task per wave instead pays a drain per task: ~2^17.
         constexpr uint32_t kMinAutoGroup = 4, kMaxAutoGroup = 32;
-        const uint64_t target = c->target_tasks ? c->target_tasks : (c->persist ? 1u << 19 : 1u << 17);
+        const uint64_t target = c->target_tasks ? c->target_tasks : 1u << 17;
         const uint64_t n_groups = p.n_local_tiles ? (target + p.n_local_tiles - 1) / p.n_local_tiles : 1;
         group = (uint32_t)((p.n_chunks + n_groups - 1) / std::max<uint64_t>(n_groups, 1));
         group = std::max(kMinAutoGroup, std::min(group, kMaxAutoGroup));
@@ -867,7 +871,13 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
     p.hit64 = c->hit64 ? 1u : 0u;
     p.tile_order = nullptr;
     p.tile_cost = nullptr;
-    if (c->lpt && need_out && p.spp >= std::max(c->lpt_min_spp, 1u) && p.max_depth && p.n_local_tiles > 1) {
+    // Reordering the tiles scatters the tiles in flight over the image: a tree
+    // larger than an XCD's L2 (4 MiB) loses its locality (C5, 1M spheres,
+    // ~100 MB: +8 %), so by default only worlds held in LDS or small enough
+    // for L2 take it (C2: -4 %, C3 (10k spheres): -4 %).
+    const bool on_chip = world == rtw::kWorldBvhLds || world == rtw::kWorldLds || c->scene_used <= (4u << 20);
+    if ((c->lpt == 2 || (c->lpt == 1 && on_chip)) && need_out && p.spp >= std::max(c->lpt_min_spp, 1u) &&
+        p.max_depth && p.n_local_tiles > 1) {
         const bool same = c->lpt_valid && c->lpt_serial == c->scene_serial && c->lpt_rank == rank &&
                           c->lpt_nranks == nranks && c->lpt_prec == (uint32_t)sizeof(R) &&
                           memcmp(&c->lpt_cam, cam, sizeof *cam) == 0;
@@ -985,7 +995,7 @@ int rtw_set_tuning(rtw_ctx* c, const char* key, int64_t value) {
     else if (k == "light_grid") c->light_grid = (uint32_t)std::min<int64_t>(value, 1024);
     else if (k == "item_order") c->item_order = value ? 1u : 0u;
     else if (k == "hit64") c->hit64 = value ? 1u : 0u;
-    else if (k == "lpt") c->lpt = value ? 1u : 0u;
+    else if (k == "lpt") c->lpt = (uint32_t)std::min<int64_t>(value, 2);
     else if (k == "lpt_min_spp") c->lpt_min_spp = (uint32_t)std::min<int64_t>(value, 1u << 30);
     else if (k == "light_bvh_min") c->light_bvh_min = (uint32_t)std::min<int64_t>(value, 1u << 30);
     else if (k == "partial_max") c->partial_max = std::max<size_t>(1 << 20, (size_t)value);
@@ -1112,6 +1122,7 @@ int rtw_set_scene(rtw_ctx* c, const rtw_scene* s) {
         HIP_TRY(c, hipMalloc(&c->d_scene, blob.size()));
         c->scene_bytes = blob.size();
     }
+    c->scene_used = blob.size();
     // scale of the scene for the f32 test choice (render_device_t)
     c->scene_extent = 0.0;
     c->min_radius = INFINITY;

@@ -747,6 +747,7 @@ def test_scheduling_knobs_do_not_change_the_image(prec):
     for t in ({"item_order": 0}, {"persist": 2}, {"persist": 3, "group": 1}, {"persist": 0},
               {"persist": 0, "target_tasks": 1000}, {"item_order": 0, "target_tasks": 1000},
               {"persist": 5, "group": 3}, {"persist": 1, "group": 2},
-              {"lpt_min_spp": 1}, {"lpt_min_spp": 1, "persist": 0}, {"lpt_min_spp": 1, "persist": 2, "group": 1}):
+              {"lpt_min_spp": 1}, {"lpt_min_spp": 1, "persist": 0}, {"lpt_min_spp": 1, "persist": 2, "group": 1},
+              {"lpt": 2, "lpt_min_spp": 1, "lds": 0}):
         img, _, cv = _render_gpu(soa, cam, 113, prec, tuning=t)
         assert _same(base, img) and cb == cv, t
