@@ -80,13 +80,20 @@ struct rtw_ctx {
     std::vector<unsigned char> h_out;
     // longest-tiles-first order: one allocation [cost | order | pilot partial | pilot out]
     uint64_t scene_serial = 0;        // ++ per rtw_upload_scene
-    void* d_lpt = nullptr;
+    static constexpr uint32_t kPilotSpp = 2, kMaxGroup = 32;
+    void* d_lpt = nullptr;            // pilot: [tile cost | chunk sums | tiles]
     size_t lpt_cap = 0;
-    bool lpt_valid = false;
+    bool lpt_valid = false;           // h_lpt_cost is the pilot of (lpt_cam, lpt_serial, rank split, precision)
     rtw_camera lpt_cam{};
     uint64_t lpt_serial = 0;
     uint32_t lpt_rank = 0, lpt_nranks = 0, lpt_prec = 0;
-    std::vector<uint32_t> h_lpt_cost, h_lpt_order;
+    std::vector<uint32_t> h_lpt_cost;
+    void* d_lpt_tasks = nullptr;      // the task list of (h_lpt_cost, lpt_tab_*)
+    size_t lpt_tasks_cap = 0;
+    bool lpt_tab_valid = false;
+    uint32_t lpt_tab_chunks = 0, lpt_tab_group = 0;
+    uint64_t lpt_tab_target = 0;
+    std::vector<uint32_t> h_lpt_tasks;
     rtw_stats last{};
     uint32_t last_n_sph = 0;
     std::string err;
@@ -95,6 +102,7 @@ struct rtw_ctx {
 namespace {
 
 constexpr size_t kLdsLimit = 160 * 1024;
+constexpr uint64_t kAutoTasks = 1u << 17;   // auto task size: about this many tasks per render
 
 int fail(rtw_ctx* c, int code, const std::string& msg) {
     if (c) c->err = msg;
@@ -696,32 +704,26 @@ void fill_camera(rtw::KParams<R>& p, const rtw_camera* cam) {
 }
 
 // Longest tiles first: a 2-sample-per-pixel pilot render of the rank's tiles
-// counts each tile's segments; the tiles sorted by that count (descending,
-// ties by index) become the task order of the renders that follow, so the
-// launch does not end on a late-started tile whose samples bounce max_depth
-// times (a glass sphere's interior).  Only the order of tasks changes: every
-// item is still folded in sample order by the reduce, the image is the same
-// bit for bit.  Blocking (reads the counts back); cached by the caller.
+// counts each tile's segments (h_lpt_cost); lpt_tasks turns them into the task
+// list.  Blocking (reads the counts back); cached by the caller.
 template <typename R>
 int lpt_pilot(rtw_ctx* c, const rtw::KParams<R>& p, int world, size_t launch_lds, hipStream_t stream) {
-    constexpr uint32_t kPilotSpp = 2;
     const uint32_t nt = p.n_local_tiles;
     rtw::KParams<R> q = p;
-    q.spp = std::min(p.spp, kPilotSpp);
+    q.spp = std::min(p.spp, rtw_ctx::kPilotSpp);
     q.chunk = 1;
     q.n_chunks = q.spp;
     q.group = q.n_chunks;
     q.n_groups = 1;
     q.n_tasks = nt;
     q.seed = p.seed ^ 0x5851F42D4C957F2Dull;
-    q.tile_order = nullptr;
-    const size_t words = align_up((size_t)nt * 2, 64);
+    q.task_table = nullptr;
+    const size_t words = align_up((size_t)nt, 64);
     const size_t tile_bytes = (size_t)nt * 64 * 3 * sizeof(R);
     const size_t bytes = words * sizeof(uint32_t) + (size_t)q.n_chunks * tile_bytes + tile_bytes;
     int rc = ensure(c, &c->d_lpt, &c->lpt_cap, bytes);
     if (rc) return rc;
     uint32_t* d_cost = reinterpret_cast<uint32_t*>(c->d_lpt);
-    uint32_t* d_order = d_cost + nt;
     R* d_part = reinterpret_cast<R*>(d_cost + words);
     R* d_pout = d_part + (size_t)q.n_chunks * nt * 64 * 3;
     q.partial = d_part;
@@ -733,14 +735,47 @@ int lpt_pilot(rtw_ctx* c, const rtw::KParams<R>& p, int world, size_t launch_lds
     else lrc = rtw::launch_render_f64(q, world, launch_lds, d_pout, stream, nullptr);
     if (lrc) return fail(c, RTW_E_DEVICE, std::string("pilot launch failed: ") + hipGetErrorString(hipGetLastError()));
     c->h_lpt_cost.resize(nt);
-    c->h_lpt_order.resize(nt);
     HIP_TRY(c, hipMemcpyAsync(c->h_lpt_cost.data(), d_cost, (size_t)nt * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
     HIP_TRY(c, hipStreamSynchronize(stream));
-    for (uint32_t k = 0; k < nt; ++k) c->h_lpt_order[k] = k;
+    return RTW_OK;
+}
+
+// The task list from the pilot's tile costs: tiles longest first (ties by
+// index), each cut into tasks of g chunks.  With the auto task size, g is
+// sized per tile so that tasks cost about the same (total cost / target
+// tasks, 1..kMaxGroup chunks): a tile whose every sample bounces max_depth
+// times (a glass sphere's interior) gets 1-chunk tasks and no task outlasts
+// the launch's tail; cheap tiles (sky) get long ones, fewer task switches.
+// Only the order and cut of tasks change: every item is still one (pixel,
+// chunk) folded in sample order by the reduce, the image is the same bit for
+// bit.  Entry: {local tile, first chunk | chunks << 20}.
+template <typename R>
+int lpt_tasks(rtw_ctx* c, const rtw::KParams<R>& p, uint32_t fixed_group, uint64_t target, hipStream_t stream) {
+    const uint32_t nt = p.n_local_tiles;
     const std::vector<uint32_t>& cost = c->h_lpt_cost;
-    std::stable_sort(c->h_lpt_order.begin(), c->h_lpt_order.end(),
-                     [&](uint32_t a, uint32_t b) { return cost[a] > cost[b]; });
-    HIP_TRY(c, hipMemcpyAsync(d_order, c->h_lpt_order.data(), (size_t)nt * sizeof(uint32_t), hipMemcpyHostToDevice, stream));
+    std::vector<uint32_t> order(nt);
+    for (uint32_t k = 0; k < nt; ++k) order[k] = k;
+    std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return cost[a] > cost[b]; });
+    double total = 0;
+    for (uint32_t k = 0; k < nt; ++k) total += std::max<uint32_t>(cost[k], 1);
+    const double per_task = total * p.n_chunks / (double)std::max<uint64_t>(target, 1);   // pilot-cost units x chunks
+    std::vector<uint32_t>& tab = c->h_lpt_tasks;
+    tab.clear();
+    for (uint32_t k : order) {
+        uint32_t g = fixed_group;
+        if (!g) {
+            const double want = per_task / (double)std::max<uint32_t>(cost[k], 1);
+            g = (uint32_t)std::max(1.0, std::min((double)rtw_ctx::kMaxGroup, std::floor(want + 0.5)));
+        }
+        g = std::min(g, p.n_chunks);
+        for (uint32_t cb = 0; cb < p.n_chunks; cb += g) {
+            tab.push_back(k);
+            tab.push_back(cb | (std::min(g, p.n_chunks - cb) << 20));
+        }
+    }
+    int rc = ensure(c, &c->d_lpt_tasks, &c->lpt_tasks_cap, tab.size() * sizeof(uint32_t));
+    if (rc) return rc;
+    HIP_TRY(c, hipMemcpyAsync(c->d_lpt_tasks, tab.data(), tab.size() * sizeof(uint32_t), hipMemcpyHostToDevice, stream));
     HIP_TRY(c, hipStreamSynchronize(stream));
     return RTW_OK;
 }
@@ -784,7 +819,7 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
         // group 32 93.7 ms vs 16 94.4, 4 104.4; an 8-way share: 8 13.2 ms vs
         // 4 13.6).  One task per wave instead pays a drain per task: ~2^17.
         constexpr uint32_t kMinAutoGroup = 4, kMaxAutoGroup = 32;
-        const uint64_t target = c->target_tasks ? c->target_tasks : 1u << 17;
+        const uint64_t target = c->target_tasks ? c->target_tasks : kAutoTasks;
         const uint64_t n_groups = p.n_local_tiles ? (target + p.n_local_tiles - 1) / p.n_local_tiles : 1;
         group = (uint32_t)((p.n_chunks + n_groups - 1) / std::max<uint64_t>(n_groups, 1));
         group = std::max(kMinAutoGroup, std::min(group, kMaxAutoGroup));
@@ -869,7 +904,7 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
     // f64 hit points: the f32 kernels of sphere + plane scenes (the launch
     // routes textured / quad / cuboid scenes to kernels without them)
     p.hit64 = c->hit64 ? 1u : 0u;
-    p.tile_order = nullptr;
+    p.task_table = nullptr;
     p.tile_cost = nullptr;
     // Reordering the tiles scatters the tiles in flight over the image: a tree
     // larger than an XCD's L2 (4 MiB) loses its locality (C5, 1M spheres,
@@ -877,12 +912,13 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
     // for L2 take it (C2: -4 %, C3 (10k spheres): -4 %).
     const bool on_chip = world == rtw::kWorldBvhLds || world == rtw::kWorldLds || c->scene_used <= (4u << 20);
     if ((c->lpt == 2 || (c->lpt == 1 && on_chip)) && need_out && p.spp >= std::max(c->lpt_min_spp, 1u) &&
-        p.max_depth && p.n_local_tiles > 1) {
+        p.max_depth && p.n_local_tiles > 1 && p.n_chunks < (1u << 20)) {
         const bool same = c->lpt_valid && c->lpt_serial == c->scene_serial && c->lpt_rank == rank &&
                           c->lpt_nranks == nranks && c->lpt_prec == (uint32_t)sizeof(R) &&
                           memcmp(&c->lpt_cam, cam, sizeof *cam) == 0;
         if (!same) {
             c->lpt_valid = false;
+            c->lpt_tab_valid = false;
             rc = lpt_pilot(c, p, world, launch_lds, stream);
             if (rc) return rc;
             c->lpt_valid = true;
@@ -893,7 +929,19 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
             c->lpt_prec = (uint32_t)sizeof(R);
             HIP_TRY(c, hipMemsetAsync(c->d_counters, 0, rtw_ctx::kCounters * sizeof(unsigned long long), stream));
         }
-        p.tile_order = reinterpret_cast<const uint32_t*>(c->d_lpt) + p.n_local_tiles;
+        const uint64_t target = c->target_tasks ? c->target_tasks : kAutoTasks;
+        if (!c->lpt_tab_valid || c->lpt_tab_chunks != p.n_chunks || c->lpt_tab_group != c->group ||
+            c->lpt_tab_target != target) {
+            c->lpt_tab_valid = false;
+            rc = lpt_tasks(c, p, c->group ? p.group : 0u, target, stream);
+            if (rc) return rc;
+            c->lpt_tab_valid = true;
+            c->lpt_tab_chunks = p.n_chunks;
+            c->lpt_tab_group = c->group;
+            c->lpt_tab_target = target;
+        }
+        p.task_table = reinterpret_cast<const uint32_t*>(c->d_lpt_tasks);
+        p.n_tasks = (uint32_t)(c->h_lpt_tasks.size() / 2);
     }
     hipEvent_t* ev = c->ring[c->n_renders % rtw_ctx::kRing];
     HIP_TRY(c, hipEventRecord(c->ev0, stream));
@@ -965,6 +1013,7 @@ void rtw_destroy(rtw_ctx* c) {
     if (c->d_img) (void)hipFree(c->d_img);
     if (c->d_counters) (void)hipFree(c->d_counters);
     if (c->d_lpt) (void)hipFree(c->d_lpt);
+    if (c->d_lpt_tasks) (void)hipFree(c->d_lpt_tasks);
     for (auto& tri : c->ring)
         for (auto& e : tri)
             if (e) (void)hipEventDestroy(e);

@@ -1240,14 +1240,20 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
     uint32_t glen_m = 0;          // glen > 1: ceil(2^32 / glen), q / glen = umulhi(q, glen_m) for q < 64 glen
                                   // (2^32 does not fit: glen == 1 is special-cased)
     auto set_task = [&](uint32_t t) {
-        lt = t / p.n_groups;
-        const uint32_t cg = t - lt * p.n_groups;
-        if (p.tile_order) lt = p.tile_order[lt];   // longest tiles first
+        if (p.task_table) {   // longest tiles first, cut by cost
+            lt = p.task_table[2 * t];
+            const uint32_t e = p.task_table[2 * t + 1];
+            c_begin = e & 0xFFFFFu;
+            glen = e >> 20;
+        } else {
+            lt = t / p.n_groups;
+            const uint32_t cg = t - lt * p.n_groups;
+            c_begin = cg * p.group;
+            glen = min(c_begin + p.group, p.n_chunks) - c_begin;
+        }
         const uint32_t T = lt * p.nranks + p.rank;
         ty = T / p.tiles_x;
         tx = T - ty * p.tiles_x;
-        c_begin = cg * p.group;
-        glen = min(c_begin + p.group, p.n_chunks) - c_begin;
         n_items = 64u * glen;
         glen_m = glen > 1 ? (uint32_t)((0xFFFFFFFFull + glen) / glen) : 0u;
     };

@@ -177,8 +177,9 @@ struct KParams {
     uint32_t persist;                 // > 0: workgroups launched (waves take tasks from
                                       // counters[6]; kPersistResident: as many as fit on the
                                       // GPU at once); 0: one task per wave
-    const uint32_t* tile_order;       // non-null: task slot -> local tile (longest tiles first,
-                                      // from a pilot render's costs); null: identity
+    const uint32_t* task_table;       // non-null: task t = {local tile, first chunk | chunks << 20}
+                                      // at [2t, 2t + 1] (longest tiles first, sized by a pilot
+                                      // render's costs); null: t = tile * n_groups + group
     uint32_t* tile_cost;              // non-null (pilot render, chunk 1): += segments of each sample
 };
 

@@ -5,7 +5,7 @@ RTW_TIMELINE build of librtw.so): every wave's begin / end wall-clock tick
 spread of wave start and end times, the idle tail, per-XCD end times.
 
     python tools/share_timeline.py build                  # here (hipcc cross-compiles)
-    python tools/share_timeline.py run [--ns 1,8] [--tuning k=v,...]
+    python tools/share_timeline.py run [--ns 1,8] [--rank K] [--tuning k=v,...]
 """
 import argparse
 import ctypes as C
@@ -53,7 +53,7 @@ def run(a):
     r.render_device(cam, 1, out.data_ptr(), out.numel() * 4)
     for n in (int(x) for x in a.ns.split(",")):
         rd(buf_tl, n_tl, 1)
-        r.render_device(cam, 7, out.data_ptr(), out.numel() * 4, rank=0, nranks=n)
+        r.render_device(cam, 7, out.data_ptr(), out.numel() * 4, rank=min(a.rank, n - 1), nranks=n)
         torch.cuda.synchronize()
         kern = r.get_timings(1)[0][0]
         rd(buf_tl, n_tl, 1)
@@ -68,7 +68,7 @@ def run(a):
         q = lambda x, p: float(np.percentile(x, p))
         xcc = {int(x): round(float(end[t[:, 3] == x].max()) / 1e3, 3) for x in np.unique(t[:, 3])}
         print(json.dumps({
-            "nranks": n, "tuning": a.tuning, "kernel_ms": round(kern, 3), "waves": int(len(t)),
+            "nranks": n, "rank": min(a.rank, n - 1), "segments": int(r.get_stats().segments), "tuning": a.tuning, "kernel_ms": round(kern, 3), "waves": int(len(t)),
             "span_ms": round(span / 1e3, 3),
             "begin_us_p50_p99_max": [round(q(beg, 50), 1), round(q(beg, 99), 1), round(float(beg.max()), 1)],
             "end_ms_p1_p50_p90_p99_max": [round(q(end, p) / 1e3, 3) for p in (1, 50, 90, 99)] + [round(span / 1e3, 3)],
@@ -85,5 +85,6 @@ if __name__ == "__main__":
     ap.add_argument("mode", choices=["build", "run"])
     ap.add_argument("--ns", default="1,8")
     ap.add_argument("--tuning", default="")
+    ap.add_argument("--rank", type=int, default=0)
     a = ap.parse_args()
     build() if a.mode == "build" else run(a)
