@@ -78,7 +78,7 @@ struct rtw_ctx {
     static constexpr int kCounters = 7;   // rtw_kernels.h KParams::counters
     unsigned long long* d_counters = nullptr;
     std::vector<unsigned char> h_out;
-    // longest-tiles-first order: one allocation [cost | order | pilot partial | pilot out]
+    // longest-tiles-first task list (pilot render, see lpt_pilot / lpt_tasks)
     uint64_t scene_serial = 0;        // ++ per rtw_upload_scene
     static constexpr uint32_t kPilotSpp = 2, kMaxGroup = 32;
     void* d_lpt = nullptr;            // pilot: [tile cost | chunk sums | tiles]

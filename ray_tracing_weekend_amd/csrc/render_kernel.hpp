@@ -16,7 +16,7 @@
 // lengths range from 1 to max_depth segments (its t_min = f64::EPSILON makes
 // self-intersecting, depth-long paths common).
 //
-// Chunk sums land in partial[chunk][tile][pixel]; reduce_chunks_kernel folds
+// Chunk sums land in partial[tile][pixel][chunk]; reduce_chunks_kernel folds
 // them in chunk order.  Inside a chunk the samples are folded exactly like
 // `(0..spp).map(..).fold(Colour::default(), +)` (camera.rs:323-335), so with
 // chunk >= spp the f64 result is the reference's fold order bit for bit.
@@ -1734,7 +1734,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                     start_sample();
                 RTW_PROBE_LANES(10);
                 } else {
-                    R* dst = p.partial + (((size_t)c * p.n_local_tiles + my_lt) * 64 + px) * 3;
+                    R* dst = p.partial + (((size_t)my_lt * 64 + px) * p.n_chunks + c) * 3;
                     dst[0] = part.x;
                     dst[1] = part.y;
                     dst[2] = part.z;
@@ -1769,25 +1769,57 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
 // image: 0).  The fold accumulates in double whatever R is: with many chunks
 // (C4: 4096 spp) an f32 running sum would lose low bits; in f64 mode this is
 // the reference's sequential f64 fold (camera.rs:323-335).
+constexpr uint32_t kFoldWindow = 16;                  // chunks staged per pass
+constexpr uint32_t kFoldRow = kFoldWindow * 3 + 1;    // LDS row (odd: no bank conflicts)
+
 template <typename R>
-__global__ void __launch_bounds__(256) reduce_chunks_kernel(const KParams<R> p, R* __restrict__ out) {
-    const uint32_t gid = blockIdx.x * 256 + threadIdx.x;
-    const uint32_t lt = gid >> 6, lane = gid & 63;
-    if (lt >= p.n_local_tiles) return;
+__global__ void __launch_bounds__(64) reduce_chunks_kernel(const KParams<R> p, R* __restrict__ out) {
+    // one wave per tile; a pixel's chunk sums are contiguous (the sample-major
+    // item pool hands the lanes consecutive chunks of one pixel, whose sums
+    // then fill whole cache lines together), so the wave stages a window of
+    // kFoldWindow chunks x 64 pixels through LDS with row-contiguous loads and
+    // each lane folds its pixel's row in chunk order
+    __shared__ R win[64 * kFoldRow];
+    const uint32_t lt = blockIdx.x, lane = threadIdx.x;
     const uint32_t T = lt * p.nranks + p.rank;
     const uint32_t ty = T / p.tiles_x, tx = T - ty * p.tiles_x;
     const uint32_t i = tx * kTile + (lane & 7), j = ty * kTile + (lane >> 3);
+    const size_t row_len = (size_t)p.n_chunks * 3;
+    const R* tile = p.partial + (size_t)lt * 64 * row_len;
     double sx = 0, sy = 0, sz = 0;
-    if (i < p.W && j < p.H) {
-        const size_t stride = (size_t)p.n_local_tiles * 64 * 3;
-        const R* src = p.partial + ((size_t)lt * 64 + lane) * 3;
-        for (uint32_t c = 0; c < p.n_chunks; ++c) {
-            sx = sx + (double)src[0];
-            sy = sy + (double)src[1];
-            sz = sz + (double)src[2];
-            src += stride;
+    constexpr uint32_t kNv = kFoldWindow * 3;
+    for (uint32_t c0 = 0; c0 < p.n_chunks; c0 += kFoldWindow) {
+        const uint32_t kw = min(kFoldWindow, p.n_chunks - c0), nv = kw * 3;
+        const R* src = tile + (size_t)c0 * 3;
+        if (kw == kFoldWindow) {
+            // full window: every lane's kNv loads issued back to back
+            R v[kNv];
+#pragma unroll
+            for (uint32_t it = 0; it < kNv; ++it) {
+                const uint32_t idx = it * 64 + lane, r = idx / kNv, col = idx - r * kNv;
+                v[it] = src[r * row_len + col];
+            }
+#pragma unroll
+            for (uint32_t it = 0; it < kNv; ++it) {
+                const uint32_t idx = it * 64 + lane, r = idx / kNv, col = idx - r * kNv;
+                win[r * kFoldRow + col] = v[it];
+            }
+        } else {
+            for (uint32_t idx = lane; idx < 64 * nv; idx += 64) {
+                const uint32_t r = idx / nv, col = idx - r * nv;
+                win[r * kFoldRow + col] = src[r * row_len + col];
+            }
         }
+        __syncthreads();
+        const R* row = win + lane * kFoldRow;
+        for (uint32_t k = 0; k < kw; ++k) {
+            sx = sx + (double)row[3 * k];
+            sy = sy + (double)row[3 * k + 1];
+            sz = sz + (double)row[3 * k + 2];
+        }
+        __syncthreads();
     }
+    if (i >= p.W || j >= p.H) sx = sy = sz = 0;   // never written
     R* dst = out + ((size_t)lt * 64 + lane) * 3;
     dst[0] = (R)sx;
     dst[1] = (R)sy;
@@ -1956,9 +1988,8 @@ inline int launch_render_impl(const KParams<R>& p, int world, size_t lds_bytes, 
         if (hipGetLastError() != hipSuccess) return -1;
     }
     if (mid && hipEventRecord(mid, stream) != hipSuccess) return -1;
-    const uint32_t rblocks = (p.n_local_tiles * 64 + 255) / 256;
-    if (rblocks) {
-        hipLaunchKernelGGL((dev::reduce_chunks_kernel<R>), dim3(rblocks), dim3(256), 0, stream, p,
+    if (p.n_local_tiles) {
+        hipLaunchKernelGGL((dev::reduce_chunks_kernel<R>), dim3(p.n_local_tiles), dim3(64), 0, stream, p,
                            out);
         if (hipGetLastError() != hipSuccess) return -1;
     }

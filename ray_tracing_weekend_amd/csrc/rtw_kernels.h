@@ -157,7 +157,7 @@ constexpr uint32_t kPersistResident = 0xFFFFFFFFu;   // KParams::persist: one re
 template <typename R>
 struct KParams {
     DevScene<R> sc;
-    R* partial;                       // [n_chunks][n_local_tiles][64][3] item (chunk) sums
+    R* partial;                       // [n_local_tiles][64][n_chunks][3] item (chunk) sums
     unsigned long long* counters;     // [0] segments, [1] lambertian, [2] node visits,
                                       // [3] sphere tests, [4] plane-UV panics, [5] empty-light panics,
                                       // [6] next task (persistent waves)

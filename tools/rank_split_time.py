@@ -45,7 +45,7 @@ def main():
     torch.cuda.synchronize()
     base = None
     for n in (int(x) for x in a.ns.split(",")):
-        per_rank, kern = [], []
+        per_rank, kern, rend = [], [], []
         only = [int(x) for x in a.ranks.split(",")] if a.ranks else range(n)
         for rank in only:
             best = float("inf")
@@ -55,7 +55,9 @@ def main():
                 r.render_device(cam, 7, buf.data_ptr(), buf.numel() * 4, rank=rank, nranks=n)
                 torch.cuda.synchronize()
                 best = min(best, time.perf_counter() - t0)
-            kern.append(min(r.get_timings(a.reps)[1]))
+            tm = r.get_timings(a.reps)
+            kern.append(min(tm[1]))
+            rend.append(min(tm[0]))
             per_rank.append(best * 1e3)
         slowest = max(per_rank)
         base = base or slowest
@@ -63,6 +65,7 @@ def main():
         print(json.dumps({"size": a.size, "spp": SPP, "tuning": a.tuning, "nranks": n, "ranks": list(only),
                           "chunk": int(st.chunk), "max_rank_ms": round(slowest, 2), "min_rank_ms": round(min(per_rank), 2),
                           "speedup_vs_1": round(base / slowest, 2), "max_rank_launch_ms": round(max(kern), 2),
+                          "max_rank_render_kernel_ms": round(max(rend), 2),
                           "msamples_s_if_parallel": round(W * H * SPP / (slowest * 1e-3) / 1e6, 1),
                           "per_rank_ms": [round(x, 2) for x in per_rank]}), flush=True)
     r.close()
