@@ -1,5 +1,7 @@
 #!/usr/bin/env python3
-"""Summarise rocprofv3 PMC csvs for the render kernel: per-dispatch averages."""
+"""Summarise rocprofv3 PMC csvs for the render kernel: per-dispatch averages
+over the full renders (a launch under a quarter of the largest one of a
+counter -- the 2-spp tile-cost pilot render -- is left out)."""
 import collections, csv, glob, sys
 root = sys.argv[1]
 agg = collections.defaultdict(list)
@@ -9,8 +11,12 @@ for f in sorted(glob.glob(f"{root}/pmc*/pmc_counter_collection.csv")):
         if "render_kernel" not in row["Kernel_Name"]:
             continue
         per[(row["Dispatch_Id"], row["Counter_Name"])] += float(row["Counter_Value"])
+    top = collections.defaultdict(float)
     for (d, name), v in per.items():
-        agg[name].append(v)
+        top[name] = max(top[name], v)
+    for (d, name), v in per.items():
+        if v >= 0.25 * top[name]:
+            agg[name].append(v)
 for k in sorted(agg):
     v = agg[k]
     print(f"{k:32s} {sum(v)/len(v):.4e}  (n={len(v)})")
