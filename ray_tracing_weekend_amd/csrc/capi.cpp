@@ -292,6 +292,9 @@ std::vector<unsigned char> stage_scene(const rtw_scene* s, rtw::DevScene<R>* ds,
     const rtw::BvhBuild bb = rtw::build_bvh(s->spheres, s->n_spheres,
                                             std::is_same<R, float>::value ? 1e-5 : 1e-12, leaf_max);
     const size_t o_nodes = reserve(sizeof(rtw::BvhNode<R>) * bb.nodes.size());
+    // f64: the same tree in f32 (boxes rounded outward), which the while-while
+    // traversal culls on with an error slack (bvh_traverse_ww)
+    const size_t o_nodes32 = reserve(std::is_same<R, double>::value ? sizeof(rtw::BvhNode<float>) * bb.nodes.size() : 0);
     const size_t o_bsph = reserve(sizeof(R4) * s->n_spheres);
     const size_t o_bid = reserve(sizeof(uint32_t) * s->n_spheres);
     // isolated spheres (self-hit shortcut): bit 31 of sphere_mat.  The margin
@@ -505,6 +508,30 @@ std::vector<unsigned char> stage_scene(const rtw_scene* s, rtw::DevScene<R>* ds,
     };
     for (size_t k = 0; k < bb.nodes.size(); ++k)
         reinterpret_cast<rtw::BvhNode<R>*>(b + o_nodes)[k] = pack_node(bb.nodes[k]);
+    if constexpr (std::is_same<R, double>::value) {
+        auto down32 = [](double x) {
+            float r = (float)x;
+            return (double)r > x ? std::nextafter(r, -INFINITY) : r;
+        };
+        auto up32 = [](double x) {
+            float r = (float)x;
+            return (double)r < x ? std::nextafter(r, INFINITY) : r;
+        };
+        for (size_t k = 0; k < bb.nodes.size(); ++k) {
+            const rtw::BvhBuild::Node& n = bb.nodes[k];
+            rtw::BvhNode<float> d{};
+            for (int c = 0; c < 2; ++c) {
+                d.lo_x[c] = down32(n.lo[c][0]);
+                d.lo_y[c] = down32(n.lo[c][1]);
+                d.lo_z[c] = down32(n.lo[c][2]);
+                d.hi_x[c] = up32(n.hi[c][0]);
+                d.hi_y[c] = up32(n.hi[c][1]);
+                d.hi_z[c] = up32(n.hi[c][2]);
+                d.child[c] = n.child[c];
+            }
+            reinterpret_cast<rtw::BvhNode<float>*>(b + o_nodes32)[k] = d;
+        }
+    }
     for (uint32_t k = 0; k < s->n_spheres; ++k) {
         const uint32_t id = bb.order[k];
         reinterpret_cast<R4*>(b + o_bsph)[k] = reinterpret_cast<const R4*>(b + o_sph)[id];
@@ -579,6 +606,8 @@ std::vector<unsigned char> stage_scene(const rtw_scene* s, rtw::DevScene<R>* ds,
     ds->n_nodes4 = (uint32_t)n4;
     ds->bvh4_stack = b4.max_stack;
     ds->bvh = reinterpret_cast<const rtw::BvhNode<R>*>(base + o_nodes);
+    if constexpr (std::is_same<R, double>::value)
+        ds->bvh32 = reinterpret_cast<const rtw::BvhNode<float>*>(base + o_nodes32);
     ds->bsph = reinterpret_cast<const R4*>(base + o_bsph);
     ds->bid = reinterpret_cast<const uint32_t*>(base + o_bid);
     ds->n_sph = s->n_spheres;
@@ -869,8 +898,8 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
         // binary traversal pushes at most one entry per inner level
         const uint32_t bin_stack = std::max(p.sc.bvh_depth + 1, min_stack);
         const size_t stacks = (size_t)rtw::kWavesPerBlock * 64 * sizeof(int32_t);
-        // kWorldBvhLds layout: stacks | nodes | leaf spheres | ids (padded to 8) | lights | (f32) light pairs
-        const size_t tree_lds = stacks * bin_stack + (size_t)p.sc.n_nodes * sizeof(rtw::BvhNode<R>) +
+        // kWorldBvhLds layout: stacks | f32 nodes (bvh32) | leaf spheres | ids (padded to 8) | lights | (f32) light pairs
+        const size_t tree_lds = stacks * bin_stack + (size_t)p.sc.n_nodes * sizeof(rtw::BvhNode<float>) +
                                 (size_t)p.sc.n_sph * sizeof(rtw::R4<R>) +
                                 (size_t)((p.sc.n_sph + 7u) & ~7u) * sizeof(uint32_t) +
                                 (size_t)p.sc.n_lights * sizeof(rtw::R4<R>) +
@@ -1193,9 +1222,11 @@ int rtw_set_scene(rtw_ctx* c, const rtw_scene* s) {
         };
         fix(ds.sph); fix(ds.sph_r); fix(ds.sph_mat); fix(ds.sph_shade); fix(ds.planes); fix(ds.plane_mat);
         fix(ds.mat_type); fix(ds.mat_p); fix(ds.lights); fix(ds.bvh); fix(ds.bsph); fix(ds.bid);
-        fix(ds.bvh4); fix(ds.lbvh); fix(ds.lsph); fix(ds.lid); fix(ds.lg_start); fix(ds.lg_sph); fix(ds.lg_id);
+        fix(ds.bvh4); fix(ds.lbvh);
+        fix(ds.lsph); fix(ds.lid); fix(ds.lg_start); fix(ds.lg_sph); fix(ds.lg_id);
         fix(ds.quads); fix(ds.quad_mat); fix(ds.lquads); fix(ds.sph64); fix(ds.pl64); fix(ds.mat64);
         if (ds.lref) fix(ds.lref);
+        if constexpr (std::is_same<std::decay_t<decltype(ds)>, rtw::DevScene<double>>::value) fix(ds.bvh32);
         fix(ds.boxes); fix(ds.box_mat);
         if (ds.mat_tex) fix(ds.mat_tex);
         fix(ds.tex_type); fix(ds.tex_p); fix(ds.tex_refs); fix(ds.perlin_vec); fix(ds.perlin_perm);

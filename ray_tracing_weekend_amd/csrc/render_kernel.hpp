@@ -530,14 +530,42 @@ __device__ __forceinline__ void test_leaf(const DevScene<R>& sc, int32_t base, i
 // branch.  A lane that reaches a leaf parks it and keeps descending until it
 // holds a second leaf; the inner phase ends when every lane holds a leaf (or
 // is done), then all parked leaves are tested together.
+//
+// Both precisions cull on the f32 tree (sc.bvh32).  An f64 ray (the parity
+// mode) is rounded to f32 and every slab interval is widened by a bound on
+// the error of that f32 arithmetic, so a box the exact f64 ray meets within
+// [0, tb] is never culled; the spheres that survive are tested in f64 as
+// before (the result is the brute-force result, bit for bit).  With ix the
+// f32 reciprocal (1 ulp) of the rounded direction, o and d rounded (2^-24),
+// each slab parameter t = (b - o) / d comes out within
+// |t| 2^-22 + |o ix| 2^-22.9 of its exact value; the interval [tn, tf] is
+// widened to [tn (1 - 2^-20) - s, tf (1 + 2^-20) + s], s = 2^-20 max |o ix|,
+// and the bound tb is rounded up to f32.
+__device__ __forceinline__ const BvhNode<float>* cull_nodes(const DevScene<float>& sc) { return sc.bvh; }
+__device__ __forceinline__ const BvhNode<float>* cull_nodes(const DevScene<double>& sc) { return sc.bvh32; }
+__device__ __forceinline__ float cull_bound(float t) { return t; }
+__device__ __forceinline__ float cull_bound(double t) {   // t rounded up to f32
+    const float f = (float)t;
+    return (double)f < t ? __uint_as_float(__float_as_uint(f) + 1u) : f;   // t > 0
+}
 template <typename R, typename TT>
 __device__ __forceinline__ void bvh_traverse_ww(const DevScene<R>& sc, int32_t base, V3<R> o, V3<R> d,
                                                 TT& T, int32_t* __restrict__ stk,
                                                 uint32_t& nvis, uint32_t& ntest, bool skip) {
     constexpr int32_t kDone = 0x7fffffff;
-    const R ix = inv_(d.x), iy = inv_(d.y), iz = inv_(d.z);
-    const R oix = o.x * ix, oiy = o.y * iy, oiz = o.z * iz;
-    const BvhNode<R>* __restrict__ nodes = sc.bvh;
+    constexpr bool kWide = sizeof(R) == 8;   // f64 ray on the f32 tree: widened intervals
+    const float ix = inv_((float)d.x), iy = inv_((float)d.y), iz = inv_((float)d.z);
+    const float oix = (float)o.x * ix, oiy = (float)o.y * iy, oiz = (float)o.z * iz;
+    // fmaxf drops a NaN (0 x inf: that slab is unbounded anyway); an infinite
+    // o ix (a zero direction component) keeps every box: correct, only slow
+    const float slack = kWide ? 0x1p-20f * fmaxf(fmaxf(fabsf(oix), fabsf(oiy)), fmaxf(fabsf(oiz), 0.0f)) : 0.0f;
+    float tbw = kWide ? cull_bound(T.bound()) : 0.0f;   // kWide: tb as the culling bound, per leaf phase
+    const BvhNode<float>* __restrict__ nodes = cull_nodes(sc);
+    // b ix - o ix: fused in the f64 build too (built without contraction)
+    auto slab = [](float b, float i, float oi) {
+        if constexpr (kWide) return __builtin_fmaf(b, i, -oi);
+        else return b * i - oi;
+    };
     int32_t sp = 0;
     int32_t node = skip ? kDone : 0;   // inner node index, leaf code (< 0) or kDone
     int32_t leaf = 0;   // parked leaf code, 0 = none
@@ -552,16 +580,20 @@ __device__ __forceinline__ void bvh_traverse_ww(const DevScene<R>& sc, int32_t b
             if (inner) {
                 RTW_PROBE_LANES(1);
                 ++nvis;
-                const BvhNode<R>& nd = nodes[node];
-                const R tb = T.bound();
-                R tn[2], tf[2];
+                const BvhNode<float>& nd = nodes[node];
+                const float tb = kWide ? tbw : (float)T.bound();
+                float tn[2], tf[2];
 #pragma unroll
                 for (int c = 0; c < 2; ++c) {
-                    const R x0 = nd.lo_x[c] * ix - oix, x1 = nd.hi_x[c] * ix - oix;
-                    const R y0 = nd.lo_y[c] * iy - oiy, y1 = nd.hi_y[c] * iy - oiy;
-                    const R z0 = nd.lo_z[c] * iz - oiz, z1 = nd.hi_z[c] * iz - oiz;
-                    tn[c] = fmax(fmax(fmin(x0, x1), fmin(y0, y1)), fmax(fmin(z0, z1), (R)0));
-                    tf[c] = fmin(fmin(fmax(x0, x1), fmax(y0, y1)), fmin(fmax(z0, z1), tb));
+                    const float x0 = slab(nd.lo_x[c], ix, oix), x1 = slab(nd.hi_x[c], ix, oix);
+                    const float y0 = slab(nd.lo_y[c], iy, oiy), y1 = slab(nd.hi_y[c], iy, oiy);
+                    const float z0 = slab(nd.lo_z[c], iz, oiz), z1 = slab(nd.hi_z[c], iz, oiz);
+                    tn[c] = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), 0.0f));
+                    tf[c] = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), tb));
+                    if constexpr (kWide) {
+                        tn[c] = __builtin_fmaf(tn[c], 1.0f - 0x1p-20f, -slack);
+                        tf[c] = __builtin_fmaf(tf[c], 1.0f + 0x1p-20f, slack);
+                    }
                 }
                 const bool h0 = tn[0] <= tf[0], h1 = tn[1] <= tf[1];
                 const int32_t c0 = nd.child[0], c1 = nd.child[1];
@@ -582,6 +614,7 @@ __device__ __forceinline__ void bvh_traverse_ww(const DevScene<R>& sc, int32_t b
             RTW_PROBE_LANES(2);
             test_leaf(sc, base, leaf, T, ntest);
             leaf = 0;
+            if constexpr (kWide) tbw = cull_bound(T.bound());
         }
     }
 }
@@ -1159,15 +1192,21 @@ enum : int { kOptRobust = 1, kOptLightBvh = 2, kOptTex = 4, kOptPrims = 8, kOptH
 #endif
 
 template <typename R, int kWorld, int kOpt>
-// f32: ask for 5 waves per SIMD (<= 96 VGPRs; the kernel fits without
-// spilling); f64 keeps the compiler's choice.
+// f32: ask for 5 waves per SIMD (<= 96 VGPRs), 4 for the hit64 kernels.
 #ifndef RTW_WAVES
 #define RTW_WAVES 5
 #endif
 #ifndef RTW_WAVES_H64
 #define RTW_WAVES_H64 4
 #endif
-__global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ? RTW_WAVES_H64 : RTW_WAVES) : 1)
+// f64 sphere + plane kernels (no quads / cuboids / textures): 4 waves per SIMD
+// (128 VGPRs, ~50 spilled: C2 184 -> 174 ms vs 153 VGPRs at 3 waves); the
+// other f64 kernels keep the compiler's choice.
+#ifndef RTW_WAVES_F64
+#define RTW_WAVES_F64 4
+#endif
+__global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ? RTW_WAVES_H64 : RTW_WAVES)
+                                                         : ((kOpt & (kOptPrims | kOptTex)) ? 1 : RTW_WAVES_F64))
     render_kernel(const KParams<R> p) {
     using PR = P<R>;
     constexpr bool kRobust = (kOpt & kOptRobust) != 0;
@@ -1197,12 +1236,13 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
     DevScene<R> scw = p.sc;
     if constexpr (kWorld == kWorldBvhLds) {
         unsigned char* base = smem + (size_t)kWavesPerBlock * p.stack * 64 * sizeof(int32_t);
-        BvhNode<R>* l_nodes = reinterpret_cast<BvhNode<R>*>(base);
+        // the f32 tree (bvh32) in both precisions: the while-while traversal culls on it
+        BvhNode<float>* l_nodes = reinterpret_cast<BvhNode<float>*>(base);
         R4<R>* l_bsph = reinterpret_cast<R4<R>*>(l_nodes + p.sc.n_nodes);
         uint32_t* l_bid = reinterpret_cast<uint32_t*>(l_bsph + p.sc.n_sph);
-        static_assert(sizeof(BvhNode<R>) % 16 == 0, "nodes are copied in 16-B units");
-        const uint4* g_nodes = reinterpret_cast<const uint4*>(p.sc.bvh);
-        constexpr uint32_t kNode16 = sizeof(BvhNode<R>) / 16;
+        static_assert(sizeof(BvhNode<float>) % 16 == 0, "nodes are copied in 16-B units");
+        const uint4* g_nodes = reinterpret_cast<const uint4*>(cull_nodes(p.sc));
+        constexpr uint32_t kNode16 = sizeof(BvhNode<float>) / 16;
         for (uint32_t k = threadIdx.x; k < p.sc.n_nodes * kNode16; k += kBlock)
             reinterpret_cast<uint4*>(l_nodes)[k] = g_nodes[k];
         for (uint32_t k = threadIdx.x; k < p.sc.n_sph; k += kBlock) {
@@ -1225,7 +1265,8 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
             }
         }
         __syncthreads();
-        scw.bvh = l_nodes;
+        if constexpr (sizeof(R) == 4) scw.bvh = l_nodes;
+        else scw.bvh32 = l_nodes;
         scw.bsph = l_bsph;
         scw.bid = l_bid;
     }

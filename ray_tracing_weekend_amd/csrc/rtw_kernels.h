@@ -44,6 +44,7 @@ struct alignas(4 * sizeof(R)) R4 {
 //   bvh      : n_nodes x BvhNode<R>            -- RTW_ACCEL_BVH
 //   bsph     : n_sph   x R4 {cx, cy, cz, r*r} in BVH leaf order
 //   bid      : n_sph   x u32 original sphere index of bsph[k]
+//   bvh32    : n_nodes x BvhNode<float>        -- R = double: the same tree in f32 (while-while culling)
 //   bvh4     : 8 x n_nodes4 x Bvh4Node<R>      -- RTW_ACCEL_BVH, 4-wide
 //   lbvh     : n_lnodes x BvhNode<R>           -- light pdf query (BVH kernels)
 //   lsph/lid : n_li x R4 {c, r} / u32 in light-BVH leaf order
@@ -74,8 +75,18 @@ struct alignas(sizeof(R) == 4 ? 128 : 256) Bvh4Node {
     R4<R> b[4];
 };
 
+// f64 scenes also carry the binary tree in f32 (boxes rounded outward): the
+// while-while traversal culls on f32 nodes in both precisions (R = float:
+// `bvh` itself; the empty base keeps the f32 layout unchanged).
 template <typename R>
-struct DevScene {
+struct DevSceneCull {};
+template <>
+struct DevSceneCull<double> {
+    const BvhNode<float>* bvh32;
+};
+
+template <typename R>
+struct DevScene : DevSceneCull<R> {
     const R4<R>* sph;
     const R* sph_r;
     const uint32_t* sph_mat;
