@@ -262,17 +262,53 @@ __device__ __forceinline__ void sweep_spheres_excl(const R4<float>* __restrict__
 
 // Sum of Sphere::pdf_value over the light list in list order
 // (HittableList::pdf_value, hittable_list.rs:408-412; sphere.rs:101-111).
-// f64: the reference's arithmetic, light by light.
+// f64: the reference's arithmetic, light by light, for every light an f32
+// pre-pass cannot rule out.  A light the ray misses adds exactly +0.0 (the sum
+// starts at +0.0), so skipping it changes no bit.  The pre-pass rounds the ray
+// and the light to f32 and tests the closest approach l (see light_hit_f32)
+// against r + E and the direction (hb <= 0 or the origin inside) with slack,
+// E = 2^-18 (|o|_1 + |c|_1 + r): far above the f32 error of l (a few 2^-24
+// (|o| + |c|)) and of the f64 decision itself (disc's rounding), so every
+// light the f64 test hits stays in.
 template <bool kRobust = false>
 __device__ __forceinline__ double lights_pdf_sum(const R4<double>* __restrict__ li, uint32_t n,
                                                  V3<double> o, V3<double> d) {
+    const float ox = (float)o.x, oy = (float)o.y, oz = (float)o.z;
+    const float dx = (float)d.x, dy = (float)d.y, dz = (float)d.z;
+    const float a = __builtin_fmaf(dx, dx, __builtin_fmaf(dy, dy, dz * dz));
+    const float ia = __builtin_amdgcn_rcpf(a);
+    const float on = fabsf(ox) + fabsf(oy) + fabsf(oz);
+    const float dn = fabsf(dx) + fabsf(dy) + fabsf(dz);
     double acc = 0.0;
-    for (uint32_t k = 0; k < n; ++k) {
-        const R4<double> L = li[k];
-        acc = acc + sphere_pdf_value(mk(L.x, L.y, L.z), L.w, o, d);
+    for (uint32_t base = 0; base < n; base += 32) {
+        const uint32_t m = min(32u, n - base);
+        uint32_t mask = 0;
+        for (uint32_t k = 0; k < m; ++k) {
+            const R4<double> L = li[base + k];
+            const float cx = (float)L.x, cy = (float)L.y, cz = (float)L.z, r = fabsf((float)L.w);
+            const float fx = ox - cx, fy = oy - cy, fz = oz - cz;
+            const float hb = __builtin_fmaf(dz, fz, __builtin_fmaf(dy, fy, dx * fx));
+            const float tc = -hb * ia;
+            const float lx = __builtin_fmaf(tc, dx, fx), ly = __builtin_fmaf(tc, dy, fy),
+                        lz = __builtin_fmaf(tc, dz, fz);
+            const float l2 = __builtin_fmaf(lx, lx, __builtin_fmaf(ly, ly, lz * lz));
+            const float f2 = __builtin_fmaf(fx, fx, __builtin_fmaf(fy, fy, fz * fz));
+            const float e = 0x1p-18f * (on + fabsf(cx) + fabsf(cy) + fabsf(cz) + r);
+            const float rr = (r + e) * (r + e);
+            // NaN anywhere (a NaN ray): no candidate; the f64 test gives 0 too
+            const bool cand = (l2 <= rr) & ((hb <= 2.0f * e * dn) | (f2 <= rr));
+            mask |= (cand ? 1u : 0u) << k;
+        }
+        while (mask) {
+            const uint32_t k = (uint32_t)__builtin_ctz(mask);
+            mask &= mask - 1u;
+            const R4<double> L = li[base + k];
+            acc = acc + sphere_pdf_value(mk(L.x, L.y, L.z), L.w, o, d);
+        }
     }
     return acc;
 }
+
 // f32 light test: does the ray hit the light sphere with t in [0, inf)?  The
 // closest-approach offset l (see sphere_u) gives disc > 0 <=> l.l < r^2
 // without cancellation; the far root is >= 0 exactly when tc >= 0 or the
