@@ -233,13 +233,23 @@ def mode_line(scene, cam, precision, tuning, steps, dev):
     flops = exe_flops_of(st, n_pl, n_li)
     peak = PEAK_FP32_TFLOPS if prec == rtw.RTW_F32 else PEAK_FP64_TFLOPS
     rate = flops / (avg_ms * 1e-3) / 1e12
-    return {"value": round(W * H * SPP * steps / elapsed / 1e6, 3), "unit": "Msamples/s",
+    line = {"value": round(W * H * SPP * steps / elapsed / 1e6, 3), "unit": "Msamples/s",
             "ms_per_step": round(elapsed / steps * 1e3, 3), "steps": steps, "dtype": precision,
             "tuning": tuning, "kernel": f"render_kernel<{precision}, {KERNEL_NAMES.get(int(st.kernel), st.kernel)}>",
             "kernel_ms_avg": round(avg_ms, 3),
             "roofline": {"bound": "valu", "achieved": round(rate, 3), "peak": peak, "unit": "TFLOP/s",
                          "frac": round(rate / peak, 4), "flops_per_launch": int(flops)},
             "segments_per_sample": round(st.segments / max(st.samples, 1), 4)}
+    if precision == "f64":
+        # the f64 kernel's committed PMC pass (one kernel per world: no other
+        # f64 variant of this workload shares the name prefix)
+        traffic = pmc_traffic(f"book1_simple_{W}x{H}_{SPP}spp_depth{DEPTH}", "f64", int(st.kernel))
+        if traffic:
+            line["roofline"]["traffic"] = traffic["bytes_per_launch"]
+            for k in ("valu_issue_frac", "lanes_active_frac", "wave_wait_frac", "pmc_source"):
+                if k in traffic:
+                    line["roofline"][k] = traffic[k]
+    return line
 
 
 def run_steps(step, steps, warmup, dist, sync, device=None):
