@@ -536,11 +536,46 @@ __device__ __forceinline__ void bvh_traverse(const DevScene<R>& sc, int32_t base
 // so a short group re-tests its last sphere -- a no-op: same t, same id, and
 // ties only move to a LOWER id) and tested without a data-dependent trip
 // count.  With the default 4-sphere leaves there is exactly one group.
+// f64 leaves: an f32 pre-pass (sphere_may_hit: the light pre-pass of
+// lights_pdf_sum on {c, r^2}, with (r + e)^2 <= r^2 + e (r^2 + 1) + e^2) masks
+// the spheres the ray may hit; only those get the f64 test, each re-read from
+// the (LDS) leaf array -- the closest (t, id) does not depend on the order or
+// on spheres the ray misses.  Holding the four f64 spheres across the mask
+// loop instead spilled 78 VGPRs and ran slower.
+__device__ __forceinline__ bool sphere_may_hit(const R4<double>& S, float ox, float oy, float oz, float dx,
+                                               float dy, float dz, float ia, float on, float dn) {
+    const float cx = (float)S.x, cy = (float)S.y, cz = (float)S.z, r2 = (float)S.w;
+    const float fx = ox - cx, fy = oy - cy, fz = oz - cz;
+    const float hb = __builtin_fmaf(dz, fz, __builtin_fmaf(dy, fy, dx * fx));
+    const float tc = -hb * ia;
+    const float lx = __builtin_fmaf(tc, dx, fx), ly = __builtin_fmaf(tc, dy, fy), lz = __builtin_fmaf(tc, dz, fz);
+    const float l2 = __builtin_fmaf(lx, lx, __builtin_fmaf(ly, ly, lz * lz));
+    const float f2 = __builtin_fmaf(fx, fx, __builtin_fmaf(fy, fy, fz * fz));
+    const float e = 0x1p-18f * (on + fabsf(cx) + fabsf(cy) + fabsf(cz) + 0.5f * (r2 + 1.0f));
+    const float rr = __builtin_fmaf(e, r2 + 1.0f + e, r2);
+    return (l2 <= rr) & ((hb <= 2.0f * e * dn) | (f2 <= rr));
+}
 template <typename R, typename TT>
 __device__ __forceinline__ void test_leaf(const DevScene<R>& sc, int32_t base, int32_t leaf,
                                           TT& T, uint32_t& ntest) {
     const uint32_t code = (uint32_t)~leaf;
     const uint32_t first = code >> 4, cnt = code & 15u;
+    if constexpr (sizeof(R) == 8) {
+        const float ox = (float)T.o.x, oy = (float)T.o.y, oz = (float)T.o.z;
+        const float dx = (float)T.d.x, dy = (float)T.d.y, dz = (float)T.d.z;
+        const float ia = __builtin_amdgcn_rcpf(__builtin_fmaf(dx, dx, __builtin_fmaf(dy, dy, dz * dz)));
+        const float on = fabsf(ox) + fabsf(oy) + fabsf(oz), dn = fabsf(dx) + fabsf(dy) + fabsf(dz);
+        uint32_t mask = 0;
+        for (uint32_t k = 0; k < cnt; ++k)
+            mask |= (sphere_may_hit(sc.bsph[first + k], ox, oy, oz, dx, dy, dz, ia, on, dn) ? 1u : 0u) << k;
+        while (mask) {
+            const uint32_t k = (uint32_t)__builtin_ctz(mask);
+            mask &= mask - 1u;
+            T.test(sc.bsph[first + k], base + (int32_t)sc.bid[first + k]);
+        }
+        ntest += cnt;
+        return;
+    }
     for (uint32_t g0 = 0; g0 < cnt; g0 += 4) {
         R4<R> s[4];
         int32_t id[4];
