@@ -127,6 +127,35 @@ __device__ __forceinline__ bool aabb_hit_ref(const R* lo, const R* hi, V3<R> o, 
     return P<R>::max_(rs, tmin) <= P<R>::min_((R)INFINITY, tmax);
 }
 
+// aabb_hit_ref on a plane's box (Plane::get_aabbox, plane.rs:218-242: every
+// axis pinned at [0, 0] or [-inf, inf]) for a finite ray: an infinite axis
+// always yields (-inf, +inf) after the sign swap, which no later max_ / min_
+// or comparison changes, so the test reduces to the one pinned axis, q = (0 -
+// o_a) / d_a, and hits iff !(q < rs) -- the same IEEE quotient and the same
+// outcome (NaN included) as the six-division reference sequence.  Anything
+// else (a non-finite ray, other boxes) takes aabb_hit_ref itself.
+template <typename R>
+__device__ __forceinline__ bool aabb_hit_plane(const R* lo, const R* hi, V3<R> o, V3<R> d, R rs) {
+    const bool fin = __builtin_isfinite(o.x) && __builtin_isfinite(o.y) && __builtin_isfinite(o.z) &&
+                     __builtin_isfinite(d.x) && __builtin_isfinite(d.y) && __builtin_isfinite(d.z);
+    int npin = 0, pin = 0;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        if (lo[a] == (R)0 && hi[a] == (R)0 && !__builtin_signbit(lo[a])) {
+            ++npin;
+            pin = a;
+        } else if (!(lo[a] == (R)-INFINITY && hi[a] == (R)INFINITY)) {
+            npin = 4;
+        }
+    }
+    if (!fin || npin > 1) return aabb_hit_ref(lo, hi, o, d, rs);
+    if (npin == 0) return true;
+    const R oa = pin == 0 ? o.x : (pin == 1 ? o.y : o.z);
+    const R da = pin == 0 ? d.x : (pin == 1 ? d.y : d.z);
+    const R q = P<R>::div_(lo[pin] - oa, da);
+    return !(q < rs);
+}
+
 // Transformed<Cuboid>::hit (entities/transformations.rs:14-29, cuboid.rs:50-58)
 // on the staged record B (rtw_kernels.h kBoxR), as the oracle's box_hit: the
 // ray into object space through the inverse (the direction ALSO gets the
@@ -1515,7 +1544,9 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
             for (int32_t k = 0; k < nplanes; ++k) {
                 R t;
                 const R* pl = p.sc.planes + kPlaneR * k;
-                if (aabb_hit_ref(pl + 6, pl + 9, o, d, tmin) && plane_t(pl, o, d, tmin, t, p.counters + 4) &&
+                const bool box_hit = sizeof(R) == 8 ? aabb_hit_plane(pl + 6, pl + 9, o, d, tmin)
+                                                    : aabb_hit_ref(pl + 6, pl + 9, o, d, tmin);
+                if (box_hit && plane_t(pl, o, d, tmin, t, p.counters + 4) &&
                     (best < 0 || t < tb)) {
                     tb = t;
                     best = k;
