@@ -48,6 +48,11 @@ __device__ __forceinline__ V3<R> cross(V3<R> a, V3<R> b) {
 template <typename R>
 struct P;
 
+// The sin / cos kernel coefficients (P<double>::k_sin / k_cos) and rt_sin's reduction constants are fdlibm's:
+//   Copyright (C) 1993 by Sun Microsystems, Inc. All rights reserved.
+//   Developed at SunSoft, a Sun Microsystems, Inc. business.
+//   Permission to use, copy, modify, and distribute this software is freely
+//   granted, provided that this notice is preserved.
 template <>
 struct P<double> {
     static constexpr double kPi = 3.14159265358979323846;
