@@ -55,8 +55,6 @@ FLOP_PLANE = 6               # d.n (5) + compare
 FLOP_LAMBERT_BASE = 40       # mixture sample + ONB + cosine pdf, per Lambertian bounce
 FLOP_LIGHT = 17              # one light's Sphere::hit discriminant in HittablePdf::value
 ACCEL_NAMES = {1: "brute_lds", 2: "bvh"}
-KERNEL_NAMES = {0: "brute_l2", 1: "brute_lds", 2: "bvh2_loop", 3: "bvh2_ww", 4: "bvh4_octant",
-                5: "bvh2_ww_lds"}
 
 
 def parse():
@@ -77,26 +75,50 @@ def parse():
     return ap.parse_args()
 
 
-def pmc_traffic(workload, precision, world):
-    """HBM bytes per render-kernel launch from the committed rocprofv3 PMC
-    summary of this workload and kernel (tools/pmc_summary.py --traffic:
-    FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md "HBM"), or None."""
+def pmc_traffic(workload, kernel_name, isa_sha):
+    """HBM bytes per render-kernel launch and the PMC fractions of the newest
+    committed rocprofv3 PMC summary (tools/pmc_summary.py --traffic: FETCH_SIZE
+    x2 + WRITE_SIZE, MI355X_MICROARCH.md "HBM") of this workload whose
+    recorded ISA hash of `kernel_name` equals `isa_sha` -- the machine code
+    that ran now -- or None (then the line prints null: no profile of this
+    code exists)."""
     import glob
-    dtype = "float" if precision == "f32" else "double"
     import re
     best = None
 
     def version(f):   # profiles/r01_v11_traffic.json -> (1, 11): the newest profile wins
-        m = re.search(r"r(\d+)_v(\d+)_traffic", os.path.basename(f))
+        m = re.search(r"r(\d+)_v(\d+)\w*_traffic", os.path.basename(f))
         return (int(m.group(1)), int(m.group(2))) if m else (0, 0)
 
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json")), key=version):
         with open(f) as fh:
             d = json.load(fh)
-        if d.get("workload") == workload and "bytes_per_launch" in d and any(
-                k.startswith(f"void rtw::dev::render_kernel<{dtype}, {world},") for k in d.get("kernel", [])):
-            best = d
+        if d.get("workload") == workload and "bytes_per_launch" in d and isa_sha and \
+                d.get("isa_sha", {}).get(kernel_name) == isa_sha:
+            best = dict(d, file=os.path.relpath(f, ROOT))
     return best
+
+
+def kernel_identity(r, precision):
+    """(rocprof name, ISA hash) of the render kernel the last render of `r`
+    launched (rtw_last_kernel + the code object of the loaded librtw.so)."""
+    from ray_tracing_weekend_amd import isa
+    v = r.last_kernel()
+    if v is None:
+        return None, None
+    return isa.render_kernel_name(precision, *v), isa.kernel_isa_sha(isa.render_kernel_symbol(precision, *v))
+
+
+def attach_pmc(roof, workload, kname, sha):
+    """traffic + PMC fractions into a roofline dict, only from a profile of
+    the same machine code (else null)."""
+    t = pmc_traffic(workload, kname, sha)
+    roof["isa_sha"] = sha
+    roof["traffic"] = t["bytes_per_launch"] if t else None
+    roof["traffic_source"] = t["file"] if t else None
+    for k in ("valu_issue_frac", "lanes_active_frac", "wave_wait_frac", "scratch_write_frac"):
+        roof[k] = t.get(k) if t else None
+    return roof
 
 
 def host_cpus():
@@ -208,9 +230,10 @@ def exe_flops_of(st, n_pl, n_li):
         st.segments * FLOP_PLANE * n_pl + st.lambertian * (FLOP_LIGHT * n_li + FLOP_LAMBERT_BASE)
 
 
-def mode_line(scene, cam, precision, tuning, steps, dev):
+def mode_line(scene, cam, precision, tuning, steps, warmup, dev):
     """A secondary single-GPU line of the same C2 workload: `steps` timed full
-    renders (device-resident output, one warm-up) in another arithmetic mode,
+    renders after `warmup` untimed ones (device-resident output; the same
+    counts as the headline) in another arithmetic mode,
     with its executed-flops roofline.  Modes: the f64 parity mode (bit-identical
     to the oracle; FP64 VALU peak) and f32 without f64 hit points (hit64 = 0:
     the plain-f32 speed mode, outside the stated f32 tolerance)."""
@@ -226,30 +249,45 @@ def mode_line(scene, cam, precision, tuning, steps, dev):
 
         def step(seed):
             r.render_device(cam, seed, buf.data_ptr(), buf.numel() * buf.element_size(), stream=stream)
-        elapsed = run_steps(step, steps, 1, None, lambda: torch.cuda.synchronize(dev))
+        elapsed = run_steps(step, steps, warmup, None, lambda: torch.cuda.synchronize(dev))
         render_ms, _ = r.get_timings(steps)
         st = r.get_stats()
+        kname, sha = kernel_identity(r, precision)
     avg_ms = float(np.mean(render_ms))
     flops = exe_flops_of(st, n_pl, n_li)
     peak = PEAK_FP32_TFLOPS if prec == rtw.RTW_F32 else PEAK_FP64_TFLOPS
     rate = flops / (avg_ms * 1e-3) / 1e12
     line = {"value": round(W * H * SPP * steps / elapsed / 1e6, 3), "unit": "Msamples/s",
-            "ms_per_step": round(elapsed / steps * 1e3, 3), "steps": steps, "dtype": precision,
-            "tuning": tuning, "kernel": f"render_kernel<{precision}, {KERNEL_NAMES.get(int(st.kernel), st.kernel)}>",
+            "ms_per_step": round(elapsed / steps * 1e3, 3), "steps": steps, "warmup": warmup, "dtype": precision,
+            "tuning": tuning, "kernel": kname,
             "kernel_ms_avg": round(avg_ms, 3),
             "roofline": {"bound": "valu", "achieved": round(rate, 3), "peak": peak, "unit": "TFLOP/s",
                          "frac": round(rate / peak, 4), "flops_per_launch": int(flops)},
             "segments_per_sample": round(st.segments / max(st.samples, 1), 4)}
-    if precision == "f64":
-        # the f64 kernel's committed PMC pass (one kernel per world: no other
-        # f64 variant of this workload shares the name prefix)
-        traffic = pmc_traffic(f"book1_simple_{W}x{H}_{SPP}spp_depth{DEPTH}", "f64", int(st.kernel))
-        if traffic:
-            line["roofline"]["traffic"] = traffic["bytes_per_launch"]
-            for k in ("valu_issue_frac", "lanes_active_frac", "wave_wait_frac", "pmc_source"):
-                if k in traffic:
-                    line["roofline"][k] = traffic[k]
+    attach_pmc(line["roofline"], f"book1_simple_{W}x{H}_{SPP}spp_depth{DEPTH}", kname, sha)
     return line
+
+
+def cold_render(scene, cam, prec, dev):
+    """One render of the headline workload by a fresh context, timed alone
+    (host clock, device synced on both sides): what a one-shot
+    Camera::render pays on top of the steady state -- the 2-spp pilot render
+    that orders the tasks, the task table, the work buffers.  The scene
+    upload is excluded, as in the metric."""
+    tdtype = torch.float32 if prec == rtw.RTW_F32 else torch.float64
+    with rtw.Renderer(device=dev.index, precision=prec) as r:
+        r.set_scene(scene)
+        buf = torch.empty((rtw.tiles_for_rank(W, H, 0, 1) * 64 * 3,), dtype=tdtype, device=dev)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        r.render_device(cam, 7, buf.data_ptr(), buf.numel() * buf.element_size(),
+                        stream=torch.cuda.current_stream(dev).cuda_stream)
+        torch.cuda.synchronize(dev)
+        dt = time.perf_counter() - t0
+        render_ms, _ = r.get_timings(1)
+    return {"ms": round(dt * 1e3, 3), "value": round(W * H * SPP / dt / 1e6, 3), "unit": "Msamples/s",
+            "render_kernel_ms": round(float(render_ms[0]), 3) if render_ms else None,
+            "includes": "pilot render (2 spp) + task table + work-buffer allocation + render + fold"}
 
 
 def run_steps(step, steps, warmup, dist, sync, device=None):
@@ -360,7 +398,7 @@ def main():
     alg_rate = alg_flops / (avg_ms * 1e-3) / 1e12
     exe_rate = exe_flops / (avg_ms * 1e-3) / 1e12
     peak = PEAK_FP32_TFLOPS if prec == rtw.RTW_F32 else PEAK_FP64_TFLOPS
-    traffic = pmc_traffic(f"book1_simple_{W}x{H}_{SPP}spp_depth{DEPTH}", a.precision, int(st.kernel))
+    kname, sha = kernel_identity(r, a.precision)
     out = {
         "metric": "Msamples/s (pixels x spp) on Book-1 final scene",
         "value": round(value, 3),
@@ -384,9 +422,7 @@ def main():
                    "hit64=0" not in a.tuning else a.precision},
         "roofline": {"bound": "valu", "achieved": round(exe_rate, 3), "peak": peak,
                      "unit": "TFLOP/s", "frac": round(exe_rate / peak, 4),
-                     "traffic": traffic["bytes_per_launch"] if traffic else None,
-                     "traffic_source": traffic["source"] if traffic else None,
-                     "kernel": f"render_kernel<{a.precision}, {KERNEL_NAMES.get(int(st.kernel), st.kernel)}>",
+                     "kernel": kname,
                      "kernel_ms_avg": round(avg_ms, 3),
                      "flops_per_launch": int(exe_flops),
                      "flops_basis": "executed: node visits x width x 20 + sphere tests x 17 + segments x planes x 6 "
@@ -401,15 +437,13 @@ def main():
                      "sphere_tests_per_segment": round(st.sphere_tests / max(st.segments, 1), 3),
                      "lambertian_per_sample": round(st.lambertian / max(st.samples, 1), 4)},
     }
-    if traffic:
-        for k in ("valu_issue_frac", "lanes_active_frac", "wave_wait_frac", "pmc_source"):
-            if k in traffic:
-                out["roofline"][k] = traffic[k]
+    attach_pmc(out["roofline"], out["config"]["workload"], kname, sha)
     if world_size == 1 and not a.no_modes:
         # the same workload in the other arithmetic modes (single GPU, after the timed region)
-        out["modes"] = {"f64_parity": mode_line(scene, cam, "f64", {}, 2, dev)}
+        out["modes"] = {"f64_parity": mode_line(scene, cam, "f64", {}, a.steps, a.warmup, dev)}
         if a.precision == "f32":
-            out["modes"]["f32_plain"] = mode_line(scene, cam, "f32", {"hit64": 0}, 3, dev)
+            out["modes"]["f32_plain"] = mode_line(scene, cam, "f32", {"hit64": 0}, a.steps, a.warmup, dev)
+        out["cold_render"] = cold_render(scene, cam, prec, dev)
     if world_size == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(scene, a.cpu_seconds)
     print(json.dumps(out), flush=True)

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define RTW_ABI_VERSION 6
+#define RTW_ABI_VERSION 7
 
 /* error codes */
 #define RTW_OK 0
@@ -265,6 +265,13 @@ int rtw_get_stats(rtw_ctx *ctx, rtw_stats *stats);
  * render_ms = the render kernel alone, total_ms = render + chunk reduction.
  * Waits for them; returns how many were written. */
 int rtw_get_timings(rtw_ctx *ctx, float *render_ms, float *total_ms, int max);
+/* The render-kernel variant of the last render: (kernel << 8) | options, with
+ * kernel as rtw_stats.kernel and options the compile-time option bits of the
+ * launched instantiation (1 closest-approach f32 tests, 2 light BVH / grid,
+ * 4 textures, 8 quads / cuboids / mixed light lists, 16 f64 hit points);
+ * 0 when no render kernel has run.  Measurement tooling uses it to name the
+ * exact machine code that ran (render_kernel<R, kernel, options>). */
+int rtw_last_kernel(const rtw_ctx *ctx);
 
 /* ---- scenes::simple (scenes/src/lib.rs:155-233) ----------------------- */
 /* The library owns the arrays; view them through rtw_world_scene(). grid_n =

@@ -489,6 +489,7 @@ class Renderer:
         if not self.ctx:
             raise RenderError(_capi.RTW_E_DEVICE, f"rtw_create(device={device}) failed: no gfx950 "
                               "device visible (this library has no CPU path)")
+        self.device = device
         self.precision = precision
         self.stats = _capi.rtw_stats()
 
@@ -538,7 +539,7 @@ class Renderer:
         torch's current stream, so that the render is ordered after the torch
         work that prepared `out_ptr` and before the work that reads it."""
         if stream is None:
-            stream = _torch_stream()
+            stream = _torch_stream(self.device)
         self._check(_lib.rtw_render_device(self.ctx, C.byref(cam.raw), C.c_uint64(seed), rank,
                                            nranks, C.c_void_p(out_ptr) if out_ptr else None, out_bytes,
                                            C.c_void_p(stream) if stream else None),
@@ -549,7 +550,7 @@ class Renderer:
         """The ranks' gathered packed tiles -> the image [H, W, 3] on the device
         (rtw_assemble_tiles), on torch's current stream by default."""
         if stream is None:
-            stream = _torch_stream()
+            stream = _torch_stream(self.device)
         self._check(_lib.rtw_assemble_tiles(self.ctx, C.c_void_p(ranks_ptr), rank_stride_bytes, nranks,
                                             width, height, C.c_void_p(image_ptr),
                                             C.c_void_p(stream) if stream else None),
@@ -562,6 +563,14 @@ class Renderer:
         if got < 0:
             self._check(got, "rtw_get_timings")
         return list(a[:got]), list(b[:got])
+
+    def last_kernel(self):
+        """(kernel, options) of the render kernel the last render launched
+        (rtw_last_kernel), or None before any: render_kernel<R, kernel, options>."""
+        v = _lib.rtw_last_kernel(self.ctx)
+        if v < 0:
+            self._check(v, "rtw_last_kernel")
+        return None if v == 0 else (v >> 8, v & 0xff)
 
     def get_stats(self) -> "_capi.rtw_stats":
         self._check(_lib.rtw_get_stats(self.ctx, C.byref(self.stats)), "rtw_get_stats")
@@ -577,12 +586,14 @@ def tile_size() -> int:
     return int(_lib.rtw_tile_size())
 
 
-def _torch_stream() -> int:
-    """hipStream_t of torch's current stream (0 when torch has no GPU)."""
+def _torch_stream(device: int) -> int:
+    """hipStream_t of torch's current stream on `device` (the Renderer's
+    device, whatever torch's current device is); 0 -- the context's own
+    stream -- when torch has no GPU."""
     try:
         import torch
         if torch.cuda.is_available():
-            return int(torch.cuda.current_stream().cuda_stream)
+            return int(torch.cuda.current_stream(device).cuda_stream)
     except ImportError:
         pass
     return 0

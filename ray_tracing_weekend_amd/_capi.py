@@ -67,7 +67,7 @@ class rtw_scene(C.Structure):
     ]
 
 
-ABI_VERSION = 6     # RTW_ABI_VERSION of include/rtw.h
+ABI_VERSION = 7     # RTW_ABI_VERSION of include/rtw.h
 
 
 class rtw_stats(C.Structure):
@@ -103,6 +103,7 @@ PROTOTYPES = [
                                      C.c_uint32, C.c_void_p, C.c_void_p]),
     ("rtw_get_stats", C.c_int, [C.c_void_p, C.POINTER(rtw_stats)]),
     ("rtw_get_timings", C.c_int, [C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_float), C.c_int]),
+    ("rtw_last_kernel", C.c_int, [C.c_void_p]),
     ("rtw_scene_simple", C.c_void_p, [C.c_uint64, C.c_int]),
     ("rtw_world_scene", C.POINTER(rtw_scene), [C.c_void_p]),
     ("rtw_world_camera_builder", None, [C.c_void_p, C.POINTER(rtw_camera_builder)]),

@@ -65,6 +65,7 @@ struct rtw_ctx {
     void* d_scene = nullptr;
     size_t scene_bytes = 0;           // allocation
     size_t scene_used = 0;            // the current scene's bytes
+    size_t tree_bytes = 0;            // ... of them the BVH nodes + leaf spheres + ids
     rtw::DevScene<float> sc32{};
     rtw::DevScene<double> sc64{};
     bool has_scene = false;
@@ -95,6 +96,7 @@ struct rtw_ctx {
     uint64_t lpt_tab_target = 0;
     std::vector<uint32_t> h_lpt_tasks;
     rtw_stats last{};
+    int last_variant = 0;             // render kernel of the last render: launch_render_impl's code
     uint32_t last_n_sph = 0;
     std::string err;
 };
@@ -103,6 +105,7 @@ namespace {
 
 constexpr size_t kLdsLimit = 160 * 1024;
 constexpr uint64_t kAutoTasks = 1u << 17;   // auto task size: about this many tasks per render
+constexpr uint32_t kTaskMaxChunks = 4095;    // task-table entry {first chunk | chunks << 20}: 12 bits
 
 int fail(rtw_ctx* c, int code, const std::string& msg) {
     if (c) c->err = msg;
@@ -262,9 +265,11 @@ std::vector<unsigned char> stage_scene(const rtw_scene* s, rtw::DevScene<R>* ds,
         return o;
     };
     const size_t o_sph = reserve(sizeof(R4) * s->n_spheres);
-    const size_t o_s64 = reserve(sizeof(double) * 4 * s->n_spheres);
-    const size_t o_pl64 = reserve(sizeof(double) * 8 * s->n_planes);
-    const size_t o_m64 = reserve(sizeof(double) * 4 * s->n_materials);
+    // the f64 copies read by the f32 kernels' kOptHit64 parts only
+    constexpr bool k64 = std::is_same<R, float>::value;
+    const size_t o_s64 = reserve(k64 ? sizeof(double) * 4 * s->n_spheres : 0);
+    const size_t o_pl64 = reserve(k64 ? sizeof(double) * 8 * s->n_planes : 0);
+    const size_t o_m64 = reserve(k64 ? sizeof(double) * 4 * s->n_materials : 0);
     const size_t o_r = reserve(sizeof(R) * s->n_spheres);
     const size_t o_smat = reserve(sizeof(uint32_t) * s->n_spheres);
     const size_t o_sshade = reserve(sizeof(R4) * s->n_spheres);
@@ -329,7 +334,8 @@ std::vector<unsigned char> stage_scene(const rtw_scene* s, rtw::DevScene<R>* ds,
         // passes (sphere.rs:42-45): r^2 = -inf makes the discriminant -inf
         reinterpret_cast<R4*>(b + o_sph)[k] = R4{(R)p[0], (R)p[1], (R)p[2], p[3] < 0 ? (R)-INFINITY : r * r};
         reinterpret_cast<R*>(b + o_r)[k] = r;
-        for (int a = 0; a < 4; ++a) reinterpret_cast<double*>(b + o_s64)[4 * k + a] = p[a];
+        if (k64)
+            for (int a = 0; a < 4; ++a) reinterpret_cast<double*>(b + o_s64)[4 * k + a] = p[a];
         const uint32_t m = s->sphere_mat[k], t = s->mat_type[m];
         reinterpret_cast<uint32_t*>(b + o_smat)[k] = m | (t << 24);
         const double* mp = s->mat_params + 5 * m;
@@ -349,7 +355,7 @@ std::vector<unsigned char> stage_scene(const rtw_scene* s, rtw::DevScene<R>* ds,
                                fx ? 0.0 : INFINITY, fy ? 0.0 : INFINITY, fz ? 0.0 : INFINITY};
         R* dst = reinterpret_cast<R*>(b + o_pl) + rtw::kPlaneR * k;
         for (int q = 0; q < 6; ++q) dst[q] = (R)pl[q];
-        for (int q = 0; q < 3; ++q) {
+        for (int q = 0; k64 && q < 3; ++q) {
             reinterpret_cast<double*>(b + o_pl64)[8 * k + q] = pl[q];
             reinterpret_cast<double*>(b + o_pl64)[8 * k + 4 + q] = pl[3 + q];
         }
@@ -442,7 +448,8 @@ std::vector<unsigned char> stage_scene(const rtw_scene* s, rtw::DevScene<R>* ds,
         // the f64 scatter constants of kOptHit64 (dielectric_dir64): Dialectric's
         // index_of_refraction.recip() and reflectance's r0 for both faces, with the
         // reference's operations (material.rs:450-454, 464-468); Metal's fuzz
-        double* m64 = reinterpret_cast<double*>(b + o_m64) + 4 * k;
+        double m64s[4];
+        double* m64 = k64 ? reinterpret_cast<double*>(b + o_m64) + 4 * k : m64s;
         if (t == RTW_DIELECTRIC) {
             const double ior = m[4], rf = 1.0 / ior;
             const double r0f = (1.0 - rf) / (1.0 + rf), r0b = (1.0 - ior) / (1.0 + ior);
@@ -762,7 +769,7 @@ int lpt_pilot(rtw_ctx* c, const rtw::KParams<R>& p, int world, size_t launch_lds
     int lrc;
     if constexpr (std::is_same<R, float>::value) lrc = rtw::launch_render_f32(q, world, launch_lds, d_pout, stream, nullptr);
     else lrc = rtw::launch_render_f64(q, world, launch_lds, d_pout, stream, nullptr);
-    if (lrc) return fail(c, RTW_E_DEVICE, std::string("pilot launch failed: ") + hipGetErrorString(hipGetLastError()));
+    if (lrc < 0) return fail(c, RTW_E_DEVICE, std::string("pilot launch failed: ") + hipGetErrorString(hipGetLastError()));
     c->h_lpt_cost.resize(nt);
     HIP_TRY(c, hipMemcpyAsync(c->h_lpt_cost.data(), d_cost, (size_t)nt * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
     HIP_TRY(c, hipStreamSynchronize(stream));
@@ -796,7 +803,8 @@ int lpt_tasks(rtw_ctx* c, const rtw::KParams<R>& p, uint32_t fixed_group, uint64
             const double want = per_task / (double)std::max<uint32_t>(cost[k], 1);
             g = (uint32_t)std::max(1.0, std::min((double)rtw_ctx::kMaxGroup, std::floor(want + 0.5)));
         }
-        g = std::min(g, p.n_chunks);
+        // the entry holds the chunk count in 12 bits (first chunk < 2^20 in the low 20)
+        g = std::min(std::min(g, p.n_chunks), kTaskMaxChunks);
         for (uint32_t cb = 0; cb < p.n_chunks; cb += g) {
             tab.push_back(k);
             tab.push_back(cb | (std::min(g, p.n_chunks - cb) << 20));
@@ -939,7 +947,7 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
     // larger than an XCD's L2 (4 MiB) loses its locality (C5, 1M spheres,
     // ~100 MB: +8 %), so by default only worlds held in LDS or small enough
     // for L2 take it (C2: -4 %, C3 (10k spheres): -4 %).
-    const bool on_chip = world == rtw::kWorldBvhLds || world == rtw::kWorldLds || c->scene_used <= (4u << 20);
+    const bool on_chip = world == rtw::kWorldBvhLds || world == rtw::kWorldLds || c->tree_bytes <= (4u << 20);
     if ((c->lpt == 2 || (c->lpt == 1 && on_chip)) && need_out && p.spp >= std::max(c->lpt_min_spp, 1u) &&
         p.max_depth && p.n_local_tiles > 1 && p.n_chunks < (1u << 20)) {
         const bool same = c->lpt_valid && c->lpt_serial == c->scene_serial && c->lpt_rank == rank &&
@@ -987,7 +995,8 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
     } else {
         lrc = rtw::launch_render_f64(p, world, launch_lds, reinterpret_cast<double*>(d_out), stream, ev[1]);
     }
-    if (lrc) return fail(c, RTW_E_DEVICE, std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
+    if (lrc < 0) return fail(c, RTW_E_DEVICE, std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
+    c->last_variant = lrc;
     HIP_TRY(c, hipEventRecord(c->ev1, stream));
     HIP_TRY(c, hipEventRecord(ev[2], stream));
     ++c->n_renders;
@@ -1201,6 +1210,12 @@ int rtw_set_scene(rtw_ctx* c, const rtw_scene* s) {
         c->scene_bytes = blob.size();
     }
     c->scene_used = blob.size();
+    // the closest-hit working set (tree + leaf spheres + ids): what the lpt
+    // heuristic weighs against an XCD's L2
+    c->tree_bytes = c->precision == RTW_F32
+                        ? (size_t)tmp32.n_nodes * sizeof(rtw::BvhNode<float>) + (size_t)tmp32.n_sph * (sizeof(rtw::R4<float>) + 4)
+                        : (size_t)tmp64.n_nodes * (sizeof(rtw::BvhNode<double>) + sizeof(rtw::BvhNode<float>)) +
+                              (size_t)tmp64.n_sph * (sizeof(rtw::R4<double>) + 4);
     // scale of the scene for the f32 test choice (render_device_t)
     c->scene_extent = 0.0;
     c->min_radius = INFINITY;
@@ -1283,6 +1298,11 @@ int rtw_render_device(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     return c->precision == RTW_F32 ? render_device_t<float>(c, cam, seed, rank, nranks, d_out, out_bytes, s)
                                    : render_device_t<double>(c, cam, seed, rank, nranks, d_out, out_bytes, s);
+}
+
+int rtw_last_kernel(const rtw_ctx* c) {
+    if (!c) return RTW_E_INVALID;
+    return c->last_variant & 0xffff;
 }
 
 int rtw_get_stats(rtw_ctx* c, rtw_stats* out) {

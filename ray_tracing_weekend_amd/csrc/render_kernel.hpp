@@ -36,7 +36,7 @@ namespace dev {
 // build; the profiling builds of tools/exp_cost.sh (RTW_EXP) and
 // tools/trace_paths.py (RTW_TRACE) and tools/lane_profile.py (RTW_PROF)
 // define them in rtw_probes.hpp.
-#if defined(RTW_EXP) || defined(RTW_TRACE) || defined(RTW_PROF) || defined(RTW_TIMELINE)
+#if defined(RTW_EXP) || defined(RTW_TRACE) || defined(RTW_PROF) || defined(RTW_TIMELINE) || defined(RTW_ABL)
 #include "rtw_probes.hpp"
 #else
 #define RTW_PROBE_WAVE_BEGIN()
@@ -51,6 +51,10 @@ namespace dev {
 #define RTW_PROBE_LANES(id)
 #define RTW_PROBE_H64()
 #define RTW_PROBE_SCATTER64(expr)
+#define RTW_PROBE_ABL_DITHER(v)
+#define RTW_PROBE_ABL_SELF(hit, ts)
+#define RTW_PROBE_ABL_WINNER()
+#define RTW_PROBE_ABL_SCATTER(f64)
 #endif
 
 template <typename R>
@@ -922,9 +926,7 @@ __device__ __forceinline__ uint32_t mix32(uint32_t h) {
     return h;
 }
 __device__ __forceinline__ V3<double> dither64(V3<float> v) {
-#if RTW_ABL == 4
-    return V3<double>{v.x, v.y, v.z};
-#endif
+    RTW_PROBE_ABL_DITHER(v);
     const uint32_t h0 = mix32(__float_as_uint(v.x) ^ mix32(__float_as_uint(v.y) ^ mix32(__float_as_uint(v.z))));
     const uint32_t h1 = mix32(h0 + 0x9e3779b9u), h2 = mix32(h1 + 0x9e3779b9u);
     constexpr double kScale = 0x1p-25 / 4294967296.0;        // (h - 2^31) * 2^-57: |rel| < 2^-26
@@ -1287,10 +1289,6 @@ __device__ V3<R> tex_colour(const DevScene<R>& sc, uint32_t tid, R u, R v, V3<R>
 //   kOptHit64    (f32 kernels of sphere + plane scenes) f64 ray origin, own-sphere re-hit test,
 //                hit t and hit point (sphere_t_ref64): the reference's self-intersection odds
 enum : int { kOptRobust = 1, kOptLightBvh = 2, kOptTex = 4, kOptPrims = 8, kOptHit64 = 16 };
-#ifndef RTW_ABL
-#define RTW_ABL 0     // timing ablations of the kOptHit64 parts (experiment builds only)
-#endif
-
 template <typename R, int kWorld, int kOpt>
 // f32: ask for 5 waves per SIMD (<= 96 VGPRs), 4 for the hit64 kernels.
 #ifndef RTW_WAVES
@@ -1583,11 +1581,9 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                     RTW_PROBE_LANES(5);
                     ++ntest;
                     double ts;
-#if RTW_ABL == 1
-                    if (sphere_t(mk(p.sc.sph[self_s].x, p.sc.sph[self_s].y, p.sc.sph[self_s].z), p.sc.sph[self_s].w, o, d, tmin, tb) && (double)tb < tb64) { ts = tb;
-#else
-                    if (sphere_t_ref64(p.sc.sph64[self_s], o64, d64, ts) && ts < tb64) {
-#endif
+                    bool self_hit = sphere_t_ref64(p.sc.sph64[self_s], o64, d64, ts) && ts < tb64;
+                    RTW_PROBE_ABL_SELF(self_hit, ts);
+                    if (self_hit) {
                         tb64 = ts;
                         tb = (float)ts;
                         best = sbase + self_s;
@@ -1605,11 +1601,8 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                         sweep_spheres_excl<kRobust>(sph, p.sc.n_sph, sbase, o, d, tmin, tb, best, excl);
                     }
                     if (best != prev && best >= sbase) {
-#if RTW_ABL == 2
-                        tb64 = (double)tb;
-#else
                         if (!sphere_t_ref64(p.sc.sph64[best - sbase], o64, d64, tb64)) tb64 = (double)tb;
-#endif
+                        RTW_PROBE_ABL_WINNER();
                     }
                 }
                 // a plane's t in f64 too, so that its hit points lie within f64 rounding
@@ -1709,7 +1702,9 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                         next_iso = (mw >> 31) != 0;
                         // Metal / Dielectric scatter in f64 from the f64 normal: their
                         // directions decide the next re-hit at the ulp level
-                        if (RTW_ABL != 3 && (mtype == kMatMetal || mtype == kMatDielectric)) {
+                        bool scatter64 = mtype == kMatMetal || mtype == kMatDielectric;
+                        RTW_PROBE_ABL_SCATTER(scatter64);
+                        if (scatter64) {
                             n64 = sphere_normal64(pnt64, p.sc.sph64[k]);
                             outward = mk((float)n64.x, (float)n64.y, (float)n64.z);
                             sph_hit = true;
@@ -2020,9 +2015,13 @@ inline uint32_t resident_blocks(uint32_t blocks, size_t lds_bytes) {
     return std::min<uint32_t>(blocks, (uint32_t)(per_cu * cus));
 }
 
+constexpr int kVariantRan = 1 << 16;
+// Launch the render kernel of `world` with options kOpt; returns the variant
+// that ran as kVariantRan | (world << 8) | options (the brute-force worlds drop
+// the light BVH, textured scenes map to the while-while BVH).
 template <typename R, int kOpt>
-inline void launch_world(const KParams<R>& p, int world, size_t lds_bytes, uint32_t blocks,
-                         hipStream_t stream) {
+inline int launch_world(const KParams<R>& p, int world, size_t lds_bytes, uint32_t blocks,
+                        hipStream_t stream) {
     const size_t stacks = (size_t)kWavesPerBlock * p.stack * 64 * sizeof(int32_t);
     const bool resident = p.persist == kPersistResident;
     constexpr int kBrute = kOpt & ~dev::kOptLightBvh;   // the light BVH needs the BVH kernels' stack
@@ -2037,46 +2036,48 @@ inline void launch_world(const KParams<R>& p, int world, size_t lds_bytes, uint3
         if (resident) blocks = resident_blocks<R, kWorldLds, kBrute>(blocks, lds_bytes);
         hipLaunchKernelGGL((dev::render_kernel<R, kWorldLds, kBrute>), dim3(blocks), dim3(kBlock), lds_bytes,
                            stream, p);
-        break;
+        return kVariantRan | (kWorldLds << 8) | kBrute;
     case kWorldBvhLds:
         allow_lds<R, kWorldBvhLds, kOpt>(lds_bytes);
         if (resident) blocks = resident_blocks<R, kWorldBvhLds, kOpt>(blocks, lds_bytes);
         hipLaunchKernelGGL((dev::render_kernel<R, kWorldBvhLds, kOpt>), dim3(blocks), dim3(kBlock), lds_bytes,
                            stream, p);
-        break;
+        return kVariantRan | (kWorldBvhLds << 8) | kOpt;
     case kWorldBvh4:
         if constexpr ((kOpt & dev::kOptTex) == 0) {
             if (resident) blocks = resident_blocks<R, kWorldBvh4, kOpt>(blocks, stacks);
             hipLaunchKernelGGL((dev::render_kernel<R, kWorldBvh4, kOpt>), dim3(blocks), dim3(kBlock), stacks,
                                stream, p);
         }
-        break;
+        return kVariantRan | (kWorldBvh4 << 8) | kOpt;
     case kWorldBvhWW:
         if (resident) blocks = resident_blocks<R, kWorldBvhWW, kOpt>(blocks, stacks);
         hipLaunchKernelGGL((dev::render_kernel<R, kWorldBvhWW, kOpt>), dim3(blocks), dim3(kBlock), stacks,
                            stream, p);
-        break;
+        return kVariantRan | (kWorldBvhWW << 8) | kOpt;
     case kWorldBvh:
         if constexpr ((kOpt & dev::kOptTex) == 0) {
             if (resident) blocks = resident_blocks<R, kWorldBvh, kOpt>(blocks, stacks);
             hipLaunchKernelGGL((dev::render_kernel<R, kWorldBvh, kOpt>), dim3(blocks), dim3(kBlock), stacks,
                                stream, p);
         }
-        break;
+        return kVariantRan | (kWorldBvh << 8) | kOpt;
     default:
         if (resident) blocks = resident_blocks<R, kWorldGlobal, kBrute>(blocks, 0);
         hipLaunchKernelGGL((dev::render_kernel<R, kWorldGlobal, kBrute>), dim3(blocks), dim3(kBlock), 0, stream,
                            p);
-        break;
+        return kVariantRan | (kWorldGlobal << 8) | kBrute;
     }
 }
 
 // Options per launch: the f32 sphere-test form (DevScene::robust; f64 keeps
 // the reference arithmetic only) and the light BVH (KParams::light_bvh).
+// Returns the variant that ran (launch_world's code; 0: no launch), or -1.
 template <typename R>
 inline int launch_render_impl(const KParams<R>& p, int world, size_t lds_bytes, R* out,
                               hipStream_t stream, hipEvent_t mid) {
     uint32_t blocks = (p.n_tasks + kWavesPerBlock - 1) / kWavesPerBlock;
+    int ran = 0;
     if (p.persist && p.persist != kPersistResident)
         blocks = blocks < p.persist ? blocks : p.persist;   // fixed grid, tasks from the counter
     if (blocks) {
@@ -2088,32 +2089,32 @@ inline int launch_render_impl(const KParams<R>& p, int world, size_t lds_bytes, 
         constexpr int T = dev::kOptTex | dev::kOptPrims, Pr = dev::kOptPrims;
         if (p.sc.mat_tex) {
             if constexpr (sizeof(R) == 4) {
-                if (robust && lbvh) launch_world<R, T | dev::kOptRobust | dev::kOptLightBvh>(p, world, lds_bytes, blocks, stream);
-                else if (robust) launch_world<R, T | dev::kOptRobust>(p, world, lds_bytes, blocks, stream);
-                else if (lbvh) launch_world<R, T | dev::kOptLightBvh>(p, world, lds_bytes, blocks, stream);
-                else launch_world<R, T>(p, world, lds_bytes, blocks, stream);
+                if (robust && lbvh) ran = launch_world<R, T | dev::kOptRobust | dev::kOptLightBvh>(p, world, lds_bytes, blocks, stream);
+                else if (robust) ran = launch_world<R, T | dev::kOptRobust>(p, world, lds_bytes, blocks, stream);
+                else if (lbvh) ran = launch_world<R, T | dev::kOptLightBvh>(p, world, lds_bytes, blocks, stream);
+                else ran = launch_world<R, T>(p, world, lds_bytes, blocks, stream);
             } else {
-                if (lbvh) launch_world<R, T | dev::kOptLightBvh>(p, world, lds_bytes, blocks, stream);
-                else launch_world<R, T>(p, world, lds_bytes, blocks, stream);
+                if (lbvh) ran = launch_world<R, T | dev::kOptLightBvh>(p, world, lds_bytes, blocks, stream);
+                else ran = launch_world<R, T>(p, world, lds_bytes, blocks, stream);
             }
         } else if constexpr (sizeof(R) == 4) {
             if (prims) {
-                if (robust && lbvh) launch_world<R, Pr | dev::kOptRobust | dev::kOptLightBvh>(p, world, lds_bytes, blocks, stream);
-                else if (robust) launch_world<R, Pr | dev::kOptRobust>(p, world, lds_bytes, blocks, stream);
-                else if (lbvh) launch_world<R, Pr | dev::kOptLightBvh>(p, world, lds_bytes, blocks, stream);
-                else launch_world<R, Pr>(p, world, lds_bytes, blocks, stream);
+                if (robust && lbvh) ran = launch_world<R, Pr | dev::kOptRobust | dev::kOptLightBvh>(p, world, lds_bytes, blocks, stream);
+                else if (robust) ran = launch_world<R, Pr | dev::kOptRobust>(p, world, lds_bytes, blocks, stream);
+                else if (lbvh) ran = launch_world<R, Pr | dev::kOptLightBvh>(p, world, lds_bytes, blocks, stream);
+                else ran = launch_world<R, Pr>(p, world, lds_bytes, blocks, stream);
             } else {
                 constexpr int H = dev::kOptHit64;
                 if (p.hit64) {
-                    if (robust && lbvh) launch_world<R, H | dev::kOptRobust | dev::kOptLightBvh>(p, world, lds_bytes, blocks, stream);
-                    else if (robust) launch_world<R, H | dev::kOptRobust>(p, world, lds_bytes, blocks, stream);
-                    else if (lbvh) launch_world<R, H | dev::kOptLightBvh>(p, world, lds_bytes, blocks, stream);
-                    else launch_world<R, H>(p, world, lds_bytes, blocks, stream);
+                    if (robust && lbvh) ran = launch_world<R, H | dev::kOptRobust | dev::kOptLightBvh>(p, world, lds_bytes, blocks, stream);
+                    else if (robust) ran = launch_world<R, H | dev::kOptRobust>(p, world, lds_bytes, blocks, stream);
+                    else if (lbvh) ran = launch_world<R, H | dev::kOptLightBvh>(p, world, lds_bytes, blocks, stream);
+                    else ran = launch_world<R, H>(p, world, lds_bytes, blocks, stream);
                 } else {
-                    if (robust && lbvh) launch_world<R, dev::kOptRobust | dev::kOptLightBvh>(p, world, lds_bytes, blocks, stream);
-                    else if (robust) launch_world<R, dev::kOptRobust>(p, world, lds_bytes, blocks, stream);
-                    else if (lbvh) launch_world<R, dev::kOptLightBvh>(p, world, lds_bytes, blocks, stream);
-                    else launch_world<R, 0>(p, world, lds_bytes, blocks, stream);
+                    if (robust && lbvh) ran = launch_world<R, dev::kOptRobust | dev::kOptLightBvh>(p, world, lds_bytes, blocks, stream);
+                    else if (robust) ran = launch_world<R, dev::kOptRobust>(p, world, lds_bytes, blocks, stream);
+                    else if (lbvh) ran = launch_world<R, dev::kOptLightBvh>(p, world, lds_bytes, blocks, stream);
+                    else ran = launch_world<R, 0>(p, world, lds_bytes, blocks, stream);
                 }
             }
         } else {
@@ -2121,11 +2122,11 @@ inline int launch_render_impl(const KParams<R>& p, int world, size_t lds_bytes, 
             // too (156 instead of 176 VGPRs: 3 waves per SIMD instead of 2)
             (void)robust;
             if (prims) {
-                if (lbvh) launch_world<R, Pr | dev::kOptLightBvh>(p, world, lds_bytes, blocks, stream);
-                else launch_world<R, Pr>(p, world, lds_bytes, blocks, stream);
+                if (lbvh) ran = launch_world<R, Pr | dev::kOptLightBvh>(p, world, lds_bytes, blocks, stream);
+                else ran = launch_world<R, Pr>(p, world, lds_bytes, blocks, stream);
             } else {
-                if (lbvh) launch_world<R, dev::kOptLightBvh>(p, world, lds_bytes, blocks, stream);
-                else launch_world<R, 0>(p, world, lds_bytes, blocks, stream);
+                if (lbvh) ran = launch_world<R, dev::kOptLightBvh>(p, world, lds_bytes, blocks, stream);
+                else ran = launch_world<R, 0>(p, world, lds_bytes, blocks, stream);
             }
         }
         if (hipGetLastError() != hipSuccess) return -1;
@@ -2136,7 +2137,7 @@ inline int launch_render_impl(const KParams<R>& p, int world, size_t lds_bytes, 
                            out);
         if (hipGetLastError() != hipSuccess) return -1;
     }
-    return 0;
+    return ran;
 }
 
 template <typename R>

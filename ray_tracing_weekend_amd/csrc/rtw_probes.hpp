@@ -1,6 +1,12 @@
 // rtw_probes.hpp -- experiment-only hooks of the render kernel (never in the
-// product build: render_kernel.hpp includes this file only when RTW_EXP or
-// RTW_TRACE is defined; otherwise every RTW_PROBE_* hook is empty).
+// product build: render_kernel.hpp includes this file only when RTW_EXP,
+// RTW_TRACE, RTW_PROF, RTW_TIMELINE or RTW_ABL is defined; otherwise every
+// RTW_PROBE_* hook is empty).
+//
+// RTW_ABL (timing ablations of the kOptHit64 parts): 1 = the
+// own-sphere re-hit test in f32, 2 = the winner's t from the f32 traversal,
+// 3 = Metal / Dielectric scatter in f32, 4 = f32 directions carried into f64
+// without the dither.  Timing only: the images are not the product's.
 //
 // RTW_EXP (tools/exp_cost.sh): repeat one part of the per-segment work so that
 // the time difference prices it.  1 = closest-hit query, 2 = light pdf sum,
@@ -26,6 +32,36 @@
 
 #ifndef RTW_EXP
 #define RTW_EXP 0
+#endif
+#ifndef RTW_ABL
+#define RTW_ABL 0
+#endif
+
+#if RTW_ABL == 4
+#define RTW_PROBE_ABL_DITHER(v) return V3<double>{(v).x, (v).y, (v).z}
+#else
+#define RTW_PROBE_ABL_DITHER(v)
+#endif
+#if RTW_ABL == 1
+#define RTW_PROBE_ABL_SELF(hit, ts) \
+    do { \
+        R tf_; \
+        const R4<R> s_ = p.sc.sph[self_s]; \
+        hit = sphere_t(mk(s_.x, s_.y, s_.z), s_.w, o, d, tmin, tf_) && (double)tf_ < tb64; \
+        ts = (double)tf_; \
+    } while (0)
+#else
+#define RTW_PROBE_ABL_SELF(hit, ts)
+#endif
+#if RTW_ABL == 2
+#define RTW_PROBE_ABL_WINNER() (tb64 = (double)tb)
+#else
+#define RTW_PROBE_ABL_WINNER()
+#endif
+#if RTW_ABL == 3
+#define RTW_PROBE_ABL_SCATTER(f64) (f64 = false)
+#else
+#define RTW_PROBE_ABL_SCATTER(f64)
 #endif
 
 #ifdef RTW_TIMELINE

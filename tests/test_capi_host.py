@@ -33,7 +33,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert rtw._lib.rtw_abi_version() == rtw._capi.ABI_VERSION == 6
+    assert rtw._lib.rtw_abi_version() == rtw._capi.ABI_VERSION == 7
 
 
 def test_camera_builder_defaults_match_reference():
@@ -221,3 +221,18 @@ def test_renderer_without_gpu_fails_loudly():
         pytest.skip("GPU present")
     with pytest.raises(rtw.RenderError):
         rtw.Renderer()
+
+
+def test_kernel_isa_identity_covers_every_render_kernel_variant():
+    """isa.py finds the gfx950 machine code of the launched variants by name
+    (bench.py ties the committed PMC profiles to it): the headline f32 hit64
+    kernel and the f64 parity kernel have distinct, stable hashes."""
+    from ray_tracing_weekend_amd import isa
+    h32 = isa.kernel_isa_sha(isa.render_kernel_symbol("f32", 5, 16))
+    h64 = isa.kernel_isa_sha(isa.render_kernel_symbol("f64", 5, 0))
+    assert h32 and h64 and h32 != h64 and len(h32) == 16
+    assert isa.kernel_isa_sha(isa.render_kernel_symbol("f32", 5, 16)) == h32
+    name = isa.render_kernel_name("f32", 5, 16)
+    assert name == "void rtw::dev::render_kernel<float, 5, 16>(rtw::KParams<float>)"
+    assert isa.demangled_to_symbol(name) == isa.render_kernel_symbol("f32", 5, 16)
+    assert isa.kernel_isa_sha("_ZN3rtw3dev13no_such_kernelEv") is None

@@ -751,3 +751,18 @@ def test_scheduling_knobs_do_not_change_the_image(prec):
               {"lpt": 2, "lpt_min_spp": 1, "lds": 0}):
         img, _, cv = _render_gpu(soa, cam, 113, prec, tuning=t)
         assert _same(base, img) and cb == cv, t
+
+
+def test_task_table_with_4096_chunk_groups_keeps_every_chunk():
+    """A fixed group of 4096 chunks at chunk 1 with the task table on: the
+    table entry holds the chunk count in 12 bits, so the host cuts such tasks
+    at 4095 chunks (a 4096 would wrap to 0 and the kernel would skip the
+    task, leaving its chunk sums unwritten).  Same image bit for bit as the
+    plain tile-major schedule."""
+    soa, b = _scene()
+    cam = b.with_image_width(16).with_image_height(8).with_samples_per_pixel(4100).with_max_depth(6).build()
+    base, chunk, cb = _render_gpu(soa, cam, 131, rtw.RTW_F32, tuning={"lpt": 0})
+    assert chunk == 1
+    img, _, cv = _render_gpu(soa, cam, 131, rtw.RTW_F32,
+                             tuning={"group": 4096, "lpt_min_spp": 1, "chunk": 1})
+    assert _same(base, img) and cb == cv

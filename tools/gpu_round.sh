@@ -1,14 +1,17 @@
 #!/bin/bash
-# One GPU session: parity tests, smoke, bench, rocprofv3 kernel trace.
+# One GPU session: parity tests, smoke, bench, then rocprofv3 kernel-trace +
+# PMC passes of the headline (f32 hit64) and the f64 parity kernels, each
+# summarised on the box against the library that ran (ISA-hash stamped).
 # Stops at the first fault-type exit (abort/segfault/timeout); a plain test
 # failure (pytest rc 1) still lets the measurement steps run.
+#   tools/gpu_round.sh TAG          (PROFILE=0: no rocprofv3 steps)
 set -u
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$ROOT"
 OUT="$ROOT/gpurun_out"
 mkdir -p "$OUT"
-TAG="${1:-r02}"
-STEPS="${STEPS:-3}"
+TAG="${1:-r03}"
+STEPS="${STEPS:-5}"
 
 fatal() { case "$1" in 0|1) return 1;; *) return 0;; esac; }
 
@@ -20,16 +23,12 @@ timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smo
 rc=$?; echo "smoke rc=$rc"; tail -3 "$OUT/smoke_$TAG.log"
 if fatal $rc; then exit $rc; fi
 
-timeout -k 10 600 python bench.py --steps "$STEPS" --warmup 1 > "$OUT/bench_$TAG.json" 2> "$OUT/bench_$TAG.err"
-rc=$?; echo "bench rc=$rc"; cat "$OUT/bench_$TAG.json"; tail -3 "$OUT/bench_$TAG.err"
+timeout -k 10 600 python bench.py --steps "$STEPS" --warmup 2 > "$OUT/bench_$TAG.json" 2> "$OUT/bench_$TAG.err"
+rc=$?; echo "bench rc=$rc"; cut -c1-1500 "$OUT/bench_$TAG.json"; tail -3 "$OUT/bench_$TAG.err"
 if [ $rc -ne 0 ]; then exit $rc; fi
 
 if [ "${PROFILE:-1}" = "1" ]; then
-  export TMPDIR=/tmp
-  ( cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$TAG" -o run \
-      --output-format csv -- python3 "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline \
-      > "$OUT/prof_$TAG.log" 2>&1 )
-  rc=$?; echo "rocprof rc=$rc"; tail -3 "$OUT/prof_$TAG.log"
-  find "$OUT/prof_$TAG" -name "*stats*" | head
+  bash "$ROOT/tools/profile.sh" "$TAG" --steps 2 --warmup 1 --no-cpu-baseline --no-modes || exit $?
+  bash "$ROOT/tools/profile.sh" "${TAG}_f64" --precision f64 --steps 2 --warmup 1 --no-cpu-baseline --no-modes || exit $?
 fi
-exit $rc
+exit 0

@@ -53,6 +53,17 @@ if len(sys.argv) > 3 and sys.argv[2] == "--traffic":
             if "render_kernel" in row["Kernel_Name"]:
                 names.add(row["Kernel_Name"])
     d["kernel"] = sorted(names)
+    if len(names) != 1:
+        sys.exit(f"--traffic needs exactly one render-kernel variant in the passes, found {sorted(names)}: "
+                 "profile one mode per run (bench.py --no-modes [--precision f64])")
+    # the machine code these counters belong to: bench.py attaches them to a
+    # line only when the kernel that ran has the same hash (run this on the
+    # box, right after the passes, against the library they ran)
+    import os
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+    from ray_tracing_weekend_amd import isa
+    d["isa_sha"] = {n: isa.kernel_isa_sha(isa.demangled_to_symbol(n)) for n in d["kernel"]
+                    if isa.demangled_to_symbol(n)}
     if len(sys.argv) > 4:
         d["workload"] = sys.argv[4]
     json.dump(d, open(sys.argv[3], "w"), indent=1)

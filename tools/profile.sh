@@ -16,7 +16,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$TAG" -o trace 
   -- python3 "$ROOT/bench.py" $ARGS > "$OUT/prof_${TAG}_trace.log" 2>&1
 rc=$?; echo "trace rc=$rc"; if bad $rc; then exit $rc; fi
 # counter sets separated by ';' (PMC_SETS overrides the default list)
-SETS="${PMC_SETS:-FETCH_SIZE;WRITE_SIZE;SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES;SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE}"
+SETS="${PMC_SETS:-FETCH_SIZE;WRITE_SIZE;SQ_WAVES SQ_INSTS_VALU SQ_THREAD_CYCLES_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY;SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE}"
 i=0
 IFS=';' read -ra SETLIST <<< "$SETS"
 for set in "${SETLIST[@]}"; do
@@ -25,4 +25,10 @@ for set in "${SETLIST[@]}"; do
     -- python3 "$ROOT/bench.py" $ARGS > "$OUT/prof_${TAG}_pmc$i.log" 2>&1
   rc=$?; echo "pmc$i ($set) rc=$rc"; if bad $rc; then exit $rc; fi
 done
-exit 0
+# per-launch means + the traffic / fractions file bench.py reads, stamped with
+# the ISA hash of the profiled kernel in the library that ran (WORKLOAD names
+# the bench configuration)
+python3 "$ROOT/tools/pmc_summary.py" "$OUT/prof_$TAG" --traffic "$OUT/prof_${TAG}_traffic.json" \
+  "${WORKLOAD:-book1_simple_1200x800_500spp_depth50}" > "$OUT/prof_${TAG}_pmc_summary.txt"
+rc=$?; echo "summary rc=$rc"; cat "$OUT/prof_${TAG}_pmc_summary.txt"
+exit $rc
