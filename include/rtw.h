@@ -213,7 +213,7 @@ int rtw_set_accel(rtw_ctx *ctx, int accel);
  * "bvh_kind" (3 = binary while-while on the tree staged in LDS, the
  * default, 1 = binary while-while from L1/L2, 2 = 4-wide octant BVH, 0 =
  * binary single loop), "bvh_lds_max" (LDS bytes per workgroup bvh_kind 3 may
- * use; 0 = by precision: 32 KiB f32, 52 KiB f64), "bvh_ww" (legacy: 1 -> bvh_kind 1, 0 -> 0), "auto_accel" */
+ * use; 0 = by precision: 36 KiB f32, 52 KiB f64), "bvh_ww" (legacy: 1 -> bvh_kind 1, 0 -> 0), "auto_accel" */
 int rtw_set_tuning(rtw_ctx *ctx, const char *key, int64_t value);
 
 /* ---- CameraBuilder::build (camera.rs:114-218) ------------------------- */

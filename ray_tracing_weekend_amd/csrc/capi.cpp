@@ -34,8 +34,8 @@ struct rtw_ctx {
                                   // tree staged in LDS (falls back to 1 when it does not fit),
                                   // 1 = the same from L1/L2, 2 = 4-wide octant tree, 0 = binary
                                   // single loop
-    // LDS per workgroup allowed for bvh_kind 3 (0: by precision -- f32 32 KiB, five
-    // 256-thread workgroups per CU at 5 waves/SIMD; f64 52 KiB, three at 3 waves/SIMD)
+    // LDS per workgroup allowed for bvh_kind 3 (0: by precision -- f32 36 KiB, four
+    // 256-thread workgroups per CU at 4 waves/SIMD; f64 52 KiB)
     size_t bvh_lds_max = 0;
     int robust = 2;                   // f32 closest-approach tests: 1 on, 0 off, 2 by scene scale
     double scene_extent = 0.0, min_radius = 0.0;   // of the staged scene (robust = 2)
@@ -300,6 +300,8 @@ std::vector<unsigned char> stage_scene(const rtw_scene* s, rtw::DevScene<R>* ds,
     // f64: the same tree in f32 (boxes rounded outward), which the while-while
     // traversal culls on with an error slack (bvh_traverse_ww)
     const size_t o_nodes32 = reserve(std::is_same<R, double>::value ? sizeof(rtw::BvhNode<float>) * bb.nodes.size() : 0);
+    // f64: the leaf spheres {c, r^2} rounded to f32, the leaf pre-pass of the f64 kernels
+    const size_t o_bsph32 = reserve(std::is_same<R, double>::value ? sizeof(rtw::R4<float>) * s->n_spheres : 0);
     const size_t o_bsph = reserve(sizeof(R4) * s->n_spheres);
     const size_t o_bid = reserve(sizeof(uint32_t) * s->n_spheres);
     // isolated spheres (self-hit shortcut): bit 31 of sphere_mat.  The margin
@@ -541,8 +543,12 @@ std::vector<unsigned char> stage_scene(const rtw_scene* s, rtw::DevScene<R>* ds,
     }
     for (uint32_t k = 0; k < s->n_spheres; ++k) {
         const uint32_t id = bb.order[k];
-        reinterpret_cast<R4*>(b + o_bsph)[k] = reinterpret_cast<const R4*>(b + o_sph)[id];
+        const R4 sk = reinterpret_cast<const R4*>(b + o_sph)[id];
+        reinterpret_cast<R4*>(b + o_bsph)[k] = sk;
         reinterpret_cast<uint32_t*>(b + o_bid)[k] = id;
+        if constexpr (std::is_same<R, double>::value)
+            reinterpret_cast<rtw::R4<float>*>(b + o_bsph32)[k] =
+                rtw::R4<float>{(float)sk.x, (float)sk.y, (float)sk.z, (float)sk.w};
     }
     // 4-wide tree, one copy per ray octant: slots in that octant's
     // front-to-back order, slab planes pre-selected as near/far (see Bvh4Node)
@@ -613,8 +619,10 @@ std::vector<unsigned char> stage_scene(const rtw_scene* s, rtw::DevScene<R>* ds,
     ds->n_nodes4 = (uint32_t)n4;
     ds->bvh4_stack = b4.max_stack;
     ds->bvh = reinterpret_cast<const rtw::BvhNode<R>*>(base + o_nodes);
-    if constexpr (std::is_same<R, double>::value)
+    if constexpr (std::is_same<R, double>::value) {
         ds->bvh32 = reinterpret_cast<const rtw::BvhNode<float>*>(base + o_nodes32);
+        ds->bsph32 = reinterpret_cast<const rtw::R4<float>*>(base + o_bsph32);
+    }
     ds->bsph = reinterpret_cast<const R4*>(base + o_bsph);
     ds->bid = reinterpret_cast<const uint32_t*>(base + o_bid);
     ds->n_sph = s->n_spheres;
@@ -905,11 +913,11 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
         const uint32_t min_stack = p.light_bvh == 1 ? light_stack : 1u;
         // binary traversal pushes at most one entry per inner level
         const uint32_t bin_stack = std::max(p.sc.bvh_depth + 1, min_stack);
-        const size_t stacks = (size_t)rtw::kWavesPerBlock * 64 * sizeof(int32_t);
-        // kWorldBvhLds layout: stacks | f32 nodes (bvh32) | leaf spheres | ids (padded to 8) | lights | (f32) light pairs
-        const size_t tree_lds = stacks * bin_stack + (size_t)p.sc.n_nodes * sizeof(rtw::BvhNode<float>) +
-                                (size_t)p.sc.n_sph * sizeof(rtw::R4<R>) +
-                                (size_t)((p.sc.n_sph + 7u) & ~7u) * sizeof(uint32_t) +
+        // kWorldBvhLds layout: stacks + stealing area (traversal_lds) | f32 nodes (bvh32) | leaf spheres |
+        // ids (padded to 8) | lights | (f32) light pairs
+        const size_t tree_lds = rtw::traversal_lds<R>(bin_stack) + (size_t)p.sc.n_nodes * sizeof(rtw::BvhNode<float>) +
+                                (size_t)p.sc.n_sph * sizeof(rtw::R4<float>) +
+                                (size_t)((p.sc.n_sph + 7u) & ~7u) * sizeof(uint32_t) + 32 +   // (light list 32-B aligned)
                                 (size_t)p.sc.n_lights * sizeof(rtw::R4<R>) +
                                 // f32: the light pairs of the packed light test
                                 (sizeof(R) == 4 ? (size_t)((p.sc.n_lights + 1u) & ~1u) * sizeof(rtw::R4<R>) : 0);
@@ -920,7 +928,7 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
         } else if (bin_stack <= rtw::kBvhStack) {
             p.stack = bin_stack;
             bvh_width = 2;
-            const size_t lds_max = c->bvh_lds_max ? c->bvh_lds_max : (sizeof(R) == 4 ? 32 * 1024 : 52 * 1024);
+            const size_t lds_max = c->bvh_lds_max ? c->bvh_lds_max : (sizeof(R) == 4 ? 36 * 1024 : 52 * 1024);
             if (c->bvh_kind == 3 && tree_lds <= lds_max) {
                 world = rtw::kWorldBvhLds;
                 launch_lds = tree_lds;
@@ -1241,7 +1249,10 @@ int rtw_set_scene(rtw_ctx* c, const rtw_scene* s) {
         fix(ds.lsph); fix(ds.lid); fix(ds.lg_start); fix(ds.lg_sph); fix(ds.lg_id);
         fix(ds.quads); fix(ds.quad_mat); fix(ds.lquads); fix(ds.sph64); fix(ds.pl64); fix(ds.mat64);
         if (ds.lref) fix(ds.lref);
-        if constexpr (std::is_same<std::decay_t<decltype(ds)>, rtw::DevScene<double>>::value) fix(ds.bvh32);
+        if constexpr (std::is_same<std::decay_t<decltype(ds)>, rtw::DevScene<double>>::value) {
+            fix(ds.bvh32);
+            fix(ds.bsph32);
+        }
         fix(ds.boxes); fix(ds.box_mat);
         if (ds.mat_tex) fix(ds.mat_tex);
         fix(ds.tex_type); fix(ds.tex_p); fix(ds.tex_refs); fix(ds.perlin_vec); fix(ds.perlin_perm);

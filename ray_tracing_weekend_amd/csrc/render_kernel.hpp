@@ -464,12 +464,29 @@ __device__ __forceinline__ float lights_pdf_sum_pk(const R4<float>* __restrict__
 template <typename R, bool kRobust>
 struct SphereTester;
 
+__device__ __forceinline__ float bperm_f(float x, int32_t src) {
+    return __int_as_float(__builtin_amdgcn_ds_bpermute(src << 2, __float_as_int(x)));
+}
+__device__ __forceinline__ int32_t bperm_i(int32_t x, int32_t src) { return __builtin_amdgcn_ds_bpermute(src << 2, x); }
+__device__ __forceinline__ double bperm_d(double x, int32_t src) {
+    const uint64_t b = (uint64_t)__double_as_longlong(x);
+    const uint32_t lo = (uint32_t)bperm_i((int32_t)(uint32_t)b, src), hi = (uint32_t)bperm_i((int32_t)(b >> 32), src);
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
 template <bool kRobust>
 struct SphereTester<double, kRobust> {   // exact reference arithmetic (sphere.rs:61-80)
     V3<double> o, d;
     double tmin, tb;
     int32_t best;
     __device__ __forceinline__ double bound() const { return tb; }
+    // the ray and running result of lane `src` (subtree stealing)
+    __device__ __forceinline__ void take(int32_t src) {
+        o = mk(bperm_d(o.x, src), bperm_d(o.y, src), bperm_d(o.z, src));
+        d = mk(bperm_d(d.x, src), bperm_d(d.y, src), bperm_d(d.z, src));
+        tb = bperm_d(tb, src);
+        best = bperm_i(best, src);
+    }
     // returns whether the sphere is hit at all (t in [tmin, inf])
     __device__ __forceinline__ bool test_hit(const R4<double>& s, int32_t id) {
         double t;
@@ -490,6 +507,26 @@ struct SphereTester<float, kRobust> {    // the f32 sweep's arithmetic (see sphe
     uint32_t tminb, ub;
     int32_t best;
     __device__ __forceinline__ float bound() const { return __uint_as_float(ub + tminb); }
+    // (ub, best) as one unsigned key whose order is test()'s: ub first, then the
+    // id in signed order (best = -1 below every id); the minimum over partial
+    // traversals of one ray is the single traversal's result (subtree stealing)
+    __device__ __forceinline__ uint64_t key() const {
+        return ((uint64_t)ub << 32) | ((uint32_t)best ^ 0x80000000u);
+    }
+    __device__ __forceinline__ void from_key(uint64_t k) {
+        ub = (uint32_t)(k >> 32);
+        best = (int32_t)((uint32_t)k ^ 0x80000000u);
+    }
+    // the ray and running result of lane `src` (every lane of the wave takes
+    // part: ds_bpermute reads the source lane's registers)
+    __device__ __forceinline__ void take(int32_t src) {
+        o = mk(bperm_f(o.x, src), bperm_f(o.y, src), bperm_f(o.z, src));
+        d = mk(bperm_f(d.x, src), bperm_f(d.y, src), bperm_f(d.z, src));
+        ub = (uint32_t)bperm_i((int32_t)ub, src);
+        best = bperm_i(best, src);
+        a = len2_f32(d);
+        ia = __builtin_amdgcn_rcpf(a);
+    }
     __device__ __forceinline__ void test(const R4<float>& s, int32_t id) {
         const uint32_t u = sphere_u<kRobust>(s, o, d, a, ia, tminb);
         const bool upd = u < ub || (u == ub && id < best);
@@ -571,13 +608,16 @@ __device__ __forceinline__ void bvh_traverse(const DevScene<R>& sc, int32_t base
 // count.  With the default 4-sphere leaves there is exactly one group.
 // f64 leaves: an f32 pre-pass (sphere_may_hit: the light pre-pass of
 // lights_pdf_sum on {c, r^2}, with (r + e)^2 <= r^2 + e (r^2 + 1) + e^2) masks
-// the spheres the ray may hit; only those get the f64 test, each re-read from
-// the (LDS) leaf array -- the closest (t, id) does not depend on the order or
-// on spheres the ray misses.  Holding the four f64 spheres across the mask
-// loop instead spilled 78 VGPRs and ran slower.
-__device__ __forceinline__ bool sphere_may_hit(const R4<double>& S, float ox, float oy, float oz, float dx,
+// the spheres the ray may hit; only those get the f64 test, each read from
+// the f64 leaf array -- the closest (t, id) does not depend on the order or on
+// spheres the ray misses.  The pre-pass reads the leaf spheres rounded to f32
+// (DevScene::bsph32, staged in LDS by the LDS-world kernel: half the bytes of
+// the f64 array, which stays in HBM / L1 for the few candidates).  Holding the
+// four f64 spheres across the mask loop instead spilled 78 VGPRs and ran
+// slower.
+__device__ __forceinline__ bool sphere_may_hit(const R4<float>& S, float ox, float oy, float oz, float dx,
                                                float dy, float dz, float ia, float on, float dn) {
-    const float cx = (float)S.x, cy = (float)S.y, cz = (float)S.z, r2 = (float)S.w;
+    const float cx = S.x, cy = S.y, cz = S.z, r2 = S.w;   // the f64 sphere rounded to f32 (bsph32)
     const float fx = ox - cx, fy = oy - cy, fz = oz - cz;
     const float hb = __builtin_fmaf(dz, fz, __builtin_fmaf(dy, fy, dx * fx));
     const float tc = -hb * ia;
@@ -600,7 +640,7 @@ __device__ __forceinline__ void test_leaf(const DevScene<R>& sc, int32_t base, i
         const float on = fabsf(ox) + fabsf(oy) + fabsf(oz), dn = fabsf(dx) + fabsf(dy) + fabsf(dz);
         uint32_t mask = 0;
         for (uint32_t k = 0; k < cnt; ++k)
-            mask |= (sphere_may_hit(sc.bsph[first + k], ox, oy, oz, dx, dy, dz, ia, on, dn) ? 1u : 0u) << k;
+            mask |= (sphere_may_hit(sc.bsph32[first + k], ox, oy, oz, dx, dy, dz, ia, on, dn) ? 1u : 0u) << k;
         while (mask) {
             const uint32_t k = (uint32_t)__builtin_ctz(mask);
             mask &= mask - 1u;
@@ -821,6 +861,233 @@ __device__ __forceinline__ void bvh4_traverse(const DevScene<R>& sc, int32_t bas
     }
 }
 
+// Subtree stealing: the result slots of one wave's rays in LDS.  f32: one
+// u64 key per ray (SphereTester<float>::key, folded with an atomic min).  f64:
+// the t bits (t >= t_min > 0: their unsigned order is t's) and the id, folded
+// in two wave-synchronous steps -- an atomic min of t, then the id of a lane
+// whose t is the new minimum (stored by the lane that lowered it, atomic min
+// among equal t) -- the tester's order (smallest t, then lowest id, best = -1
+// above every id).  fold() must be called by every lane of the wave
+// (`on` selects the folding lanes).
+template <typename R>
+struct StealSlots;
+template <>
+struct StealSlots<float> {
+    unsigned long long* key;
+    __device__ __forceinline__ explicit StealSlots(unsigned char* area)
+        : key(reinterpret_cast<unsigned long long*>(area)) {}
+    template <typename TT>
+    __device__ __forceinline__ void init(uint32_t lane, const TT& T) { key[lane] = T.key(); }
+    template <typename TT>
+    __device__ __forceinline__ void fold(bool on, int32_t owner, TT& T, bool share) {
+        if (on) {
+            const uint64_t k = T.key();
+            const uint64_t prev = atomicMin(key + owner, (unsigned long long)k);
+            if (share) T.from_key(prev < k ? prev : k);
+        }
+    }
+    template <typename TT>
+    __device__ __forceinline__ void refresh(bool on, int32_t owner, TT& T) {
+        if (on) {
+            const uint64_t ko = key[owner];
+            if (ko < T.key()) T.from_key(ko);
+        }
+    }
+    template <typename TT>
+    __device__ __forceinline__ void result(uint32_t lane, TT& T) { T.from_key(key[lane]); }
+};
+template <>
+struct StealSlots<double> {
+    unsigned long long* tb;
+    uint32_t* id;
+    __device__ __forceinline__ explicit StealSlots(unsigned char* area)
+        : tb(reinterpret_cast<unsigned long long*>(area)), id(reinterpret_cast<uint32_t*>(area + 64 * 8)) {}
+    static __device__ __forceinline__ uint64_t bits(double t) { return (uint64_t)__double_as_longlong(t); }
+    template <typename TT>
+    __device__ __forceinline__ void init(uint32_t lane, const TT& T) {
+        tb[lane] = bits(T.tb);
+        id[lane] = (uint32_t)T.best;
+    }
+    template <typename TT>
+    __device__ __forceinline__ void fold(bool on, int32_t owner, TT& T, bool share) {
+        const uint64_t t = bits(T.tb);
+        bool lowered = false;
+        if (on) lowered = t < atomicMin(tb + owner, (unsigned long long)t);
+        __builtin_amdgcn_wave_barrier();
+        const uint64_t cur = on ? tb[owner] : 0;
+        if (on && t == cur && lowered) id[owner] = (uint32_t)T.best;
+        __builtin_amdgcn_wave_barrier();
+        if (on && t == cur) atomicMin(id + owner, (uint32_t)T.best);
+        if (share) {
+            __builtin_amdgcn_wave_barrier();
+            if (on) {
+                T.tb = __longlong_as_double((long long)cur);
+                T.best = (int32_t)id[owner];
+            }
+        }
+    }
+    template <typename TT>
+    __device__ __forceinline__ void refresh(bool on, int32_t owner, TT& T) {
+        if (on) {
+            const uint64_t t = tb[owner];
+            const uint32_t i = id[owner];
+            if (t < bits(T.tb) || (t == bits(T.tb) && i < (uint32_t)T.best)) {
+                T.tb = __longlong_as_double((long long)t);
+                T.best = (int32_t)i;
+            }
+        }
+    }
+    template <typename TT>
+    __device__ __forceinline__ void result(uint32_t lane, TT& T) {
+        T.tb = __longlong_as_double((long long)tb[lane]);
+        T.best = (int32_t)id[lane];
+    }
+};
+
+// bvh_traverse_ww with intra-wave subtree stealing.  A lane with nothing left
+// to traverse -- its ray done, or never started (the own-sphere shortcut) --
+// takes the bottom entry of another lane's stack (the largest subtree that
+// lane has postponed) together with that lane's ray and running result, and
+// traverses it as its own; lanes pair up by rank (the k-th idle lane with the
+// k-th lane holding stack entries) through 64 rendezvous bytes in LDS, the ray
+// moves with ds_bpermute.  Every lane on a ray folds its result into the ray
+// owner's slot after each leaf phase and culls with the minimum so far (the
+// bound is shared), and a finished partial traversal is folded before the
+// lane steals again; the owner reads the minimum at the end.  Box tests only
+// cull and the slot order is the tester's (smallest t, then lowest id), so
+// the result is the single traversal's bit for bit (tests: BVH == brute
+// force, f64 == oracle).  f64 rays cull on the f32 tree with widened slab
+// intervals exactly as bvh_traverse_ww.  tools/steal_sim.cpp (lockstep
+// simulation on C2 ray batches): 17.0 -> 8.4 inner passes and 3.9 -> 1.9
+// leaf passes per 64 segments.
+template <typename R, typename TT>
+__device__ __forceinline__ void bvh_traverse_steal(const DevScene<R>& sc, int32_t base, TT& T,
+                                                   int32_t* __restrict__ stk_wave, uint32_t lane,
+                                                   unsigned char* __restrict__ steal_area, uint32_t& nvis,
+                                                   uint32_t& ntest, bool skip) {
+    constexpr int32_t kDone = 0x7fffffff;
+    constexpr bool kWide = sizeof(R) == 8;   // f64 ray on the f32 tree: widened intervals
+    StealSlots<R> slots(steal_area);
+    uint8_t* __restrict__ rv = steal_area + kStealSlotBytes<R>;
+    int32_t* __restrict__ stk = stk_wave + lane;
+    float ix, iy, iz, oix, oiy, oiz, slack, tbw;
+    auto setup = [&]() {
+        ix = inv_((float)T.d.x);
+        iy = inv_((float)T.d.y);
+        iz = inv_((float)T.d.z);
+        oix = (float)T.o.x * ix;
+        oiy = (float)T.o.y * iy;
+        oiz = (float)T.o.z * iz;
+        slack = kWide ? 0x1p-20f * fmaxf(fmaxf(fabsf(oix), fabsf(oiy)), fmaxf(fabsf(oiz), 0.0f)) : 0.0f;
+    };
+    auto bound = [&]() { tbw = kWide ? cull_bound(T.bound()) : 0.0f; };
+    setup();
+    bound();
+    auto slab = [](float b, float i, float oi) {
+        if constexpr (kWide) return __builtin_fmaf(b, i, -oi);
+        else return b * i - oi;
+    };
+    const BvhNode<float>* __restrict__ nodes = cull_nodes(sc);
+    int32_t sp = 0, sb = 0;             // stack entries [sb, sp): below sb they were given away
+    int32_t owner = (int32_t)lane;      // the lane whose ray this lane traverses
+    int32_t node = skip ? kDone : 0;
+    int32_t leaf = 0;
+    slots.init(lane, T);
+    for (;;) {
+        for (;;) {
+            if (node < 0 && leaf == 0) {   // park the leaf, continue with the stack
+                leaf = node;
+                node = sp > sb ? stk[--sp * 64] : kDone;
+            }
+            const bool idle = node == kDone && leaf == 0, donor = sp > sb;
+            const uint64_t mi = __ballot(idle), md = __ballot(donor);
+            if (mi != 0 && md != 0) {
+                const uint32_t np = min(__popcll(mi), __popcll(md));
+                const uint32_t ri = __builtin_amdgcn_mbcnt_hi((uint32_t)(mi >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mi, 0u));
+                const uint32_t rd = __builtin_amdgcn_mbcnt_hi((uint32_t)(md >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)md, 0u));
+                const bool thief = idle && ri < np, give = donor && rd < np;
+                if (give) rv[rd] = (uint8_t)lane;
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                const int32_t src = thief ? (int32_t)rv[ri] : (int32_t)lane;
+                slots.fold(thief, owner, T, false);   // the thief's finished traversal
+#if RTW_STEAL_TOP
+                // the donor's top entry: its nearest postponed subtree
+                const int32_t v_owner = bperm_i(owner, src), v_sb = bperm_i(sp, src) - 1;
+#else
+                const int32_t v_owner = bperm_i(owner, src), v_sb = bperm_i(sb, src);
+#endif
+                TT U = T;
+                U.take(src);
+                if (thief) {
+                    T = U;
+                    owner = v_owner;
+                    node = stk_wave[v_sb * 64 + src];
+                    sp = sb = 0;
+                    setup();
+                }
+                slots.refresh(thief, owner, T);       // the freshest shared bound
+                if (thief) bound();
+#if RTW_STEAL_TOP
+                if (give) --sp;
+#else
+                if (give) ++sb;
+#endif
+            }
+            const bool inner = node >= 0 && node != kDone;
+            if (!__any(inner) || __all(leaf != 0 || node == kDone)) break;
+            if (inner) {
+                RTW_PROBE_LANES(1);
+                ++nvis;
+                const BvhNode<float>& nd = nodes[node];
+                const float tb = kWide ? tbw : (float)T.bound();
+                float tn[2], tf[2];
+#pragma unroll
+                for (int c = 0; c < 2; ++c) {
+                    const float x0 = slab(nd.lo_x[c], ix, oix), x1 = slab(nd.hi_x[c], ix, oix);
+                    const float y0 = slab(nd.lo_y[c], iy, oiy), y1 = slab(nd.hi_y[c], iy, oiy);
+                    const float z0 = slab(nd.lo_z[c], iz, oiz), z1 = slab(nd.hi_z[c], iz, oiz);
+                    tn[c] = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), 0.0f));
+                    tf[c] = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), tb));
+                    if constexpr (kWide) {
+                        tn[c] = __builtin_fmaf(tn[c], 1.0f - 0x1p-20f, -slack);
+                        tf[c] = __builtin_fmaf(tf[c], 1.0f + 0x1p-20f, slack);
+                    }
+                }
+                const bool h0 = tn[0] <= tf[0], h1 = tn[1] <= tf[1];
+                const int32_t c0 = nd.child[0], c1 = nd.child[1];
+                if (h0 && h1) {
+                    const bool first0 = tn[0] <= tn[1];
+                    stk[sp * 64] = first0 ? c1 : c0;
+                    ++sp;
+                    node = first0 ? c0 : c1;
+                } else if (h0 | h1) {
+                    node = h0 ? c0 : c1;
+                } else {
+                    node = sp > sb ? stk[--sp * 64] : kDone;
+                }
+            }
+        }
+        if (!__any(leaf != 0)) break;   // no parked leaves: every lane is done
+        const bool tested = leaf != 0;
+        if (tested) {
+            RTW_PROBE_LANES(2);
+            test_leaf(sc, base, leaf, T, ntest);
+            leaf = 0;
+        }
+        // share the bound: every lane on this ray culls with the best hit any
+        // of them has found so far
+        slots.fold(tested, owner, T, true);
+        if (tested) bound();
+    }
+    slots.fold(true, owner, T, false);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    slots.result(lane, T);
+}
+
 // `self` >= 0: the ray starts on that (isolated) sphere; it is tested first
 // and, when the ray hits it again, that hit is the closest sphere hit (see
 // isolated_spheres, host/bvh.hpp) and the traversal is skipped.
@@ -1003,6 +1270,10 @@ __device__ __forceinline__ bool front64(V3<double> d, V3<double> n) {
 template <bool kRobust>
 struct SphereTesterX : SphereTester<float, kRobust> {
     int32_t excl;
+    __device__ __forceinline__ void take(int32_t src) {
+        SphereTester<float, kRobust>::take(src);
+        excl = bperm_i(excl, src);
+    }
     __device__ __forceinline__ void test(const R4<float>& s, int32_t id) {
         const uint32_t u = sphere_u<kRobust>(s, this->o, this->d, this->a, this->ia, this->tminb);
         const bool upd = (u < this->ub || (u == this->ub && id < this->best)) && id != excl;
@@ -1024,6 +1295,65 @@ __device__ __forceinline__ void bvh_closest_excl(const DevScene<float>& sc, int3
     T.best = best;
     T.excl = excl;
     bvh_dispatch<kKind>(sc, base, o, d, T, stk, nvis, ntest, -1);
+    tb = T.bound();
+    best = T.best;
+}
+
+// The same two queries with subtree stealing (while-while kernels): every
+// active lane of the wave calls them -- a lane whose ray needs no traversal
+// (the own-sphere shortcut: `skip`) helps the others.
+template <bool kRobust>
+__device__ __forceinline__ void bvh_closest_steal(const DevScene<double>& sc, int32_t base, V3<double> o,
+                                                  V3<double> d, double tmin, double& tb, int32_t& best,
+                                                  int32_t* stk_wave, uint32_t lane, unsigned char* steal_area,
+                                                  uint32_t& nvis, uint32_t& ntest, int32_t self) {
+    SphereTester<double, kRobust> T{o, d, tmin, tb, best};
+    bool skip = false;
+    if (self >= 0) {
+        skip = T.test_hit(sc.sph[self], base + self);
+        ++ntest;
+    }
+    bvh_traverse_steal(sc, base, T, stk_wave, lane, steal_area, nvis, ntest, skip);
+    tb = T.tb;
+    best = T.best;
+}
+template <bool kRobust>
+__device__ __forceinline__ void bvh_closest_steal(const DevScene<float>& sc, int32_t base, V3<float> o, V3<float> d,
+                                                  float tmin, float& tb, int32_t& best, int32_t* stk_wave,
+                                                  uint32_t lane, unsigned char* steal_area, uint32_t& nvis,
+                                                  uint32_t& ntest, int32_t self) {
+    SphereTester<float, kRobust> T;
+    T.o = o;
+    T.d = d;
+    T.a = len2_f32(d);
+    T.ia = __builtin_amdgcn_rcpf(T.a);
+    T.tminb = __float_as_uint(tmin);
+    T.ub = __float_as_uint(tb) - T.tminb;
+    T.best = best;
+    bool skip = false;
+    if (self >= 0) {
+        skip = T.test_hit(sc.sph[self], base + self);
+        ++ntest;
+    }
+    bvh_traverse_steal(sc, base, T, stk_wave, lane, steal_area, nvis, ntest, skip);
+    tb = T.bound();
+    best = T.best;
+}
+template <bool kRobust>
+__device__ __forceinline__ void bvh_closest_excl_steal(const DevScene<float>& sc, int32_t base, V3<float> o,
+                                                       V3<float> d, float tmin, float& tb, int32_t& best,
+                                                       int32_t* stk_wave, uint32_t lane, unsigned char* steal_area,
+                                                       uint32_t& nvis, uint32_t& ntest, int32_t excl, bool skip) {
+    SphereTesterX<kRobust> T;
+    T.o = o;
+    T.d = d;
+    T.a = len2_f32(d);
+    T.ia = __builtin_amdgcn_rcpf(T.a);
+    T.tminb = __float_as_uint(tmin);
+    T.ub = __float_as_uint(tb) - T.tminb;
+    T.best = best;
+    T.excl = excl;
+    bvh_traverse_steal(sc, base, T, stk_wave, lane, steal_area, nvis, ntest, skip);
     tb = T.bound();
     best = T.best;
 }
@@ -1289,6 +1619,14 @@ __device__ V3<R> tex_colour(const DevScene<R>& sc, uint32_t tid, R u, R v, V3<R>
 //   kOptHit64    (f32 kernels of sphere + plane scenes) f64 ray origin, own-sphere re-hit test,
 //                hit t and hit point (sphere_t_ref64): the reference's self-intersection odds
 enum : int { kOptRobust = 1, kOptLightBvh = 2, kOptTex = 4, kOptPrims = 8, kOptHit64 = 16 };
+// subtree stealing in the f32 while-while kernels (bvh_traverse_steal); 0
+// builds them without it (timing comparisons, tools/variants.sh)
+#ifndef RTW_STEAL
+#define RTW_STEAL 1
+#endif
+#ifndef RTW_STEAL_TOP
+#define RTW_STEAL_TOP 0
+#endif
 template <typename R, int kWorld, int kOpt>
 // f32: ask for 5 waves per SIMD (<= 96 VGPRs), 4 for the hit64 kernels.
 #ifndef RTW_WAVES
@@ -1333,22 +1671,28 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
     // instead of the vector-memory (TA/L1) path the shading loads use.
     DevScene<R> scw = p.sc;
     if constexpr (kWorld == kWorldBvhLds) {
-        unsigned char* base = smem + (size_t)kWavesPerBlock * p.stack * 64 * sizeof(int32_t);
+        unsigned char* base = smem + traversal_lds<R>(p.stack);
         // the f32 tree (bvh32) in both precisions: the while-while traversal culls on it
         BvhNode<float>* l_nodes = reinterpret_cast<BvhNode<float>*>(base);
-        R4<R>* l_bsph = reinterpret_cast<R4<R>*>(l_nodes + p.sc.n_nodes);
+        // the leaf spheres {c, r^2} in f32 (f64: the pre-pass copy bsph32; the
+        // f64 candidates are read from the global leaf array)
+        R4<float>* l_bsph = reinterpret_cast<R4<float>*>(l_nodes + p.sc.n_nodes);
         uint32_t* l_bid = reinterpret_cast<uint32_t*>(l_bsph + p.sc.n_sph);
         static_assert(sizeof(BvhNode<float>) % 16 == 0, "nodes are copied in 16-B units");
         const uint4* g_nodes = reinterpret_cast<const uint4*>(cull_nodes(p.sc));
         constexpr uint32_t kNode16 = sizeof(BvhNode<float>) / 16;
         for (uint32_t k = threadIdx.x; k < p.sc.n_nodes * kNode16; k += kBlock)
             reinterpret_cast<uint4*>(l_nodes)[k] = g_nodes[k];
+        const R4<float>* g_bsph32;
+        if constexpr (sizeof(R) == 4) g_bsph32 = p.sc.bsph;
+        else g_bsph32 = p.sc.bsph32;
         for (uint32_t k = threadIdx.x; k < p.sc.n_sph; k += kBlock) {
-            l_bsph[k] = p.sc.bsph[k];
+            l_bsph[k] = g_bsph32[k];
             l_bid[k] = p.sc.bid[k];
         }
         // the light list follows, 32-B aligned (read by the light pdf / sampling)
-        l_li = reinterpret_cast<R4<R>*>(l_bid + ((p.sc.n_sph + 7u) & ~7u));
+        l_li = reinterpret_cast<R4<R>*>(
+            (reinterpret_cast<uintptr_t>(l_bid + ((p.sc.n_sph + 7u) & ~7u)) + 31u) & ~(uintptr_t)31u);
         for (uint32_t k = threadIdx.x; k < p.sc.n_lights; k += kBlock) l_li[k] = p.sc.lights[k];
         if constexpr (sizeof(R) == 4) {
             // and again as pairs for the packed light test (lights_pdf_sum_pk)
@@ -1363,14 +1707,23 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
             }
         }
         __syncthreads();
-        if constexpr (sizeof(R) == 4) scw.bvh = l_nodes;
-        else scw.bvh32 = l_nodes;
-        scw.bsph = l_bsph;
+        if constexpr (sizeof(R) == 4) {
+            scw.bvh = l_nodes;
+            scw.bsph = l_bsph;
+        } else {
+            scw.bvh32 = l_nodes;
+            scw.bsph32 = l_bsph;
+        }
         scw.bid = l_bid;
     }
     if constexpr (kWorld == kWorldBvhLds) li = l_li;
 
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    // subtree stealing (while-while kernels): this wave's result slots and
+    // rendezvous bytes, after the workgroup's traversal stacks
+    constexpr bool kSteal = RTW_STEAL && (kWorld == kWorldBvhWW || kWorld == kWorldBvhLds);
+    unsigned char* const steal_area =
+        smem + (size_t)kWavesPerBlock * p.stack * 64 * sizeof(int32_t) + wave * kStealLdsPerWave<R>;
     // the wave's current task (wave-uniform): local tile lt = global 8x8 tile
     // T = lt * nranks + rank at (tx, ty) -- the ranks take the image's tiles
     // round-robin (rtw_tiles_for_rank) -- and chunks [c_begin, c_begin +
@@ -1437,7 +1790,6 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
     uint32_t px = 0, i = 0, j = 0, c = 0, s = 0, s_end = 0;
     uint32_t my_lt = 0;           // local tile of the lane's item
     uint64_t pix = 0;
-    V3<R> part = zero;            // fold(Colour::default(), +) of the item's samples
     Rng g;
     V3<R> o = zero, d = zero, mult = zero, res = zero;
     uint32_t depth = 0;
@@ -1511,7 +1863,6 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                         pix = (uint64_t)j * p.W + i;
                         s = c * p.chunk;
                         s_end = min(s + p.chunk, p.spp);
-                        part = zero;
                         active = true;
                         need = false;
                         start_sample();
@@ -1590,7 +1941,18 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                         skip = self_iso;          // isolated: provably the closest sphere hit
                     }
                 }
-                if (!skip) {
+                if constexpr (kSteal) {
+                    // every active lane calls the traversal: the skipped ones steal work
+                    RTW_PROBE_LANES(6);
+                    const int32_t prev = best, excl = self_s >= 0 ? sbase + self_s : -1;
+                    int32_t* stk_wave = reinterpret_cast<int32_t*>(smem) + wave * p.stack * 64;
+                    bvh_closest_excl_steal<kRobust>(scw, sbase, o, d, tmin, tb, best, stk_wave, lane, steal_area,
+                                                    nvis, ntest, excl, skip);
+                    if (!skip && best != prev && best >= sbase) {
+                        if (!sphere_t_ref64(p.sc.sph64[best - sbase], o64, d64, tb64)) tb64 = (double)tb;
+                        RTW_PROBE_ABL_WINNER();
+                    }
+                } else if (!skip) {   // (kernels without stealing)
                     RTW_PROBE_LANES(6);
                     const int32_t prev = best, excl = self_s >= 0 ? sbase + self_s : -1;
                     if constexpr (kWorld >= kWorldBvh) {
@@ -1613,7 +1975,12 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                 RTW_PROBE_CLOSEST();
                 int32_t* stk = reinterpret_cast<int32_t*>(smem) + wave * p.stack * 64 + lane;
                 constexpr int kKind = kWorld == kWorldBvhLds ? kWorldBvhWW : kWorld;
-                bvh_closest<kKind, kRobust>(scw, sbase, o, d, tmin, tb, best, stk, nvis, ntest, self_s);
+                if constexpr (kSteal) {
+                    bvh_closest_steal<kRobust>(scw, sbase, o, d, tmin, tb, best, stk - lane, lane, steal_area,
+                                               nvis, ntest, self_s);
+                } else {
+                    bvh_closest<kKind, kRobust>(scw, sbase, o, d, tmin, tb, best, stk, nvis, ntest, self_s);
+                }
             } else {
                 sweep_spheres<kRobust>(sph, p.sc.n_sph, sbase, o, d, tmin, tb, best);
             }
@@ -1865,17 +2232,21 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                 }
             }
             if (done) {
-                part = part + col;
+                // the item's running sum lives in its chunk-sum slot, not in
+                // registers: (0 + s_first) on the first sample, then slot + s
+                // -- the fold of camera.rs:323-335 in the same order
+                R* dst = p.partial + (((size_t)my_lt * 64 + px) * p.n_chunks + c) * 3;
+                const V3<R> prev = s == c * p.chunk ? zero : mk(dst[0], dst[1], dst[2]);
+                const V3<R> part = prev + col;
+                dst[0] = part.x;
+                dst[1] = part.y;
+                dst[2] = part.z;
                 ++s;
                 if (s < s_end) {
                     RTW_PROBE_SEED();
                     start_sample();
                 RTW_PROBE_LANES(10);
                 } else {
-                    R* dst = p.partial + (((size_t)my_lt * 64 + px) * p.n_chunks + c) * 3;
-                    dst[0] = part.x;
-                    dst[1] = part.y;
-                    dst[2] = part.z;
                     if (p.tile_cost)   // pilot render (chunk 1): this sample's segments
                         atomicAdd(p.tile_cost + my_lt, p.max_depth - depth + 1u);
                     active = false;
@@ -2022,7 +2393,7 @@ constexpr int kVariantRan = 1 << 16;
 template <typename R, int kOpt>
 inline int launch_world(const KParams<R>& p, int world, size_t lds_bytes, uint32_t blocks,
                         hipStream_t stream) {
-    const size_t stacks = (size_t)kWavesPerBlock * p.stack * 64 * sizeof(int32_t);
+    const size_t stacks = traversal_lds<R>(p.stack);
     const bool resident = p.persist == kPersistResident;
     constexpr int kBrute = kOpt & ~dev::kOptLightBvh;   // the light BVH needs the BVH kernels' stack
     // textured scenes are small: their kernels exist for the brute-force and

@@ -83,6 +83,7 @@ struct DevSceneCull {};
 template <>
 struct DevSceneCull<double> {
     const BvhNode<float>* bvh32;
+    const R4<float>* bsph32;          // bsph rounded to f32 {c, r^2}: the leaf pre-pass
 };
 
 template <typename R>
@@ -162,6 +163,19 @@ constexpr uint32_t kBoxRot = 144, kBoxInv = 153, kBoxT = 162, kBoxTi = 165, kBox
                    kBoxOk = 174;
 
 constexpr uint32_t kBvhStack = 32;    // per-lane traversal stack entries (LDS)
+// Subtree stealing in the while-while traversal (render_kernel.hpp
+// bvh_traverse_steal): per wave the result slots of its 64 rays (f32: a u64
+// key; f64: u64 t bits + u32 id) and 64 rendezvous bytes, in LDS right after
+// the traversal stacks of the workgroup's waves.
+template <typename R>
+constexpr uint32_t kStealSlotBytes = sizeof(R) == 4 ? 64 * 8 : 64 * 12;
+template <typename R>
+constexpr uint32_t kStealLdsPerWave = kStealSlotBytes<R> + 64;
+// LDS of the traversal stacks + the stealing area of one workgroup
+template <typename R>
+__host__ __device__ inline size_t traversal_lds(uint32_t stack) {
+    return (size_t)kWavesPerBlock * ((size_t)stack * 64 * sizeof(int32_t) + kStealLdsPerWave<R>);
+}
 constexpr uint32_t kPersistResident = 0xFFFFFFFFu;   // KParams::persist: one resident grid
 
 
