@@ -911,13 +911,15 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
             else if (light_stack <= rtw::kBvhStack) p.light_bvh = 1;  // light BVH
         }
         const uint32_t min_stack = p.light_bvh == 1 ? light_stack : 1u;
-        // binary traversal pushes at most one entry per inner level
-        const uint32_t bin_stack = std::max(p.sc.bvh_depth + 1, min_stack);
+        // binary traversal pushes at most one entry per inner level: a leaf at
+        // level `bvh_depth` has that many inner nodes above it (host/bvh.cpp)
+        const uint32_t bin_stack = std::max(p.sc.bvh_depth, min_stack);
         // kWorldBvhLds layout: stacks + stealing area (traversal_lds) | f32 nodes (bvh32) | leaf spheres |
         // ids (padded to 8) | lights | (f32) light pairs
         const size_t tree_lds = rtw::traversal_lds<R>(bin_stack) + (size_t)p.sc.n_nodes * sizeof(rtw::BvhNode<float>) +
                                 (size_t)p.sc.n_sph * sizeof(rtw::R4<float>) +
-                                (size_t)((p.sc.n_sph + 7u) & ~7u) * sizeof(uint32_t) + 32 +   // (light list 32-B aligned)
+                                (size_t)((p.sc.n_sph + 7u) & ~7u) * sizeof(uint32_t) +
+                                (sizeof(R) == 8 ? 32 : 0) +   // (f64: the light list 32-B aligned)
                                 (size_t)p.sc.n_lights * sizeof(rtw::R4<R>) +
                                 // f32: the light pairs of the packed light test
                                 (sizeof(R) == 4 ? (size_t)((p.sc.n_lights + 1u) & ~1u) * sizeof(rtw::R4<R>) : 0);
@@ -943,7 +945,7 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
     if (p.sc.mat_tex && (world == rtw::kWorldBvh4 || world == rtw::kWorldBvh)) {
         world = rtw::kWorldBvhWW;
         bvh_width = 2;
-        p.stack = std::max(p.sc.bvh_depth + 1, p.light_bvh == 1 ? p.sc.lbvh_depth + 1 : 1u);
+        p.stack = std::max(p.sc.bvh_depth, p.light_bvh == 1 ? p.sc.lbvh_depth + 1 : 1u);
         if (p.stack > rtw::kBvhStack) return fail(c, RTW_E_UNSUPPORTED, "BVH deeper than the kernel's traversal stack");
     }
     // f64 hit points: the f32 kernels of sphere + plane scenes (the launch

@@ -1018,10 +1018,10 @@ __device__ __forceinline__ void bvh_traverse_steal(const DevScene<R>& sc, int32_
 #else
                 const int32_t v_owner = bperm_i(owner, src), v_sb = bperm_i(sb, src);
 #endif
-                TT U = T;
-                U.take(src);
+                // every lane reads the ray of `src`: a thief its donor's, the
+                // others their own (src = lane), so no copy of T is needed
+                T.take(src);
                 if (thief) {
-                    T = U;
                     owner = v_owner;
                     node = stk_wave[v_sb * 64 + src];
                     sp = sb = 0;
@@ -1690,9 +1690,9 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
             l_bsph[k] = g_bsph32[k];
             l_bid[k] = p.sc.bid[k];
         }
-        // the light list follows, 32-B aligned (read by the light pdf / sampling)
-        l_li = reinterpret_cast<R4<R>*>(
-            (reinterpret_cast<uintptr_t>(l_bid + ((p.sc.n_sph + 7u) & ~7u)) + 31u) & ~(uintptr_t)31u);
+        // the light list follows, aligned to its element (read by the light pdf / sampling)
+        l_li = reinterpret_cast<R4<R>*>((reinterpret_cast<uintptr_t>(l_bid + ((p.sc.n_sph + 7u) & ~7u)) +
+                                         (sizeof(R4<R>) - 1)) & ~(uintptr_t)(sizeof(R4<R>) - 1));
         for (uint32_t k = threadIdx.x; k < p.sc.n_lights; k += kBlock) l_li[k] = p.sc.lights[k];
         if constexpr (sizeof(R) == 4) {
             // and again as pairs for the packed light test (lights_pdf_sum_pk)

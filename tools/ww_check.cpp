@@ -2,7 +2,7 @@
 // traversal in render_kernel.hpp (bvh_traverse_ww): 64 lanes execute the
 // same iteration with the kernel's wave-uniform loop conditions; every lane's
 // closest sphere must equal brute force, every wave must terminate, and the
-// stack must stay within depth + 1 entries.
+// stack must stay within `depth` entries (the kernel sizes it so).
 //   g++ -O2 -std=c++17 -I ray_tracing_weekend_amd/csrc tools/ww_check.cpp \
 //       ray_tracing_weekend_amd/csrc/host/bvh.cpp -o /tmp/ww_check && /tmp/ww_check
 #include <math.h>
@@ -34,7 +34,7 @@ int main(int argc, char** argv) {
         sph[4 * k + 3] = k % 7 == 0 ? 1.0 : Rr(g);
     }
     const rtw::BvhBuild bb = rtw::build_bvh(sph.data(), n, 1e-5);
-    const int cap = (int)bb.depth + 1;
+    const int cap = (int)bb.depth;
     auto hit_t = [&](uint32_t k, const double* o, const double* d, double& t) {
         const double* s = &sph[4 * k];
         const double oc[3] = {o[0] - s[0], o[1] - s[1], o[2] - s[2]};
