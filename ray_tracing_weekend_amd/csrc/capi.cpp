@@ -53,6 +53,10 @@ struct rtw_ctx {
                                       // per-tile segment counts (cached per scene / camera / split);
                                       // 1: for worlds in LDS or within an L2, 2: always, 0: never
     uint32_t lpt_min_spp = 32;        // ... for renders of at least this many samples per pixel
+    uint32_t lpt_pilot_spp = 2;       // the pilot render: samples per pixel
+    uint32_t lpt_pilot_depth = 0;     // ... and its max depth (0: the camera's); a path's segments
+                                      // run one after another, so the pilot lasts as long as its
+                                      // longest path
     uint32_t light_bvh_min = 64;      // light lists at least this long use the light BVH
                                       // (C2, 19 lights: the linear masked loop is faster)
     hipStream_t stream = nullptr;
@@ -81,7 +85,7 @@ struct rtw_ctx {
     std::vector<unsigned char> h_out;
     // longest-tiles-first task list (pilot render, see lpt_pilot / lpt_tasks)
     uint64_t scene_serial = 0;        // ++ per rtw_upload_scene
-    static constexpr uint32_t kPilotSpp = 2, kMaxGroup = 32;
+    static constexpr uint32_t kMaxGroup = 32;
     void* d_lpt = nullptr;            // pilot: [tile cost | chunk sums | tiles]
     size_t lpt_cap = 0;
     bool lpt_valid = false;           // h_lpt_cost is the pilot of (lpt_cam, lpt_serial, rank split, precision)
@@ -754,7 +758,8 @@ template <typename R>
 int lpt_pilot(rtw_ctx* c, const rtw::KParams<R>& p, int world, size_t launch_lds, hipStream_t stream) {
     const uint32_t nt = p.n_local_tiles;
     rtw::KParams<R> q = p;
-    q.spp = std::min(p.spp, rtw_ctx::kPilotSpp);
+    q.spp = std::min(p.spp, std::max(c->lpt_pilot_spp, 1u));
+    if (c->lpt_pilot_depth) q.max_depth = std::min(p.max_depth, c->lpt_pilot_depth);
     q.chunk = 1;
     q.n_chunks = q.spp;
     q.group = q.n_chunks;
@@ -1094,6 +1099,8 @@ int rtw_set_tuning(rtw_ctx* c, const char* key, int64_t value) {
     else if (k == "hit64") c->hit64 = value ? 1u : 0u;
     else if (k == "lpt") c->lpt = (uint32_t)std::min<int64_t>(value, 2);
     else if (k == "lpt_min_spp") c->lpt_min_spp = (uint32_t)std::min<int64_t>(value, 1u << 30);
+    else if (k == "lpt_pilot_spp") c->lpt_pilot_spp = (uint32_t)std::min<int64_t>(std::max<int64_t>(value, 1), 64);
+    else if (k == "lpt_pilot_depth") c->lpt_pilot_depth = (uint32_t)std::min<int64_t>(value, 1u << 20);
     else if (k == "light_bvh_min") c->light_bvh_min = (uint32_t)std::min<int64_t>(value, 1u << 30);
     else if (k == "partial_max") c->partial_max = std::max<size_t>(1 << 20, (size_t)value);
     else if (k == "group") c->group = (uint32_t)value;

@@ -135,9 +135,11 @@ __device__ __forceinline__ bool aabb_hit_ref(const R* lo, const R* hi, V3<R> o, 
 // axis pinned at [0, 0] or [-inf, inf]) for a finite ray: an infinite axis
 // always yields (-inf, +inf) after the sign swap, which no later max_ / min_
 // or comparison changes, so the test reduces to the one pinned axis, q = (0 -
-// o_a) / d_a, and hits iff !(q < rs) -- the same IEEE quotient and the same
-// outcome (NaN included) as the six-division reference sequence.  Anything
-// else (a non-finite ray, other boxes) takes aabb_hit_ref itself.
+// o_a) / d_a, and hits iff !(q < rs) -- the same quotient and the same
+// outcome (NaN included) as the six-division reference sequence (f64: IEEE
+// division; f32: a * rcp(b), whose infinities for a zero d_a or an infinite
+// a follow the same signs).  Anything else (a non-finite ray, other boxes)
+// takes aabb_hit_ref itself.
 template <typename R>
 __device__ __forceinline__ bool aabb_hit_plane(const R* lo, const R* hi, V3<R> o, V3<R> d, R rs) {
     const bool fin = __builtin_isfinite(o.x) && __builtin_isfinite(o.y) && __builtin_isfinite(o.z) &&
@@ -1893,8 +1895,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
             for (int32_t k = 0; k < nplanes; ++k) {
                 R t;
                 const R* pl = p.sc.planes + kPlaneR * k;
-                const bool box_hit = sizeof(R) == 8 ? aabb_hit_plane(pl + 6, pl + 9, o, d, tmin)
-                                                    : aabb_hit_ref(pl + 6, pl + 9, o, d, tmin);
+                const bool box_hit = aabb_hit_plane(pl + 6, pl + 9, o, d, tmin);
                 if (box_hit && plane_t(pl, o, d, tmin, t, p.counters + 4) &&
                     (best < 0 || t < tb)) {
                     tb = t;
@@ -2159,7 +2160,10 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                     const V3<R> att = colour;
                     const Onb<R> uvw(nrm);
                     V3<R> dir;
-                    if (PR::u_std(g.next()) < (R)0.5) {
+                    const bool to_light = PR::u_std(g.next()) < (R)0.5;
+                    bool sampled = false;
+                    if (to_light && (p.sc.n_list == 0 || (kPrims && p.sc.lref))) {
+                        sampled = true;
                         // HittableList::random (hittable_list.rs:414-419): a
                         // uniform light (one gen_index draw), then its random()
                         if (p.sc.n_list == 0) {
@@ -2168,7 +2172,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                             // at its next world query, as in the oracle
                             atomicAdd(p.counters + 5, 1ull);
                             dir = mk((R)NAN, (R)NAN, (R)NAN);
-                        } else if (kPrims && p.sc.lref) {
+                        } else {
                             const uint32_t ref = p.sc.lref[g.index(p.sc.n_list)];
                             if (ref & kLrefQuad) {
                                 dir = quad_random(p.sc.lquads + kQuadR * (ref & 0x3fffffffu), pnt, g);
@@ -2178,12 +2182,14 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                                 const R4<R> L = li[ref];
                                 dir = sphere_random(mk(L.x, L.y, L.z), L.w, pnt, g);
                             }
-                        } else {
-                            const R4<R> L = li[g.index(p.sc.n_lights)];
-                            dir = sphere_random(mk(L.x, L.y, L.z), L.w, pnt, g);
                         }
-                    } else {
-                        dir = uvw.transform(cosine_hemisphere<R>(g));
+                    }
+                    if (!sampled) {
+                        // a sphere light (one gen_index draw, then Sphere::random)
+                        // or the cosine lobe, in one pass (mixture_direction)
+                        R4<R> L = R4<R>{0, 0, 0, 0};
+                        if (to_light) L = li[g.index(p.sc.n_lights)];
+                        dir = mixture_direction(to_light, uvw, mk(L.x, L.y, L.z), L.w, pnt, g);
                     }
                     RTW_PROBE_LAMBERT_DIR();
                     const V3<R> ndir = PR::normalize(dir);
@@ -2236,7 +2242,10 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                 // registers: (0 + s_first) on the first sample, then slot + s
                 // -- the fold of camera.rs:323-335 in the same order
                 R* dst = p.partial + (((size_t)my_lt * 64 + px) * p.n_chunks + c) * 3;
-                const V3<R> prev = s == c * p.chunk ? zero : mk(dst[0], dst[1], dst[2]);
+                V3<R> prev = zero;
+                if (p.chunk > 1) {   // (wave-uniform: one sample per item never reads the slot)
+                    if (s != c * p.chunk) prev = mk(dst[0], dst[1], dst[2]);
+                }
                 const V3<R> part = prev + col;
                 dst[0] = part.x;
                 dst[1] = part.y;

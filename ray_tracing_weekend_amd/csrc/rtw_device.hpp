@@ -370,6 +370,54 @@ __device__ __forceinline__ V3<R> sphere_random(V3<R> c, R radius, V3<R> o, Rng& 
     }
 }
 
+// The Lambertian mixture's direction (MixturePdf::generate, pdf.rs:91-96)
+// for a light list of spheres: to_light -> Sphere::random of light L
+// (sphere.rs:113-127, as sphere_random), else CosinePdf::generate in the
+// normal's frame uvw (pdf.rs:45-48, as cosine_hemisphere).  Both draw r1, r2,
+// take an azimuth from one and a height from the other and rotate by a
+// frame, so one code path serves both: the lanes of a wave that took either
+// branch run it together (one pass instead of two).  Per lane the words and
+// the operations are those of the separate sampler, so the result is the
+// same bit for bit (f64: the oracle's rtwo_sphere_random /
+// rtwo_cosine_hemisphere).
+template <typename R>
+__device__ __forceinline__ V3<R> mixture_direction(bool to_light, const Onb<R>& uvw, V3<R> c, R radius, V3<R> o,
+                                                   Rng& g) {
+    V3<R> fu = uvw.u, fv = uvw.v, fw = uvw.w;
+    R q = (R)0;   // light: r^2 / distance^2
+    if (to_light) {
+        const V3<R> direction = c - o;
+        const R distance = P<R>::sqrt_(dot(direction, direction));
+        const Onb<R> lf(direction);
+        fu = lf.u;
+        fv = lf.v;
+        fw = lf.w;
+        if constexpr (sizeof(R) == 4) q = radius * radius * __builtin_amdgcn_rcpf(distance * distance);
+        else q = P<R>::div_(radius * radius, distance * distance);
+    }
+    const R r1 = P<R>::u_std(g.next());
+    const R r2 = P<R>::u_std(g.next());
+    R s, cph;
+    P<R>::sincos_2pi(to_light ? r2 : r1, &s, &cph);
+    const R t = P<R>::sqrt_((R)1 - (to_light ? q : r2));   // light: sqrt(1 - r^2/d^2); cosine: z
+    R z, sxy;
+    if constexpr (sizeof(R) == 4) {
+        // light: w = 1 - z = r1 (1 - cos_max), 1 - z^2 = w (2 - w) (see sphere_random)
+        const float w = r1 * (q * __builtin_amdgcn_rcpf(1.f + t));
+        z = to_light ? 1.f - w : t;
+        sxy = __builtin_amdgcn_sqrtf(to_light ? w * (2.f - w) : r2);
+    } else {
+        z = to_light ? (R)1 + r1 * (t - (R)1) : t;
+        sxy = P<R>::sqrt_(to_light ? (R)1 - z * z : r2);
+    }
+    const V3<R> x = mk(cph * sxy, s * sxy, z);
+    V3<R> acc = mk<R>(0, 0, 0);   // Onb::transform's fold
+    acc = acc + fu * x.x;
+    acc = acc + fv * x.y;
+    acc = acc + fw * x.z;
+    return acc;
+}
+
 // ---------------------------------------------------------------------------
 // Quad (quadrilateral.rs), on the staged record Q (rtw_kernels.h kQuadR):
 // Q[0..2] q, [3..5] u, [6..8] v, [9..11] w, [12..14] unit normal, [15] area.

@@ -5,6 +5,13 @@ GPU (each rank's share rendered in turn with rtw_render_device(rank, nranks)):
 the compute part of the strong-scaling curve the driver's N-GPU bench measures
 (it adds the barrier and the one RCCL gather).  Prints one JSON line per N.
 
+Per rank: the first render of a split ("cold": the 2-spp pilot render that
+orders the tasks + the task table + the render) and the best of --reps
+steady renders.  Per N the projected frame time adds, for N > 1, an estimate
+of the one gather of the packed tiles to rank 0 (each rank's buffer over its
+own xGMI link in parallel: 25 us + bytes / 50 GB/s, a conservative share of a
+link's ~153 GB/s) and the measured device assemble of N buffers on rank 0.
+
     python tools/rank_split_time.py [--ns 1,2,4,8] [--reps 3]
 """
 import argparse
@@ -43,11 +50,17 @@ def main():
     if W * H * SPP <= 2_000_000_000:
         r.render_device(cam, 1, buf.data_ptr(), buf.numel() * 4)     # warm-up
     torch.cuda.synchronize()
-    base = None
+    base = base_cold = base_frame = None
     for n in (int(x) for x in a.ns.split(",")):
-        per_rank, kern, rend = [], [], []
+        per_rank, kern, rend, cold = [], [], [], []
         only = [int(x) for x in a.ranks.split(",")] if a.ranks else range(n)
         for rank in only:
+            r.set_scene(scene)   # drops the cached task order: the next render runs its pilot
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            r.render_device(cam, 7, buf.data_ptr(), buf.numel() * 4, rank=rank, nranks=n)   # pilot + render
+            torch.cuda.synchronize()
+            cold.append((time.perf_counter() - t0) * 1e3)
             best = float("inf")
             for _ in range(a.reps):
                 torch.cuda.synchronize()
@@ -62,8 +75,29 @@ def main():
         slowest = max(per_rank)
         base = base or slowest
         st = r.get_stats()
+        # the gather + device assemble of the N packed buffers (rank 0)
+        nbytes = rtw.tiles_for_rank(W, H, 0, n) * 64 * 3 * 4
+        gather_ms = 0.0 if n == 1 else (25e-6 + nbytes / 50e9) * 1e3
+        ranks_buf = torch.zeros((n, rtw.tiles_for_rank(W, H, 0, n) * 64 * 3), dtype=torch.float32, device="cuda:0")
+        img = torch.empty((H, W, 3), dtype=torch.float32, device="cuda:0")
+        r.assemble_tiles(ranks_buf.data_ptr(), ranks_buf.stride(0) * 4, n, W, H, img.data_ptr())
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(5):
+            r.assemble_tiles(ranks_buf.data_ptr(), ranks_buf.stride(0) * 4, n, W, H, img.data_ptr())
+        torch.cuda.synchronize()
+        assemble_ms = (time.perf_counter() - t0) / 5 * 1e3
+        frame = slowest + gather_ms + assemble_ms
+        frame_cold = max(cold) + gather_ms + assemble_ms
+        base_frame = base_frame if n != 1 else frame
+        base_cold = base_cold or frame_cold
         print(json.dumps({"size": a.size, "spp": SPP, "tuning": a.tuning, "nranks": n, "ranks": list(only),
                           "chunk": int(st.chunk), "max_rank_ms": round(slowest, 2), "min_rank_ms": round(min(per_rank), 2),
+                          "max_rank_cold_ms": round(max(cold), 2), "gather_est_ms": round(gather_ms, 3),
+                          "gather_bytes_per_rank": nbytes, "assemble_ms": round(assemble_ms, 3),
+                          "frame_ms": round(frame, 2), "frame_cold_ms": round(frame_cold, 2),
+                          "speedup_frame_vs_1": round(base_frame / frame, 2) if base_frame and not a.ranks else None,
+                          "speedup_cold_vs_1": round(base_cold / frame_cold, 2),
                           "speedup_vs_1": round(base / slowest, 2), "max_rank_launch_ms": round(max(kern), 2),
                           "max_rank_render_kernel_ms": round(max(rend), 2),
                           "msamples_s_if_parallel": round(W * H * SPP / (slowest * 1e-3) / 1e6, 1),
