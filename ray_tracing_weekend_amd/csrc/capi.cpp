@@ -7,6 +7,8 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdlib>
 #include <new>
 #include <type_traits>
 #include <string>
@@ -968,10 +970,16 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
         const bool same = c->lpt_valid && c->lpt_serial == c->scene_serial && c->lpt_rank == rank &&
                           c->lpt_nranks == nranks && c->lpt_prec == (uint32_t)sizeof(R) &&
                           memcmp(&c->lpt_cam, cam, sizeof *cam) == 0;
+        const bool dbg = getenv("RTW_DEBUG_LPT") != nullptr;   // cold-render cost breakdown (stderr)
+        auto now = [] { return std::chrono::steady_clock::now(); };
+        auto t0 = now();
         if (!same) {
             c->lpt_valid = false;
             c->lpt_tab_valid = false;
             rc = lpt_pilot(c, p, world, launch_lds, stream);
+            if (dbg) fprintf(stderr, "lpt pilot %.3f ms (%u tiles)\n",
+                             std::chrono::duration<double, std::milli>(now() - t0).count(), p.n_local_tiles);
+            t0 = now();
             if (rc) return rc;
             c->lpt_valid = true;
             c->lpt_cam = *cam;
@@ -987,6 +995,8 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
             c->lpt_tab_valid = false;
             rc = lpt_tasks(c, p, c->group ? p.group : 0u, target, stream);
             if (rc) return rc;
+            if (dbg) fprintf(stderr, "lpt tasks %.3f ms (%zu tasks)\n",
+                             std::chrono::duration<double, std::milli>(now() - t0).count(), c->h_lpt_tasks.size() / 2);
             c->lpt_tab_valid = true;
             c->lpt_tab_chunks = p.n_chunks;
             c->lpt_tab_group = c->group;

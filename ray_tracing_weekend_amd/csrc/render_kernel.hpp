@@ -1257,6 +1257,45 @@ __device__ __forceinline__ V3<double> dielectric_dir64(V3<double> u, V3<double> 
     const double q = -__builtin_sqrt(1.0 - (px * px + py * py + pz * pz));
     return V3<double>{px + n.x * q, py + n.y * q, pz + n.z * q};
 }
+// Metal::scatter and Dialectric::scatter for an f64 sphere hit (kOptHit64)
+// in one pass: both start from the unit incoming direction u, its dot with
+// the normal and the mirror direction (vec.rs reflect); Metal perturbs it by
+// fuzz * UnitSphere (drawn first, as in the separate path), Dialectric keeps
+// it on total internal reflection or a Schlick draw and refracts otherwise.
+// The lanes of a wave that hit either material run it together.  Per lane
+// the draws and operations are metal_dir64's / dielectric_dir64's:
+// Dialectric's cos_theta = min(u . -n, 1) is min(-(u . n), 1) bit for bit
+// (negation is exact and round-to-nearest symmetric).
+__device__ __forceinline__ V3<double> specular_dir64(bool metal, V3<double> d, V3<double> n, bool front,
+                                                     const R4<double>& M, Rng& g, bool& keep) {
+#pragma clang fp contract(off)
+    V3<double> us = {0.0, 0.0, 0.0};
+    if (metal) us = dither64(unit_sphere<float>(g));
+    const V3<double> u = unit64(d);
+    const double vn = u.x * n.x + u.y * n.y + u.z * n.z;
+    const V3<double> r = {u.x - (n.x * 2.0) * vn, u.y - (n.y * 2.0) * vn, u.z - (n.z * 2.0) * vn};
+    keep = true;
+    if (metal) {
+        const double fuzz = M.w;
+        const V3<double> out = {r.x + us.x * fuzz, r.y + us.y * fuzz, r.z + us.z * fuzz};
+        keep = out.x * n.x + out.y * n.y + out.z * n.z > 0.0;
+        return out;
+    }
+    const double ratio = front ? M.x : M.w;
+    const double cos_t = __builtin_fmin(-vn, 1.0);
+    const double sin_t = __builtin_sqrt(1.0 - cos_t * cos_t);
+    bool refl = ratio * sin_t > 1.0;
+    if (!refl) {
+        const double r0 = front ? M.y : M.z;   // Dialectric::reflectance, powi(5) as LLVM expands it
+        const double x = 1.0 - cos_t, x2 = x * x;
+        refl = r0 + (1.0 - r0) * (x * (x2 * x2)) > P<double>::u_open01(g.next());
+    }
+    if (refl) return r;
+    // refract(v, n, eta), vec.rs: perp = (v + n cos) eta, par = n * -sqrt(1 - perp.perp)
+    const double px = (u.x + n.x * cos_t) * ratio, py = (u.y + n.y * cos_t) * ratio, pz = (u.z + n.z * cos_t) * ratio;
+    const double q = -__builtin_sqrt(1.0 - (px * px + py * py + pz * pz));
+    return V3<double>{px + n.x * q, py + n.y * q, pz + n.z * q};
+}
 // the outward normal (p - c) / radius, sphere.rs:82-83 (f64, no FMA)
 __device__ __forceinline__ V3<double> sphere_normal64(V3<double> p, const R4<double>& S) {
 #pragma clang fp contract(off)
@@ -1723,7 +1762,11 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     // subtree stealing (while-while kernels): this wave's result slots and
     // rendezvous bytes, after the workgroup's traversal stacks
-    constexpr bool kSteal = RTW_STEAL && (kWorld == kWorldBvhWW || kWorld == kWorldBvhLds);
+    // only for trees held in LDS: on large trees (C3, C5 from L2 / MALL) the
+    // subtrees idle lanes take early are mostly culled later by the owner's
+    // closest hit (C5: 9.6 -> 18.4 node visits per segment), and the steady
+    // state loses more than the lanes gain (C3 852 -> 875 ms, C5 1536 -> 1751)
+    constexpr bool kSteal = RTW_STEAL && kWorld == kWorldBvhLds;
     unsigned char* const steal_area =
         smem + (size_t)kWavesPerBlock * p.stack * 64 * sizeof(int32_t) + wave * kStealLdsPerWave<R>;
     // the wave's current task (wave-uniform): local tile lt = global 8x8 tile
@@ -2097,24 +2140,30 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                         colour = tex_colour(p.sc, p.sc.mat_tex[m], hu, hv, pnt);
                 }
                 const V3<R> emitted = mtype == kMatDiffuseLight ? colour : zero;
-                if (mtype == kMatMetal) {
+                if (kHit64 && sph_hit) {
+                    // Metal / Dielectric sphere: the f64 scatter of both in one pass
+                    RTW_PROBE_LANES(7);
+                    const bool metal = mtype == kMatMetal;
+                    bool keep;
+                    RTW_PROBE_SCATTER64(specular_dir64(metal, d64, n64, front, p.sc.mat64[m], g2, keep2).y);
+                    d64 = specular_dir64(metal, d64, n64, front, p.sc.mat64[m], g, keep);
+                    if (!keep) {
+                        col = mult * emitted + res;
+                        done = true;
+                    } else {
+                        if (metal) mult = mult * mk(mp.x, mp.y, mp.z);   // Reflect, camera.rs:488-500
+                        o = pnt;                          // (Dielectric: mult * (1, 1, 1) = mult)
+                        self_s = next_self;
+                        self_iso = next_iso;
+                        o64 = pnt64;
+                        d = from64<R>(d64);
+                    }
+                } else if (mtype == kMatMetal) {
                     RTW_PROBE_LANES(7);
                     // Metal::scatter, material.rs:407-421
-                    V3<R> dir;
-                    bool keep;
-                    if (kHit64 && sph_hit) {
-                        const V3<R> us = unit_sphere<R>(g);
-                        const double fuzz64 = p.sc.mat64[m].w;
-                        RTW_PROBE_SCATTER64(metal_dir64(unit64(d64), n64, fuzz64, dither64(us), keep2).y);
-                        d64 = metal_dir64(unit64(d64), n64, fuzz64, dither64(us), keep);
-                        dir = from64<R>(d64);
-                    } else {
-                        V3<R> refl = reflect(PR::normalize(d), nrm);
-                        dir = refl + unit_sphere<R>(g) * mp.w;
-                        keep = dot(dir, nrm) > (R)0;
-                        if constexpr (kHit64) d64 = dither64(dir);
-                    }
-                    if (!keep) {
+                    V3<R> refl = reflect(PR::normalize(d), nrm);
+                    const V3<R> dir = refl + unit_sphere<R>(g) * mp.w;
+                    if (!(dot(dir, nrm) > (R)0)) {
                         col = mult * emitted + res;
                         done = true;
                     } else {
@@ -2122,30 +2171,26 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                         o = pnt;
                         self_s = next_self;
                         self_iso = next_iso;
-                        if constexpr (kHit64) o64 = pnt64;
+                        if constexpr (kHit64) {
+                            o64 = pnt64;
+                            d64 = dither64(dir);
+                        }
                         d = dir;
                     }
                 } else if (mtype == kMatDielectric) {
                     RTW_PROBE_LANES(8);
                     // Dialectric::scatter, material.rs:458-487
                     V3<R> dir;
-                    if (kHit64 && sph_hit) {
-                        const R4<double> m64 = p.sc.mat64[m];
-                        RTW_PROBE_SCATTER64(dielectric_dir64(unit64(d64), n64, !front, m64, g2).y);
-                        d64 = dielectric_dir64(unit64(d64), n64, front, m64, g);
-                        dir = from64<R>(d64);
-                    } else {
-                        R ratio = front ? PR::div_((R)1, mp.w) : mp.w;
-                        V3<R> unit = PR::normalize(d);
-                        R cos_t = PR::min_(dot(unit, -nrm), (R)1);
-                        R sin_t = PR::sqrt_((R)1 - cos_t * cos_t);
-                        bool cannot = ratio * sin_t > (R)1;
-                        if (cannot || reflectance(cos_t, ratio) > PR::u_open01(g.next()))
-                            dir = reflect(unit, nrm);
-                        else
-                            dir = refract(unit, nrm, ratio);
-                        if constexpr (kHit64) d64 = dither64(dir);
-                    }
+                    R ratio = front ? PR::div_((R)1, mp.w) : mp.w;
+                    V3<R> unit = PR::normalize(d);
+                    R cos_t = PR::min_(dot(unit, -nrm), (R)1);
+                    R sin_t = PR::sqrt_((R)1 - cos_t * cos_t);
+                    bool cannot = ratio * sin_t > (R)1;
+                    if (cannot || reflectance(cos_t, ratio) > PR::u_open01(g.next()))
+                        dir = reflect(unit, nrm);
+                    else
+                        dir = refract(unit, nrm, ratio);
+                    if constexpr (kHit64) d64 = dither64(dir);
                     // mult * Colour(1, 1, 1) is the identity on every value
                     o = pnt;
                     self_s = next_self;
