@@ -271,9 +271,10 @@ def mode_line(scene, cam, precision, tuning, steps, warmup, dev):
 def cold_render(scene, cam, prec, dev):
     """One render of the headline workload by a fresh context, timed alone
     (host clock, device synced on both sides): what a one-shot
-    Camera::render pays on top of the steady state -- the 2-spp pilot render
-    that orders the tasks, the task table, the work buffers.  The scene
-    upload is excluded, as in the metric."""
+    Camera::render pays on top of the steady state: the work buffers, and the
+    tile index order instead of longest tiles first (this first render counts
+    the tile costs that order the next render's tasks; no separate pilot).
+    The scene upload is excluded, as in the metric."""
     tdtype = torch.float32 if prec == rtw.RTW_F32 else torch.float64
     with rtw.Renderer(device=dev.index, precision=prec) as r:
         r.set_scene(scene)
@@ -287,7 +288,7 @@ def cold_render(scene, cam, prec, dev):
         render_ms, _ = r.get_timings(1)
     return {"ms": round(dt * 1e3, 3), "value": round(W * H * SPP / dt / 1e6, 3), "unit": "Msamples/s",
             "render_kernel_ms": round(float(render_ms[0]), 3) if render_ms else None,
-            "includes": "pilot render (2 spp) + task table + work-buffer allocation + render + fold"}
+            "includes": "work-buffer allocation + render in tile index order (counting the tile costs) + fold"}
 
 
 def run_steps(step, steps, warmup, dist, sync, device=None):

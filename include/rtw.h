@@ -198,12 +198,17 @@ int rtw_set_accel(rtw_ctx *ctx, int accel);
  * "robust" (f32 ray-sphere tests in closest-approach form: 1 on, 0 off,
  * 2 = by the scene's distance-to-radius ratio, the default),
  * "item_order" (wave item pool: 1 = sample-major, the default; 0 = pixel-major),
- * "lpt" (longest tiles first: a blocking 2-spp pilot render of the rank's tiles
- * counts each tile's segments and orders the tasks by it, cached until the scene,
- * camera or rank split changes; 1 = for worlds held in LDS or of at most 4 MiB
- * (an XCD's L2), the default, 2 = for
- * every world, 0 = tiles in index order),
- * "lpt_min_spp" (renders of fewer samples per pixel skip the pilot, default 32),
+ * "lpt" (longest tiles first: the segments of each pixel's first 2 samples,
+ * summed per tile, order the tasks, cached until the scene, camera or rank split
+ * changes; 1 = for worlds held in LDS or of at most 4 MiB (an XCD's L2), the
+ * default, 2 = for every world, 0 = tiles in index order),
+ * "lpt_inline" (1 = the default: the first render of a scene / camera / split
+ * runs in tile index order and counts those segments itself, the next render
+ * reads them back (waiting for it once) and takes the ordered tasks; 0 = a
+ * blocking 2-spp pilot render before the first render),
+ * "lpt_pilot_spp" (samples per pixel counted, default 2), "lpt_pilot_depth" (the
+ * separate pilot's max depth, 0 = the camera's),
+ * "lpt_min_spp" (renders of fewer samples per pixel keep the index order, default 32),
  * "bvh_leaf" (spheres per BVH leaf, 1..15; 0 = auto, the default: 4, or 8 for
  * scenes of >= 100k spheres; takes effect at the
  * next rtw_set_scene), "light_bvh_min" (light lists this long or longer take the light grid
@@ -243,8 +248,9 @@ int rtw_render(rtw_ctx *ctx, const rtw_camera *cam, const rtw_scene *scene,
  * d_out may be NULL when the rank has no tiles.  Asynchronous on `stream`
  * (a hipStream_t; NULL = the context's own stream).  No host synchronisation
  * inside, except once per (scene, camera, rank split) when tuning "lpt" is on
- * and spp >= "lpt_min_spp": the pilot render whose tile costs order the tasks
- * is read back (a 2-spp render of the rank's tiles, then cached). */
+ * and spp >= "lpt_min_spp": the second render of the key waits for the first,
+ * whose tile costs order its tasks, and reads them back (then cached; with
+ * "lpt_inline" 0 the first render runs and reads back a 2-spp pilot instead). */
 int rtw_render_device(rtw_ctx *ctx, const rtw_camera *cam, uint64_t seed,
                       uint32_t rank, uint32_t nranks, void *d_out, size_t out_bytes,
                       void *stream);

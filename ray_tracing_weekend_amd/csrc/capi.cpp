@@ -55,6 +55,11 @@ struct rtw_ctx {
                                       // per-tile segment counts (cached per scene / camera / split);
                                       // 1: for worlds in LDS or within an L2, 2: always, 0: never
     uint32_t lpt_min_spp = 32;        // ... for renders of at least this many samples per pixel
+    uint32_t lpt_inline = 1;          // 1: no separate pilot -- the first render of a (scene,
+                                      // camera, split) runs in the plain tile order and counts the
+                                      // segments of each pixel's first lpt_pilot_spp samples; the
+                                      // renders after it take the task list of those counts
+                                      // 0: a pilot render before the first render
     uint32_t lpt_pilot_spp = 2;       // the pilot render: samples per pixel
     uint32_t lpt_pilot_depth = 0;     // ... and its max depth (0: the camera's); a path's segments
                                       // run one after another, so the pilot lasts as long as its
@@ -91,6 +96,8 @@ struct rtw_ctx {
     void* d_lpt = nullptr;            // pilot: [tile cost | chunk sums | tiles]
     size_t lpt_cap = 0;
     bool lpt_valid = false;           // h_lpt_cost is the pilot of (lpt_cam, lpt_serial, rank split, precision)
+    bool lpt_pending = false;         // ... still on the device: counted by the render before (lpt_ev)
+    hipEvent_t lpt_ev = nullptr;
     rtw_camera lpt_cam{};
     uint64_t lpt_serial = 0;
     uint32_t lpt_rank = 0, lpt_nranks = 0, lpt_prec = 0;
@@ -779,6 +786,7 @@ int lpt_pilot(rtw_ctx* c, const rtw::KParams<R>& p, int world, size_t launch_lds
     R* d_pout = d_part + (size_t)q.n_chunks * nt * 64 * 3;
     q.partial = d_part;
     q.tile_cost = d_cost;
+    q.cost_spp = q.spp;
     HIP_TRY(c, hipMemsetAsync(d_cost, 0, (size_t)nt * sizeof(uint32_t), stream));
     HIP_TRY(c, hipMemsetAsync(c->d_counters, 0, rtw_ctx::kCounters * sizeof(unsigned long long), stream));
     int lrc;
@@ -960,6 +968,7 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
     p.hit64 = c->hit64 ? 1u : 0u;
     p.task_table = nullptr;
     p.tile_cost = nullptr;
+    p.cost_spp = 0;
     // Reordering the tiles scatters the tiles in flight over the image: a tree
     // larger than an XCD's L2 (4 MiB) loses its locality (C5, 1M spheres,
     // ~100 MB: +8 %), so by default only worlds held in LDS or small enough
@@ -967,14 +976,33 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
     const bool on_chip = world == rtw::kWorldBvhLds || world == rtw::kWorldLds || c->tree_bytes <= (4u << 20);
     if ((c->lpt == 2 || (c->lpt == 1 && on_chip)) && need_out && p.spp >= std::max(c->lpt_min_spp, 1u) &&
         p.max_depth && p.n_local_tiles > 1 && p.n_chunks < (1u << 20)) {
-        const bool same = c->lpt_valid && c->lpt_serial == c->scene_serial && c->lpt_rank == rank &&
-                          c->lpt_nranks == nranks && c->lpt_prec == (uint32_t)sizeof(R) &&
+        const bool same = (c->lpt_valid || c->lpt_pending) && c->lpt_serial == c->scene_serial &&
+                          c->lpt_rank == rank && c->lpt_nranks == nranks && c->lpt_prec == (uint32_t)sizeof(R) &&
                           memcmp(&c->lpt_cam, cam, sizeof *cam) == 0;
         const bool dbg = getenv("RTW_DEBUG_LPT") != nullptr;   // cold-render cost breakdown (stderr)
         auto now = [] { return std::chrono::steady_clock::now(); };
         auto t0 = now();
-        if (!same) {
-            c->lpt_valid = false;
+        auto keep_key = [&] {
+            c->lpt_cam = *cam;
+            c->lpt_serial = c->scene_serial;
+            c->lpt_rank = rank;
+            c->lpt_nranks = nranks;
+            c->lpt_prec = (uint32_t)sizeof(R);
+        };
+        if (!same && c->lpt_inline) {
+            // this render counts its tiles' costs on the way (plain tile order)
+            c->lpt_valid = c->lpt_pending = false;
+            c->lpt_tab_valid = false;
+            const uint32_t nt = p.n_local_tiles;
+            rc = ensure(c, &c->d_lpt, &c->lpt_cap, align_up((size_t)nt, 64) * sizeof(uint32_t));
+            if (rc) return rc;
+            HIP_TRY(c, hipMemsetAsync(c->d_lpt, 0, (size_t)nt * sizeof(uint32_t), stream));
+            p.tile_cost = reinterpret_cast<uint32_t*>(c->d_lpt);
+            p.cost_spp = std::min(p.spp, std::max(c->lpt_pilot_spp, 1u));
+            keep_key();
+            c->lpt_pending = true;   // read back by the next render of the same key (after lpt_ev)
+        } else if (!same) {
+            c->lpt_valid = c->lpt_pending = false;
             c->lpt_tab_valid = false;
             rc = lpt_pilot(c, p, world, launch_lds, stream);
             if (dbg) fprintf(stderr, "lpt pilot %.3f ms (%u tiles)\n",
@@ -982,16 +1010,23 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
             t0 = now();
             if (rc) return rc;
             c->lpt_valid = true;
-            c->lpt_cam = *cam;
-            c->lpt_serial = c->scene_serial;
-            c->lpt_rank = rank;
-            c->lpt_nranks = nranks;
-            c->lpt_prec = (uint32_t)sizeof(R);
+            keep_key();
             HIP_TRY(c, hipMemsetAsync(c->d_counters, 0, rtw_ctx::kCounters * sizeof(unsigned long long), stream));
+        } else if (c->lpt_pending) {
+            // the counts of the render before (waits for it: once per key)
+            const uint32_t nt = p.n_local_tiles;
+            HIP_TRY(c, hipEventSynchronize(c->lpt_ev));
+            c->h_lpt_cost.resize(nt);
+            HIP_TRY(c, hipMemcpy(c->h_lpt_cost.data(), c->d_lpt, (size_t)nt * sizeof(uint32_t), hipMemcpyDeviceToHost));
+            c->lpt_pending = false;
+            c->lpt_valid = true;
+            if (dbg) fprintf(stderr, "lpt counts read back %.3f ms (%u tiles)\n",
+                             std::chrono::duration<double, std::milli>(now() - t0).count(), nt);
+            t0 = now();
         }
         const uint64_t target = c->target_tasks ? c->target_tasks : kAutoTasks;
-        if (!c->lpt_tab_valid || c->lpt_tab_chunks != p.n_chunks || c->lpt_tab_group != c->group ||
-            c->lpt_tab_target != target) {
+        if (c->lpt_valid && (!c->lpt_tab_valid || c->lpt_tab_chunks != p.n_chunks || c->lpt_tab_group != c->group ||
+            c->lpt_tab_target != target)) {
             c->lpt_tab_valid = false;
             rc = lpt_tasks(c, p, c->group ? p.group : 0u, target, stream);
             if (rc) return rc;
@@ -1002,8 +1037,10 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
             c->lpt_tab_group = c->group;
             c->lpt_tab_target = target;
         }
-        p.task_table = reinterpret_cast<const uint32_t*>(c->d_lpt_tasks);
-        p.n_tasks = (uint32_t)(c->h_lpt_tasks.size() / 2);
+        if (c->lpt_valid) {
+            p.task_table = reinterpret_cast<const uint32_t*>(c->d_lpt_tasks);
+            p.n_tasks = (uint32_t)(c->h_lpt_tasks.size() / 2);
+        }
     }
     hipEvent_t* ev = c->ring[c->n_renders % rtw_ctx::kRing];
     HIP_TRY(c, hipEventRecord(c->ev0, stream));
@@ -1022,6 +1059,10 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
     }
     if (lrc < 0) return fail(c, RTW_E_DEVICE, std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
     c->last_variant = lrc;
+    if (p.tile_cost) {   // the counts are complete after this render
+        if (!c->lpt_ev) HIP_TRY(c, hipEventCreateWithFlags(&c->lpt_ev, hipEventDisableTiming));
+        HIP_TRY(c, hipEventRecord(c->lpt_ev, stream));
+    }
     HIP_TRY(c, hipEventRecord(c->ev1, stream));
     HIP_TRY(c, hipEventRecord(ev[2], stream));
     ++c->n_renders;
@@ -1077,6 +1118,7 @@ void rtw_destroy(rtw_ctx* c) {
     if (c->d_counters) (void)hipFree(c->d_counters);
     if (c->d_lpt) (void)hipFree(c->d_lpt);
     if (c->d_lpt_tasks) (void)hipFree(c->d_lpt_tasks);
+    if (c->lpt_ev) (void)hipEventDestroy(c->lpt_ev);
     for (auto& tri : c->ring)
         for (auto& e : tri)
             if (e) (void)hipEventDestroy(e);
@@ -1109,6 +1151,7 @@ int rtw_set_tuning(rtw_ctx* c, const char* key, int64_t value) {
     else if (k == "hit64") c->hit64 = value ? 1u : 0u;
     else if (k == "lpt") c->lpt = (uint32_t)std::min<int64_t>(value, 2);
     else if (k == "lpt_min_spp") c->lpt_min_spp = (uint32_t)std::min<int64_t>(value, 1u << 30);
+    else if (k == "lpt_inline") c->lpt_inline = value ? 1u : 0u;
     else if (k == "lpt_pilot_spp") c->lpt_pilot_spp = (uint32_t)std::min<int64_t>(std::max<int64_t>(value, 1), 64);
     else if (k == "lpt_pilot_depth") c->lpt_pilot_depth = (uint32_t)std::min<int64_t>(value, 1u << 20);
     else if (k == "light_bvh_min") c->light_bvh_min = (uint32_t)std::min<int64_t>(value, 1u << 30);

@@ -59,7 +59,8 @@ int main(int argc, char** argv) {
         std::string s = argv[a];
         if (s == "--debug") continue;  // render_debug == render on the GPU
         else if (s == "--seed" && a + 1 < argc) opt.seed = strtoull(argv[++a], nullptr, 0);
-        else if (s == "--f64") opt.precision = RTW_F64;
+        else if (s == "--f64") opt.precision = RTW_F64;   // (the default)
+        else if (s == "--f32") opt.precision = RTW_F32;   // the speed mode
         else if (s == "--device" && a + 1 < argc) opt.device = atoi(argv[++a]);
         else if (s == "--config" && a + 1 < argc) config = argv[++a];
         else if (s == "--out" && a + 1 < argc) out = argv[++a];

@@ -209,7 +209,7 @@ class CameraBuilder {
 struct RenderOptions {
     uint64_t seed = 0x5EED0001ULL;  // the reference seeds from thread_rng (non-deterministic)
     int device = 0;
-    int precision = RTW_F32;
+    int precision = RTW_F64;        // the parity mode (the reference's sums); RTW_F32: the speed mode
     int accel = RTW_ACCEL_AUTO;
 };
 

@@ -2295,14 +2295,15 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                 dst[0] = part.x;
                 dst[1] = part.y;
                 dst[2] = part.z;
+                if (p.tile_cost) {   // tile costs for the task order: this sample's segments
+                    if (s < p.cost_spp) atomicAdd(p.tile_cost + my_lt, p.max_depth - depth + 1u);
+                }
                 ++s;
                 if (s < s_end) {
                     RTW_PROBE_SEED();
                     start_sample();
                 RTW_PROBE_LANES(10);
                 } else {
-                    if (p.tile_cost)   // pilot render (chunk 1): this sample's segments
-                        atomicAdd(p.tile_cost + my_lt, p.max_depth - depth + 1u);
                     active = false;
                     need = true;
                 }

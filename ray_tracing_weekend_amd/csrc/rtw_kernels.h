@@ -205,7 +205,8 @@ struct KParams {
     const uint32_t* task_table;       // non-null: task t = {local tile, first chunk | chunks << 20}
                                       // at [2t, 2t + 1] (longest tiles first, sized by a pilot
                                       // render's costs); null: t = tile * n_groups + group
-    uint32_t* tile_cost;              // non-null (pilot render, chunk 1): += segments of each sample
+    uint32_t* tile_cost;              // non-null: [local tile] += segments of each sample s < cost_spp
+    uint32_t cost_spp;                //   (a pilot render, or the first render of a split)
 };
 
 // Host-side launch helpers (defined in render_f32.hip / render_f64.hip).

@@ -31,7 +31,11 @@ BVH_KIND_KERNEL = {0: K_BVH_LOOP, 1: K_BVH_WW, 2: K_BVH4, 3: K_BVH_LDS}
 LAST = {}
 
 
-def _render_gpu(soa, cam, seed, precision, chunk=0, accel=rtw.RTW_ACCEL_AUTO, bvh_kind=None, tuning=None):
+def _render_gpu(soa, cam, seed, precision, chunk=0, accel=rtw.RTW_ACCEL_AUTO, bvh_kind=None, tuning=None,
+                renders=1):
+    """renders > 1: the same render repeated by one context (with tuning "lpt"
+    the first counts the tile costs, the later ones take the ordered task
+    list); every repeat must give the first's image bit for bit."""
     with rtw.Renderer(device=0, precision=precision) as r:
         if chunk:
             r.set_chunk(chunk)
@@ -43,6 +47,9 @@ def _render_gpu(soa, cam, seed, precision, chunk=0, accel=rtw.RTW_ACCEL_AUTO, bv
         r.set_accel(accel)
         r.set_scene(soa)
         img = r.render(cam, seed)
+        for _ in range(renders - 1):
+            again = r.render(cam, seed)
+            assert _same(img, again)
         LAST["kernel"] = r.stats.kernel
         if bvh_kind is not None:
             # bvh_kind 3 falls back to 1 when the tree does not fit in LDS
@@ -705,9 +712,9 @@ def test_c2_full_frame_rank_split_is_the_single_render(nranks, lpt):
     """rtw_render_device over nranks (the multi-GPU tile interleave, DESIGN.md
     §7) + rtw_assemble_tiles reassembles the one-rank C2-size image bit for
     bit (f32).  Every render runs on torch's current stream, the stream the
-    buffers were filled on.  lpt: every render (each rank's share, then the
-    one-rank frame again) takes its tiles longest first, the order of its own
-    pilot render."""
+    buffers were filled on.  lpt: each rank's share and then the one-rank
+    frame again are rendered twice, the second time with its tiles longest
+    first, in the order of the tile costs the first render counted."""
     import torch
     soa, b = _scene()
     H, W = 800, 1200
@@ -724,11 +731,13 @@ def test_c2_full_frame_rank_split_is_the_single_render(nranks, lpt):
         per = rtw.tiles_for_rank(W, H, 0, nranks) * 64 * 3
         ranks = torch.zeros((nranks, per), dtype=torch.float32, device="cuda:0")
         for k in range(nranks):
-            r.render_device(cam, 109, ranks[k].data_ptr(), per * 4, rank=k, nranks=nranks, stream=s)
+            for _ in range(1 + lpt):   # lpt: the second render of a share takes its ordered task list
+                r.render_device(cam, 109, ranks[k].data_ptr(), per * 4, rank=k, nranks=nranks, stream=s)
         img = torch.empty_like(full)
         r.assemble_tiles(ranks.data_ptr(), per * 4, nranks, W, H, img.data_ptr(), stream=s)
         again = torch.zeros_like(one)
-        r.render_device(cam, 109, again.data_ptr(), again.numel() * 4, stream=s)
+        for _ in range(1 + lpt):
+            r.render_device(cam, 109, again.data_ptr(), again.numel() * 4, stream=s)
         torch.cuda.synchronize()
     assert torch.equal(torch.nan_to_num(img, nan=-7.0), torch.nan_to_num(full, nan=-7.0))
     assert torch.equal(torch.nan_to_num(again, nan=-7.0), torch.nan_to_num(one, nan=-7.0))
@@ -739,8 +748,9 @@ def test_scheduling_knobs_do_not_change_the_image(prec):
     """The wave item pool order (pixel- / sample-major), persistent waves (a
     few workgroups draining every task from the counter, or a resident grid) or
     one task per wave and the task size only move work between lanes, and the
-    longest-tiles-first task order (a pilot render's tile costs) only moves
-    tiles between tasks: same image bit for bit."""
+    longest-tiles-first task order (the tile costs the first render counts,
+    or a separate pilot render's) only moves tiles between tasks: same image
+    bit for bit."""
     soa, b = _scene()
     cam = b.with_image_width(40).with_image_height(24).with_samples_per_pixel(9).with_max_depth(50).build()
     base, _, cb = _render_gpu(soa, cam, 113, prec)
@@ -748,8 +758,9 @@ def test_scheduling_knobs_do_not_change_the_image(prec):
               {"persist": 0, "target_tasks": 1000}, {"item_order": 0, "target_tasks": 1000},
               {"persist": 5, "group": 3}, {"persist": 1, "group": 2},
               {"lpt_min_spp": 1}, {"lpt_min_spp": 1, "persist": 0}, {"lpt_min_spp": 1, "persist": 2, "group": 1},
-              {"lpt": 2, "lpt_min_spp": 1, "lds": 0}):
-        img, _, cv = _render_gpu(soa, cam, 113, prec, tuning=t)
+              {"lpt": 2, "lpt_min_spp": 1, "lds": 0}, {"lpt_min_spp": 1, "lpt_inline": 0},
+              {"lpt_min_spp": 1, "lpt_inline": 0, "lpt_pilot_depth": 3}):
+        img, _, cv = _render_gpu(soa, cam, 113, prec, tuning=t, renders=3 if "lpt_min_spp" in t else 1)
         assert _same(base, img) and cb == cv, t
 
 
@@ -764,5 +775,5 @@ def test_task_table_with_4096_chunk_groups_keeps_every_chunk():
     base, chunk, cb = _render_gpu(soa, cam, 131, rtw.RTW_F32, tuning={"lpt": 0})
     assert chunk == 1
     img, _, cv = _render_gpu(soa, cam, 131, rtw.RTW_F32,
-                             tuning={"group": 4096, "lpt_min_spp": 1, "chunk": 1})
+                             tuning={"group": 4096, "lpt_min_spp": 1, "chunk": 1}, renders=2)
     assert _same(base, img) and cb == cv

@@ -52,7 +52,7 @@ def main():
     torch.cuda.synchronize()
     base = base_cold = base_frame = None
     for n in (int(x) for x in a.ns.split(",")):
-        per_rank, kern, rend, cold = [], [], [], []
+        per_rank, kern, rend, cold, cold_rend = [], [], [], [], []
         only = [int(x) for x in a.ranks.split(",")] if a.ranks else range(n)
         for rank in only:
             r.set_scene(scene)   # drops the cached task order: the next render runs its pilot
@@ -61,6 +61,7 @@ def main():
             r.render_device(cam, 7, buf.data_ptr(), buf.numel() * 4, rank=rank, nranks=n)   # pilot + render
             torch.cuda.synchronize()
             cold.append((time.perf_counter() - t0) * 1e3)
+            cold_rend.append(r.get_timings(1)[0][0])   # the cold render's own kernel (pilot excluded)
             best = float("inf")
             for _ in range(a.reps):
                 torch.cuda.synchronize()
@@ -93,7 +94,8 @@ def main():
         base_cold = base_cold or frame_cold
         print(json.dumps({"size": a.size, "spp": SPP, "tuning": a.tuning, "nranks": n, "ranks": list(only),
                           "chunk": int(st.chunk), "max_rank_ms": round(slowest, 2), "min_rank_ms": round(min(per_rank), 2),
-                          "max_rank_cold_ms": round(max(cold), 2), "gather_est_ms": round(gather_ms, 3),
+                          "max_rank_cold_ms": round(max(cold), 2),
+                          "max_rank_cold_render_kernel_ms": round(max(cold_rend), 2), "gather_est_ms": round(gather_ms, 3),
                           "gather_bytes_per_rank": nbytes, "assemble_ms": round(assemble_ms, 3),
                           "frame_ms": round(frame, 2), "frame_cold_ms": round(frame_cold, 2),
                           "speedup_frame_vs_1": round(base_frame / frame, 2) if base_frame and not a.ranks else None,
