@@ -1849,6 +1849,12 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
     RTW_PROBE_WAVE_BEGIN();
 
     auto start_sample = [&]() {
+        // tile costs (p.tile_cost): the sample's work is the lane's counters at
+        // its end minus at its start -- subtracted here, added at the end (a
+        // u32 sum: exact modulo 2^32, no register kept)
+        if (p.tile_cost) {
+            if (s < p.cost_spp) atomicSub(p.tile_cost + my_lt, nvis + ntest);
+        }
         // Camera::get_ray, camera.rs:274-293 + ray_colour_call, camera.rs:439-457
         g.seed(p.seed, pix, s);
         R ox = PR::u_incl(g.next(), (R)-0.5, p.u_scale);
@@ -2295,8 +2301,9 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                 dst[0] = part.x;
                 dst[1] = part.y;
                 dst[2] = part.z;
-                if (p.tile_cost) {   // tile costs for the task order: this sample's segments
-                    if (s < p.cost_spp) atomicAdd(p.tile_cost + my_lt, p.max_depth - depth + 1u);
+                if (p.tile_cost) {   // tile costs for the task order: this sample's work
+                    if (s < p.cost_spp)
+                        atomicAdd(p.tile_cost + my_lt, nvis + ntest + kCostPerSegment * (p.max_depth - depth + 1u));
                 }
                 ++s;
                 if (s < s_end) {

@@ -209,6 +209,12 @@ struct KParams {
     uint32_t cost_spp;                //   (a pilot render, or the first render of a split)
 };
 
+// The cost of a sample for the task order (KParams::tile_cost): its BVH node
+// visits + sphere tests + this many per segment (a segment's hit record and
+// scatter, in node-visit units).  Segments alone miss C5's horizon tiles,
+// whose rays skim the sphere field through thousands of nodes per segment.
+constexpr uint32_t kCostPerSegment = 12;
+
 // Host-side launch helpers (defined in render_f32.hip / render_f64.hip).
 // world: a WorldMode; lds_bytes: dynamic LDS of the kWorldLds variant.
 // `mid` (may be null) is recorded on `stream` between the render kernel and

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Summarise rocprofv3 PMC csvs for the render kernel: per-dispatch averages
 over the full renders (a launch under a quarter of the largest one of a
-counter -- the 2-spp tile-cost pilot render -- is left out)."""
+counter -- a 2-spp tile-cost pilot render, tuning lpt_inline=0 -- is left out)."""
 import collections, csv, glob, sys
 root = sys.argv[1]
 agg = collections.defaultdict(list)

@@ -1,11 +1,13 @@
 #!/bin/bash
 # rocprofv3 on the bench workload: kernel-trace stats + separate PMC passes
 # (never combined with sys/runtime traces).  Usage: profile.sh TAG [bench args]
+# PROG=tools/bench_configs.py profiles that program instead of bench.py (C3 / C5).
 set -u
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 OUT="$ROOT/gpurun_out"; mkdir -p "$OUT"
 TAG="$1"; shift
 ARGS="${*:---steps 2 --warmup 1 --no-cpu-baseline}"
+PROG="$ROOT/${PROG:-bench.py}"
 export TMPDIR=/tmp
 cd /tmp
 bad() { case "$1" in 124|134|137|139) return 0;; *) return 1;; esac; }
@@ -13,7 +15,7 @@ if [ ! -f "$OUT/rocprof_counters.txt" ]; then
   timeout -k 10 120 rocprofv3 -L > "$OUT/rocprof_counters.txt" 2>&1; echo "list rc=$?"
 fi
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$TAG" -o trace --output-format csv \
-  -- python3 "$ROOT/bench.py" $ARGS > "$OUT/prof_${TAG}_trace.log" 2>&1
+  -- python3 "$PROG" $ARGS > "$OUT/prof_${TAG}_trace.log" 2>&1
 rc=$?; echo "trace rc=$rc"; if bad $rc; then exit $rc; fi
 # counter sets separated by ';' (PMC_SETS overrides the default list)
 SETS="${PMC_SETS:-FETCH_SIZE;WRITE_SIZE;SQ_WAVES SQ_INSTS_VALU SQ_THREAD_CYCLES_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY;SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE}"
@@ -22,7 +24,7 @@ IFS=';' read -ra SETLIST <<< "$SETS"
 for set in "${SETLIST[@]}"; do
   i=$((i+1))
   timeout -k 10 240 rocprofv3 --pmc $set -d "$OUT/prof_$TAG/pmc$i" -o pmc --output-format csv \
-    -- python3 "$ROOT/bench.py" $ARGS > "$OUT/prof_${TAG}_pmc$i.log" 2>&1
+    -- python3 "$PROG" $ARGS > "$OUT/prof_${TAG}_pmc$i.log" 2>&1
   rc=$?; echo "pmc$i ($set) rc=$rc"; if bad $rc; then exit $rc; fi
 done
 # per-launch means + the traffic / fractions file bench.py reads, stamped with

@@ -5,9 +5,10 @@ GPU (each rank's share rendered in turn with rtw_render_device(rank, nranks)):
 the compute part of the strong-scaling curve the driver's N-GPU bench measures
 (it adds the barrier and the one RCCL gather).  Prints one JSON line per N.
 
-Per rank: the first render of a split ("cold": the 2-spp pilot render that
-orders the tasks + the task table + the render) and the best of --reps
-steady renders.  Per N the projected frame time adds, for N > 1, an estimate
+Per rank: the first render of a split ("cold": tile index order while it
+counts the tile costs -- or, with tuning lpt_inline=0, a 2-spp pilot render
+first) and the best of --reps steady renders (longest tiles first; the first
+of them reads the counts back and builds the task table).  Per N the projected frame time adds, for N > 1, an estimate
 of the one gather of the packed tiles to rank 0 (each rank's buffer over its
 own xGMI link in parallel: 25 us + bytes / 50 GB/s, a conservative share of a
 link's ~153 GB/s) and the measured device assemble of N buffers on rank 0.
@@ -55,13 +56,13 @@ def main():
         per_rank, kern, rend, cold, cold_rend = [], [], [], [], []
         only = [int(x) for x in a.ranks.split(",")] if a.ranks else range(n)
         for rank in only:
-            r.set_scene(scene)   # drops the cached task order: the next render runs its pilot
+            r.set_scene(scene)   # drops the cached task order: the next render counts the tile costs
             torch.cuda.synchronize()
             t0 = time.perf_counter()
-            r.render_device(cam, 7, buf.data_ptr(), buf.numel() * 4, rank=rank, nranks=n)   # pilot + render
+            r.render_device(cam, 7, buf.data_ptr(), buf.numel() * 4, rank=rank, nranks=n)   # cold render
             torch.cuda.synchronize()
             cold.append((time.perf_counter() - t0) * 1e3)
-            cold_rend.append(r.get_timings(1)[0][0])   # the cold render's own kernel (pilot excluded)
+            cold_rend.append(r.get_timings(1)[0][0])   # the cold render's own kernel
             best = float("inf")
             for _ in range(a.reps):
                 torch.cuda.synchronize()

@@ -6,6 +6,7 @@ spread of wave start and end times, the idle tail, per-XCD end times.
 
     python tools/share_timeline.py build                  # here (hipcc cross-compiles)
     python tools/share_timeline.py run [--ns 1,8] [--rank K] [--tuning k=v,...]
+                                       [--config C5 --spp 64]   (a bench_configs scene)
 """
 import argparse
 import ctypes as C
@@ -42,7 +43,14 @@ def run(a):
     n_tl = 1 << 18
     buf_tl = (C.c_ulonglong * n_tl)()
     W, H, SPP = 1200, 800, 500
-    scene, b = rtw.scenes.simple_soa()
+    if a.config:
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        from bench_configs import CONFIGS, SEED
+        cfg = CONFIGS[a.config]
+        W, H, SPP = cfg["w"], cfg["h"], a.spp or cfg["spp"]
+        scene, b = rtw.scenes.simple_soa(SEED, cfg["n"])
+    else:
+        scene, b = rtw.scenes.simple_soa()
     cam = b.with_image_width(W).with_image_height(H).with_samples_per_pixel(SPP).with_max_depth(50).build()
     r = rtw.Renderer(precision=rtw.RTW_F32)
     for kv in filter(None, a.tuning.split(",")):
@@ -73,6 +81,9 @@ def run(a):
             "begin_us_p50_p99_max": [round(q(beg, 50), 1), round(q(beg, 99), 1), round(float(beg.max()), 1)],
             "end_ms_p1_p50_p90_p99_max": [round(q(end, p) / 1e3, 3) for p in (1, 50, 90, 99)] + [round(span / 1e3, 3)],
             "wave_occupancy": round(busy / (len(t) * span), 4),
+            # fraction of the waves still running at 10 %, 20 %, ... of the span
+            "alive_at_10pct_steps": [round(float(((beg <= f * span) & (end > f * span)).mean()), 3)
+                                     for f in np.arange(0.1, 1.0, 0.1)],
             "tasks_per_wave_p1_p50_p99": [int(q(t[:, 2], p)) for p in (1, 50, 99)],
             "xcc_end_ms": xcc,
             "last_tasks_of_the_10_last_waves": [int(x) for x in last_task[np.argsort(end)[-10:]]],
@@ -86,5 +97,7 @@ if __name__ == "__main__":
     ap.add_argument("--ns", default="1,8")
     ap.add_argument("--tuning", default="")
     ap.add_argument("--rank", type=int, default=0)
+    ap.add_argument("--config", default="", help="C3 / C5: a tools/bench_configs.py scene")
+    ap.add_argument("--spp", type=int, default=0)
     a = ap.parse_args()
     build() if a.mode == "build" else run(a)
