@@ -1776,21 +1776,33 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
     uint32_t lt = 0, tx = 0, ty = 0, c_begin = 0, glen = 0, n_items = 0;
     uint32_t glen_m = 0;          // glen > 1: ceil(2^32 / glen), q / glen = umulhi(q, glen_m) for q < 64 glen
                                   // (2^32 does not fit: glen == 1 is special-cased)
+    // The camera, the background and the task parameters are read where they
+    // are used (once per sample, miss or task), from the kernarg segment
+    // through an opaque pointer: held in SGPRs across the loop they overflow
+    // the SGPR file, and the compiler parks them in VGPR lanes and reads them
+    // back with v_readlane -- a VALU instruction each, every segment.
+    typedef const KParams<R> __attribute__((address_space(4))) KArgs;
+    auto kargs = []() {
+        const KArgs* k = (const KArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+        asm volatile("" : "+s"(k));   // not loop-invariant for the compiler: loaded at each use
+        return k;
+    };
     auto set_task = [&](uint32_t t) {
-        if (p.task_table) {   // longest tiles first, cut by cost
-            lt = p.task_table[2 * t];
-            const uint32_t e = p.task_table[2 * t + 1];
+        const KArgs* k = kargs();
+        if (k->task_table) {   // longest tiles first, cut by cost
+            lt = k->task_table[2 * t];
+            const uint32_t e = k->task_table[2 * t + 1];
             c_begin = e & 0xFFFFFu;
             glen = e >> 20;
         } else {
-            lt = t / p.n_groups;
-            const uint32_t cg = t - lt * p.n_groups;
-            c_begin = cg * p.group;
-            glen = min(c_begin + p.group, p.n_chunks) - c_begin;
+            lt = t / k->n_groups;
+            const uint32_t cg = t - lt * k->n_groups;
+            c_begin = cg * k->group;
+            glen = min(c_begin + k->group, k->n_chunks) - c_begin;
         }
-        const uint32_t T = lt * p.nranks + p.rank;
-        ty = T / p.tiles_x;
-        tx = T - ty * p.tiles_x;
+        const uint32_t T = lt * k->nranks + k->rank;
+        ty = T / k->tiles_x;
+        tx = T - ty * k->tiles_x;
         n_items = 64u * glen;
         glen_m = glen > 1 ? (uint32_t)((0xFFFFFFFFull + glen) / glen) : 0u;
     };
@@ -1820,8 +1832,6 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
         }
     };
 
-    const V3<R> center = v3of(p.center), p00 = v3of(p.p00), du = v3of(p.du), dv = v3of(p.dv);
-    const V3<R> bg = v3of(p.bg);
     const V3<R> zero = mk<R>(0, 0, 0);
     const R tmin = PR::kEps;
     const int32_t nplanes = (int32_t)p.sc.n_planes;
@@ -1849,21 +1859,25 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
     RTW_PROBE_WAVE_BEGIN();
 
     auto start_sample = [&]() {
-        // tile costs (p.tile_cost): the sample's work is the lane's counters at
+        const KArgs* k = kargs();
+        // tile costs (KParams::tile_cost): the sample's work is the lane's counters at
         // its end minus at its start -- subtracted here, added at the end (a
         // u32 sum: exact modulo 2^32, no register kept)
-        if (p.tile_cost) {
-            if (s < p.cost_spp) atomicSub(p.tile_cost + my_lt, nvis + ntest);
+        if (k->tile_cost) {
+            if (s < k->cost_spp) atomicSub(k->tile_cost + my_lt, nvis + ntest);
         }
         // Camera::get_ray, camera.rs:274-293 + ray_colour_call, camera.rs:439-457
-        g.seed(p.seed, pix, s);
-        R ox = PR::u_incl(g.next(), (R)-0.5, p.u_scale);
-        R oy = PR::u_incl(g.next(), (R)-0.5, p.u_scale);
-        V3<R> ps = (p00 + du * ((R)i + ox)) + dv * ((R)j + oy);
+        g.seed(k->seed, pix, s);
+        R ox = PR::u_incl(g.next(), (R)-0.5, k->u_scale);
+        R oy = PR::u_incl(g.next(), (R)-0.5, k->u_scale);
+        V3<R> ps = (mk(k->p00[0], k->p00[1], k->p00[2]) + mk(k->du[0], k->du[1], k->du[2]) * ((R)i + ox)) +
+                   mk(k->dv[0], k->dv[1], k->dv[2]) * ((R)j + oy);
+        const V3<R> center = mk(k->center[0], k->center[1], k->center[2]);
         V3<R> origin = center;
-        if (p.defocus) {
+        if (k->defocus) {
             V3<R> qd = unit_disk<R>(g);
-            origin = (center + v3of(p.disk_u) * qd.x) + v3of(p.disk_v) * qd.z;
+            origin = (center + mk(k->disk_u[0], k->disk_u[1], k->disk_u[2]) * qd.x) +
+                     mk(k->disk_v[0], k->disk_v[1], k->disk_v[2]) * qd.z;
         }
         o = origin;
         d = ps - origin;
@@ -1873,13 +1887,14 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
         }
         mult = mk<R>(1, 1, 1);
         res = zero;
-        depth = p.max_depth;
+        depth = k->max_depth;
         self_s = -1;
         self_iso = false;
     };
     // Give every lane that needs one a valid item: from the current pool, then
     // (p.persist) from the next task's; none once no task is left.
     auto acquire = [&]() {
+        const KArgs* k = kargs();
         for (;;) {
             const uint64_t want = __ballot(need);
             if (want == 0) break;
@@ -1888,10 +1903,10 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                 if (more) {
                     const uint64_t live = __ballot(true);
                     const uint32_t leader = (uint32_t)__builtin_ctzll(live);
-                    if (lane == leader) t = (uint32_t)atomicAdd(p.counters + 6, 1ull);
+                    if (lane == leader) t = (uint32_t)atomicAdd(k->counters + 6, 1ull);
                     t = (uint32_t)__shfl((int)t, (int)leader);
                 }
-                if (t >= p.n_tasks) {   // every task is taken: these lanes are done
+                if (t >= k->n_tasks) {   // every task is taken: these lanes are done
                     more = false;
                     need = false;
                     break;
@@ -1909,11 +1924,11 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                     decode(q, px, c);
                     i = tx * kTile + (px & 7u);
                     j = ty * kTile + (px >> 3);
-                    if (i < p.W && j < p.H) {
+                    if (i < k->W && j < k->H) {
                         my_lt = lt;
-                        pix = (uint64_t)j * p.W + i;
-                        s = c * p.chunk;
-                        s_end = min(s + p.chunk, p.spp);
+                        pix = (uint64_t)j * k->W + i;
+                        s = c * k->chunk;
+                        s_end = min(s + k->chunk, k->spp);
                         active = true;
                         need = false;
                         start_sample();
@@ -1943,7 +1958,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
             RTW_PROBE_PLANES();
             for (int32_t k = 0; k < nplanes; ++k) {
                 R t;
-                const R* pl = p.sc.planes + kPlaneR * k;
+                const R* pl = kargs()->sc.planes + kPlaneR * k;
                 const bool box_hit = aabb_hit_plane(pl + 6, pl + 9, o, d, tmin);
                 if (box_hit && plane_t(pl, o, d, tmin, t, p.counters + 4) &&
                     (best < 0 || t < tb)) {
@@ -1954,7 +1969,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
             // quads, each behind its own AABB (bounded_hit, hittable.rs:190-196)
             for (int32_t k = 0; kPrims && k < nquads; ++k) {
                 R t;
-                const R* Q = p.sc.quads + kQuadR * k;
+                const R* Q = kargs()->sc.quads + kQuadR * k;
                 if (aabb_hit_ref(Q + 16, Q + 19, o, d, tmin) && quad_t_hit(Q, o, d, tmin, (R)INFINITY, t) &&
                     (best < 0 || t < tb)) {
                     tb = t;
@@ -1962,11 +1977,11 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                 }
             }
             // transformed cuboids, each behind its world AABB
-            for (int32_t k = 0; kPrims && k < (int32_t)p.sc.n_boxes; ++k) {
+            for (int32_t k = 0; kPrims && k < (int32_t)kargs()->sc.n_boxes; ++k) {
                 R t;
                 int qd;
                 V3<R> o2, d2;
-                const R* B = p.sc.boxes + kBoxR * k;
+                const R* B = kargs()->sc.boxes + kBoxR * k;
                 if (aabb_hit_ref(B + kBoxLo, B + kBoxHi, o, d, tmin) &&
                     box_t_hit(B, o, d, tmin, (R)INFINITY, t, qd, o2, d2) && (best < 0 || t < tb)) {
                     tb = t;
@@ -1982,7 +1997,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                     RTW_PROBE_LANES(5);
                     ++ntest;
                     double ts;
-                    bool self_hit = sphere_t_ref64(p.sc.sph64[self_s], o64, d64, ts) && ts < tb64;
+                    bool self_hit = sphere_t_ref64(kargs()->sc.sph64[self_s], o64, d64, ts) && ts < tb64;
                     RTW_PROBE_ABL_SELF(self_hit, ts);
                     if (self_hit) {
                         tb64 = ts;
@@ -1999,7 +2014,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                     bvh_closest_excl_steal<kRobust>(scw, sbase, o, d, tmin, tb, best, stk_wave, lane, steal_area,
                                                     nvis, ntest, excl, skip);
                     if (!skip && best != prev && best >= sbase) {
-                        if (!sphere_t_ref64(p.sc.sph64[best - sbase], o64, d64, tb64)) tb64 = (double)tb;
+                        if (!sphere_t_ref64(kargs()->sc.sph64[best - sbase], o64, d64, tb64)) tb64 = (double)tb;
                         RTW_PROBE_ABL_WINNER();
                     }
                 } else if (!skip) {   // (kernels without stealing)
@@ -2010,16 +2025,16 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                         constexpr int kKind = kWorld == kWorldBvhLds ? kWorldBvhWW : kWorld;
                         bvh_closest_excl<kKind, kRobust>(scw, sbase, o, d, tmin, tb, best, stk, nvis, ntest, excl);
                     } else {
-                        sweep_spheres_excl<kRobust>(sph, p.sc.n_sph, sbase, o, d, tmin, tb, best, excl);
+                        sweep_spheres_excl<kRobust>(sph, kargs()->sc.n_sph, sbase, o, d, tmin, tb, best, excl);
                     }
                     if (best != prev && best >= sbase) {
-                        if (!sphere_t_ref64(p.sc.sph64[best - sbase], o64, d64, tb64)) tb64 = (double)tb;
+                        if (!sphere_t_ref64(kargs()->sc.sph64[best - sbase], o64, d64, tb64)) tb64 = (double)tb;
                         RTW_PROBE_ABL_WINNER();
                     }
                 }
                 // a plane's t in f64 too, so that its hit points lie within f64 rounding
                 // of the plane (the one-sided Book-1 ground is never hit from above)
-                if (best >= 0 && best < nplanes) tb64 = plane_t_ref64(p.sc.pl64 + 2 * best, o64, d64);
+                if (best >= 0 && best < nplanes) tb64 = plane_t_ref64(kargs()->sc.pl64 + 2 * best, o64, d64);
                 RTW_PROBE_H64();
             } else if constexpr (kWorld >= kWorldBvh) {
                 RTW_PROBE_CLOSEST();
@@ -2032,7 +2047,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                     bvh_closest<kKind, kRobust>(scw, sbase, o, d, tmin, tb, best, stk, nvis, ntest, self_s);
                 }
             } else {
-                sweep_spheres<kRobust>(sph, p.sc.n_sph, sbase, o, d, tmin, tb, best);
+                sweep_spheres<kRobust>(sph, kargs()->sc.n_sph, sbase, o, d, tmin, tb, best);
             }
             ++segs;
             RTW_PROBE_SEGMENT();
@@ -2040,7 +2055,8 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
             bool done = false;
             V3<R> col = zero;
             if (best < 0) {
-                col = mult * bg + res;                                 // camera.rs:473-475
+                const KArgs* k = kargs();
+                col = mult * mk(k->bg[0], k->bg[1], k->bg[2]) + res;   // camera.rs:473-475
                 done = true;
             } else {
                 // HitRecord::new, hittable.rs:101-129
@@ -2064,7 +2080,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                     // Transformed<Cuboid>: the record of the object-space hit,
                     // its point mapped back (transform_point3d); the normal and
                     // front face stay in object space (transformations.rs:14-29)
-                    const R* B = p.sc.boxes + kBoxR * (best - bbase);
+                    const R* B = kargs()->sc.boxes + kBoxR * (best - bbase);
                     R t2;
                     int qd = 0;
                     V3<R> o2, d2;
@@ -2074,9 +2090,9 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                     outward = n;
                     const V3<R> po = o2 + d2 * t2;
                     pnt = mat3_mul(B + kBoxRot, po) + q3(B, kBoxT);
-                    m = p.sc.box_mat[best - bbase];
-                    mtype = p.sc.mat_type[m];
-                    mp = p.sc.mat_p[m];
+                    m = kargs()->sc.box_mat[best - bbase];
+                    mtype = kargs()->sc.mat_type[m];
+                    mp = kargs()->sc.mat_p[m];
                     box_hit = true;
                     if constexpr (kTex) {                          // get_quad_uv, object space
                         const R* Q = B + kQuadR * qd;
@@ -2085,18 +2101,18 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                         hv = dot(cross(q3(Q, 3), pq), q3(Q, 9));
                     }
                 } else if (best < nplanes) {
-                    const R* pl = p.sc.planes + kPlaneR * best;
+                    const R* pl = kargs()->sc.planes + kPlaneR * best;
                     outward = mk(pl[3], pl[4], pl[5]);
-                    m = p.sc.plane_mat[best];
-                    mtype = p.sc.mat_type[m];
-                    mp = p.sc.mat_p[m];
+                    m = kargs()->sc.plane_mat[best];
+                    mtype = kargs()->sc.mat_type[m];
+                    mp = kargs()->sc.mat_p[m];
                     if constexpr (kTex) plane_uv(pl, pnt, hu, hv);
                 } else if (kPrims && best < bbase) {
-                    const R* Q = p.sc.quads + kQuadR * (best - nplanes);
+                    const R* Q = kargs()->sc.quads + kQuadR * (best - nplanes);
                     outward = q3(Q, 12);                           // quadrilateral.rs:97
-                    m = p.sc.quad_mat[best - nplanes];
-                    mtype = p.sc.mat_type[m];
-                    mp = p.sc.mat_p[m];
+                    m = kargs()->sc.quad_mat[best - nplanes];
+                    mtype = kargs()->sc.mat_type[m];
+                    mp = kargs()->sc.mat_p[m];
                     if constexpr (kTex) {                          // get_quad_uv, quadrilateral.rs:58-63
                         const V3<R> pq = pnt - q3(Q, 0);
                         hu = dot(cross(pq, q3(Q, 6)), q3(Q, 9));
@@ -2104,15 +2120,15 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                     }
                 } else {
                     const uint32_t k = (uint32_t)(best - sbase);
-                    const R4<R> sk = p.sc.sph[k];
-                    outward = PR::divs(pnt - mk(sk.x, sk.y, sk.z), p.sc.sph_r[k]);  // sphere.rs:82-83
+                    const R4<R> sk = kargs()->sc.sph[k];
+                    outward = PR::divs(pnt - mk(sk.x, sk.y, sk.z), kargs()->sc.sph_r[k]);  // sphere.rs:82-83
                     // one level of loads: the sphere's material kind and
                     // parameters are copied per sphere (sph_mat word: id,
                     // kind, isolated flag; sph_shade: albedo + fuzz | ior)
-                    const uint32_t mw = p.sc.sph_mat[k];
+                    const uint32_t mw = kargs()->sc.sph_mat[k];
                     m = mw & 0xffffffu;
                     mtype = (mw >> 24) & 0x7fu;
-                    mp = p.sc.sph_shade[k];
+                    mp = kargs()->sc.sph_shade[k];
                     next_self = (mw >> 31) ? (int32_t)k : -1;   // bit 31: isolated sphere
                     if constexpr (kHit64) {
                         next_self = (int32_t)k;
@@ -2122,7 +2138,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                         bool scatter64 = mtype == kMatMetal || mtype == kMatDielectric;
                         RTW_PROBE_ABL_SCATTER(scatter64);
                         if (scatter64) {
-                            n64 = sphere_normal64(pnt64, p.sc.sph64[k]);
+                            n64 = sphere_normal64(pnt64, kargs()->sc.sph64[k]);
                             outward = mk((float)n64.x, (float)n64.y, (float)n64.z);
                             sph_hit = true;
                         }
@@ -2143,7 +2159,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                 V3<R> colour = mk(mp.x, mp.y, mp.z);
                 if constexpr (kTex) {
                     if (mtype == kMatDiffuseLight || mtype == kMatLambertian)
-                        colour = tex_colour(p.sc, p.sc.mat_tex[m], hu, hv, pnt);
+                        colour = tex_colour(p.sc, kargs()->sc.mat_tex[m], hu, hv, pnt);
                 }
                 const V3<R> emitted = mtype == kMatDiffuseLight ? colour : zero;
                 if (kHit64 && sph_hit) {
@@ -2151,8 +2167,8 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                     RTW_PROBE_LANES(7);
                     const bool metal = mtype == kMatMetal;
                     bool keep;
-                    RTW_PROBE_SCATTER64(specular_dir64(metal, d64, n64, front, p.sc.mat64[m], g2, keep2).y);
-                    d64 = specular_dir64(metal, d64, n64, front, p.sc.mat64[m], g, keep);
+                    RTW_PROBE_SCATTER64(specular_dir64(metal, d64, n64, front, kargs()->sc.mat64[m], g2, keep2).y);
+                    d64 = specular_dir64(metal, d64, n64, front, kargs()->sc.mat64[m], g, keep);
                     if (!keep) {
                         col = mult * emitted + res;
                         done = true;
@@ -2213,20 +2229,20 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                     V3<R> dir;
                     const bool to_light = PR::u_std(g.next()) < (R)0.5;
                     bool sampled = false;
-                    if (to_light && (p.sc.n_list == 0 || (kPrims && p.sc.lref))) {
+                    if (to_light && (kargs()->sc.n_list == 0 || (kPrims && kargs()->sc.lref))) {
                         sampled = true;
                         // HittableList::random (hittable_list.rs:414-419): a
                         // uniform light (one gen_index draw), then its random()
-                        if (p.sc.n_list == 0) {
+                        if (kargs()->sc.n_list == 0) {
                             // an empty list panics there (:417): counted; the
                             // sample goes on along a NaN direction and ends NaN
                             // at its next world query, as in the oracle
                             atomicAdd(p.counters + 5, 1ull);
                             dir = mk((R)NAN, (R)NAN, (R)NAN);
                         } else {
-                            const uint32_t ref = p.sc.lref[g.index(p.sc.n_list)];
+                            const uint32_t ref = kargs()->sc.lref[g.index(kargs()->sc.n_list)];
                             if (ref & kLrefQuad) {
-                                dir = quad_random(p.sc.lquads + kQuadR * (ref & 0x3fffffffu), pnt, g);
+                                dir = quad_random(kargs()->sc.lquads + kQuadR * (ref & 0x3fffffffu), pnt, g);
                             } else if (ref & kLrefDefault) {
                                 dir = mk<R>(1, 0, 0);              // Hittable::random default
                             } else {
@@ -2239,14 +2255,14 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                         // a sphere light (one gen_index draw, then Sphere::random)
                         // or the cosine lobe, in one pass (mixture_direction)
                         R4<R> L = R4<R>{0, 0, 0, 0};
-                        if (to_light) L = li[g.index(p.sc.n_lights)];
+                        if (to_light) L = li[g.index(kargs()->sc.n_lights)];
                         dir = mixture_direction(to_light, uvw, mk(L.x, L.y, L.z), L.w, pnt, g);
                     }
                     RTW_PROBE_LAMBERT_DIR();
                     const V3<R> ndir = PR::normalize(dir);
                     const R cos_w = PR::over_pi(dot(ndir, uvw.w));
                     R acc;                                                // hittable_list.rs:408-412
-                    if (kPrims && p.sc.lref)
+                    if (kPrims && kargs()->sc.lref)
                         acc = lights_pdf_mixed(p.sc, li, pnt, dir);
                     else if constexpr (kLightBvh)
                         acc = p.light_bvh == 2
@@ -2254,9 +2270,9 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                                   : lights_pdf_bvh<kRobust>(p.sc, pnt, dir,
                                                             reinterpret_cast<int32_t*>(smem) + wave * p.stack * 64 + lane);
                     else if constexpr (kWorld == kWorldBvhLds && sizeof(R) == 4)
-                        acc = lights_pdf_sum_pk<kRobust>(li, l_lp, p.sc.n_lights, pnt, dir);
+                        acc = lights_pdf_sum_pk<kRobust>(li, l_lp, kargs()->sc.n_lights, pnt, dir);
                     else
-                        acc = lights_pdf_sum<kRobust>(li, p.sc.n_lights, pnt, dir);
+                        acc = lights_pdf_sum<kRobust>(li, kargs()->sc.n_lights, pnt, dir);
                     RTW_PROBE_LIGHT_PDF();
                     // / len; a BVH leaf list multiplies by len and divides again (bvh.rs:67-76, 191-194)
                     R lpdf = PR::div_(acc, (R)p.sc.n_list);
@@ -2292,18 +2308,19 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                 // the item's running sum lives in its chunk-sum slot, not in
                 // registers: (0 + s_first) on the first sample, then slot + s
                 // -- the fold of camera.rs:323-335 in the same order
-                R* dst = p.partial + (((size_t)my_lt * 64 + px) * p.n_chunks + c) * 3;
+                const KArgs* k = kargs();
+                R* dst = k->partial + (((size_t)my_lt * 64 + px) * k->n_chunks + c) * 3;
                 V3<R> prev = zero;
-                if (p.chunk > 1) {   // (wave-uniform: one sample per item never reads the slot)
-                    if (s != c * p.chunk) prev = mk(dst[0], dst[1], dst[2]);
+                if (k->chunk > 1) {   // (wave-uniform: one sample per item never reads the slot)
+                    if (s != c * k->chunk) prev = mk(dst[0], dst[1], dst[2]);
                 }
                 const V3<R> part = prev + col;
                 dst[0] = part.x;
                 dst[1] = part.y;
                 dst[2] = part.z;
-                if (p.tile_cost) {   // tile costs for the task order: this sample's work
-                    if (s < p.cost_spp)
-                        atomicAdd(p.tile_cost + my_lt, nvis + ntest + kCostPerSegment * (p.max_depth - depth + 1u));
+                if (k->tile_cost) {   // tile costs for the task order: this sample's work
+                    if (s < k->cost_spp)
+                        atomicAdd(k->tile_cost + my_lt, nvis + ntest + kCostPerSegment * (k->max_depth - depth + 1u));
                 }
                 ++s;
                 if (s < s_end) {
