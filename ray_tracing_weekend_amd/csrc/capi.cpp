@@ -64,6 +64,8 @@ struct rtw_ctx {
     uint32_t lpt_pilot_depth = 0;     // ... and its max depth (0: the camera's); a path's segments
                                       // run one after another, so the pilot lasts as long as its
                                       // longest path
+    uint32_t grid_piece = 8;          // f32 light grid walks: cells per piece of the wave's
+                                      // cooperative walk (0: one lane walks its own ray)
     uint32_t light_bvh_min = 64;      // light lists at least this long use the light BVH
                                       // (C2, 19 lights: the linear masked loop is faster)
     hipStream_t stream = nullptr;
@@ -966,6 +968,7 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
     // f64 hit points: the f32 kernels of sphere + plane scenes (the launch
     // routes textured / quad / cuboid scenes to kernels without them)
     p.hit64 = c->hit64 ? 1u : 0u;
+    p.grid_piece = c->grid_piece;
     p.task_table = nullptr;
     p.tile_cost = nullptr;
     p.cost_spp = 0;
@@ -1155,6 +1158,7 @@ int rtw_set_tuning(rtw_ctx* c, const char* key, int64_t value) {
     else if (k == "lpt_pilot_spp") c->lpt_pilot_spp = (uint32_t)std::min<int64_t>(std::max<int64_t>(value, 1), 64);
     else if (k == "lpt_pilot_depth") c->lpt_pilot_depth = (uint32_t)std::min<int64_t>(value, 1u << 20);
     else if (k == "light_bvh_min") c->light_bvh_min = (uint32_t)std::min<int64_t>(value, 1u << 30);
+    else if (k == "grid_piece") c->grid_piece = (uint32_t)std::min<int64_t>(value, 1u << 20);
     else if (k == "partial_max") c->partial_max = std::max<size_t>(1 << 20, (size_t)value);
     else if (k == "group") c->group = (uint32_t)value;
     else if (k == "target_tasks") c->target_tasks = std::max<uint64_t>(1, (uint64_t)value);

@@ -1,7 +1,8 @@
 // light_grid.hpp -- the light grid's cell walk (the light pdf's all-hits
 // query over long light lists, render_kernel.hpp lights_pdf_grid).  Host +
 // device: tests/native/grid_walk_check.cpp runs the f64 instance on the CPU
-// against a brute-force sweep (every hit light counted exactly once).
+// against a brute-force sweep (every hit light counted exactly once), whole
+// and cut into pieces as the wave-cooperative walk cuts it.
 #pragma once
 
 #include <math.h>
@@ -75,6 +76,101 @@ __host__ __device__ inline void light_grid_walk(const DevScene<R>& sc, V3<R> o, 
         const uint32_t b = sc.lg_start[c], e = sc.lg_start[c + 1];
         for (uint32_t k = b; k < e; ++k) item(k, te, tx);
         if (last) break;
+        te = tx;
+        if (axis == 0) {
+            cx = ni;
+            c += sx;
+            tmx = exit_t(cx, sx, sc.lg_lo[0], sc.lg_cell[0], o.x, ix);
+        } else if (axis == 1) {
+            cy = ni;
+            c += sy * nx;
+            tmy = exit_t(cy, sy, sc.lg_lo[1], sc.lg_cell[1], o.y, iy);
+        } else {
+            cz = ni;
+            c += sz * nx * ny;
+            tmz = exit_t(cz, sz, sc.lg_lo[2], sc.lg_cell[2], o.z, iz);
+        }
+    }
+}
+
+// The grid interval [tn, tf] of the ray (the box clip light_grid_walk starts
+// from) and the number of cells the walk crosses in it (entry and exit cells
+// of the clip, one step per crossed cell boundary); false: the ray misses the
+// grid.  Used to cut a walk into pieces (lights_pdf_grid_coop).
+template <typename R>
+__host__ __device__ inline bool light_grid_span(const DevScene<R>& sc, V3<R> o, V3<R> d, R ix, R iy, R iz, R& tn, R& tf,
+                                       uint32_t& cells) {
+    const R x0 = (sc.lg_lo[0] - o.x) * ix, x1 = (sc.lg_hi[0] - o.x) * ix;
+    const R y0 = (sc.lg_lo[1] - o.y) * iy, y1 = (sc.lg_hi[1] - o.y) * iy;
+    const R z0 = (sc.lg_lo[2] - o.z) * iz, z1 = (sc.lg_hi[2] - o.z) * iz;
+    tn = fmax(fmax(fmin(x0, x1), fmin(y0, y1)), fmax(fmin(z0, z1), (R)0));
+    tf = fmin(fmax(x0, x1), fmin(fmax(y0, y1), fmax(z0, z1)));
+    if (!(tn <= tf)) return false;
+    auto span = [&](R oc, R dc, R lo, R inv, int n) {
+        const int a = (int)fmin(fmax((oc + tn * dc - lo) * inv, (R)0), (R)(n - 1));
+        const int b = (int)fmin(fmax((oc + tf * dc - lo) * inv, (R)0), (R)(n - 1));
+        return (uint32_t)(a > b ? a - b : b - a);
+    };
+    cells = 1u + span(o.x, d.x, sc.lg_lo[0], sc.lg_inv[0], (int)sc.lg_n[0]) +
+            span(o.y, d.y, sc.lg_lo[1], sc.lg_inv[1], (int)sc.lg_n[1]) +
+            span(o.z, d.z, sc.lg_lo[2], sc.lg_inv[2], (int)sc.lg_n[2]);
+    return true;
+}
+
+// One piece of light_grid_walk: the cells the ray crosses from t0 on, with the
+// walk's interval bookkeeping clipped to the piece -- the first interval
+// starts at t0 (-inf for the ray's first piece, `head`), and the cell the walk
+// is in when it passes t1 ends the piece at t1 (+inf for the ray's last piece,
+// `tail`).  The pieces [t_j, t_j+1) of one ray partition the real line as the
+// whole walk's intervals do, so a light is counted at most once over them; a
+// piece finds its entry cell as the whole walk does (the point at t0, clamped
+// into the grid: the same rounding, covered by the host's padding), so a hit
+// light is counted exactly once.  head && tail with t0 = tn is light_grid_walk.
+template <typename R, typename Item>
+__host__ __device__ inline void light_grid_walk_piece(const DevScene<R>& sc, V3<R> o, V3<R> d, R ix, R iy, R iz, R t0, R t1,
+                                             bool head, bool tail, Item&& item) {
+    const R kInf = (R)INFINITY;
+    const int nx = (int)sc.lg_n[0], ny = (int)sc.lg_n[1], nz = (int)sc.lg_n[2];
+    auto cell_of = [&](R oc, R dc, R lo, R inv, int n) {
+        return (int)fmin(fmax((oc + t0 * dc - lo) * inv, (R)0), (R)(n - 1));
+    };
+    int cx = cell_of(o.x, d.x, sc.lg_lo[0], sc.lg_inv[0], nx);
+    int cy = cell_of(o.y, d.y, sc.lg_lo[1], sc.lg_inv[1], ny);
+    int cz = cell_of(o.z, d.z, sc.lg_lo[2], sc.lg_inv[2], nz);
+    const int sx = d.x > 0 ? 1 : (d.x < 0 ? -1 : 0);
+    const int sy = d.y > 0 ? 1 : (d.y < 0 ? -1 : 0);
+    const int sz = d.z > 0 ? 1 : (d.z < 0 ? -1 : 0);
+    R te = head ? -kInf : t0;
+    auto exit_t = [&](int c, int s, R lo, R cell, R oc, R inv) {
+        return s == 0 ? kInf : fmax((lo + (R)(c + (s > 0 ? 1 : 0)) * cell - oc) * inv, te);
+    };
+    R tmx = exit_t(cx, sx, sc.lg_lo[0], sc.lg_cell[0], o.x, ix);
+    R tmy = exit_t(cy, sy, sc.lg_lo[1], sc.lg_cell[1], o.y, iy);
+    R tmz = exit_t(cz, sz, sc.lg_lo[2], sc.lg_cell[2], o.z, iz);
+    uint32_t c = (uint32_t)((cz * ny + cy) * nx + cx);
+    for (;;) {
+        int axis, ni, nn;
+        R tx;
+        if (tmx <= tmy && tmx <= tmz) {
+            axis = 0; tx = tmx; ni = cx + sx; nn = nx;
+        } else if (tmy <= tmz) {
+            axis = 1; tx = tmy; ni = cy + sy; nn = ny;
+        } else {
+            axis = 2; tx = tmz; ni = cz + sz; nn = nz;
+        }
+        const bool last = !(tx < kInf) || ni < 0 || ni >= nn;
+        bool stop = last;
+        if (!tail) {
+            if (last || !(tx < t1)) {
+                tx = t1;
+                stop = true;
+            }
+        } else if (last) {
+            tx = kInf;
+        }
+        const uint32_t b = sc.lg_start[c], e = sc.lg_start[c + 1];
+        for (uint32_t k = b; k < e; ++k) item(k, te, tx);
+        if (stop) break;
         te = tx;
         if (axis == 0) {
             cx = ni;

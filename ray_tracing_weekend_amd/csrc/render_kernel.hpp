@@ -1090,6 +1090,19 @@ __device__ __forceinline__ void bvh_traverse_steal(const DevScene<R>& sc, int32_
     slots.result(lane, T);
 }
 
+// A ray with a NaN component hits nothing (every sphere, plane and light test
+// compares a NaN), but its slab tests keep every box (fmin / fmax drop the
+// NaN), so a traversal would visit the whole tree for a miss -- C5: the NaN
+// directions a Lambertian point inside a light sphere samples (sphere.rs:
+// 113-127) cost one wave a quarter of a second.  Such rays skip the traversal
+// (bvh_dispatch: the trees outside LDS; a tree in LDS is small, its stealing
+// traversal shares such a walk, and the check costs C2 more than it saves).
+template <typename R>
+__device__ __forceinline__ bool ray_nan(V3<R> o, V3<R> d) {
+    return __builtin_isnan(o.x) | __builtin_isnan(o.y) | __builtin_isnan(o.z) | __builtin_isnan(d.x) |
+           __builtin_isnan(d.y) | __builtin_isnan(d.z);
+}
+
 // `self` >= 0: the ray starts on that (isolated) sphere; it is tested first
 // and, when the ray hits it again, that hit is the closest sphere hit (see
 // isolated_spheres, host/bvh.hpp) and the traversal is skipped.
@@ -1097,8 +1110,8 @@ template <int kKind, typename R, typename TT>
 __device__ __forceinline__ void bvh_dispatch(const DevScene<R>& sc, int32_t base, V3<R> o, V3<R> d,
                                              TT& T, int32_t* stk, uint32_t& nvis,
                                              uint32_t& ntest, int32_t self) {
-    bool skip = false;
-    if (self >= 0) {
+    bool skip = ray_nan(o, d);
+    if (!skip && self >= 0) {
         skip = T.test_hit(sc.sph[self], base + self);
         ++ntest;
     }
@@ -1519,6 +1532,93 @@ __device__ __forceinline__ float lights_pdf_grid(const DevScene<float>& sc, V3<f
     });
     return acc;
 }
+// lights_pdf_grid by the whole wave (f32, KParams::grid_piece = P > 0).  A ray
+// that skims a flat light layer walks the grid's whole width (C5: a ground
+// point sampling one of 50k lights at the same height, ~150 cells of ~4 lights
+// each) while most rays walk a few cells, and a lane-per-ray walk keeps its
+// wave for the longest one (C5: 10 % of lanes active).  Here every lane of
+// the wave walks for the pending rays (`pend`; the ray is (o, d)): each ray's
+// grid interval [tn, tf] is cut into k = ceil(cells / P) pieces of equal
+// length in t, the pieces of all rays are dealt to the 64 lanes round by
+// round, every piece's pdf sum lands in an LDS slot, and each ray's owner
+// adds its pieces up in order.  The cut depends on the ray and P alone and
+// the sum runs in piece order, so the result does not depend on which rays
+// share the wave; the first piece starts from the big list's sum, so a
+// one-piece ray (most of them) sums exactly as lights_pdf_grid.  `slots`:
+// `cap` (a multiple of 64) floats of the wave's LDS; every lane of the wave
+// calls this (converged), with wave-uniform P.
+template <bool kRobust>
+__device__ __forceinline__ float lights_pdf_grid_coop(const DevScene<float>& sc, bool pend, V3<float> o, V3<float> d,
+                                                   uint32_t P, float* __restrict__ slots, uint32_t cap,
+                                                   uint32_t lane) {
+    float acc = 0.f, tn = 0.f, tf = 0.f;
+    uint32_t k = 0;
+    if (pend) {
+        const float a = len2_f32(d);
+        const float ia = __builtin_amdgcn_rcpf(a);
+        for (uint32_t q = 0; q < sc.lg_big; ++q) {
+            const R4<float> L = sc.lg_sph[q];
+            if (light_hit_f32<kRobust>(L, o, d, a, ia)) acc += light_pdf_f32(L, o);
+        }
+        uint32_t cells = 0;
+        if (light_grid_span(sc, o, d, grid_inv(d.x), grid_inv(d.y), grid_inv(d.z), tn, tf, cells))
+            k = (cells + P - 1u) / P;
+    }
+    // first piece of each ray: exclusive prefix of k over the lanes
+    uint32_t incl = k;
+#pragma unroll
+    for (uint32_t off = 1; off < 64; off <<= 1) {
+        const uint32_t v = (uint32_t)__shfl_up((int)incl, off);
+        if (lane >= off) incl += v;
+    }
+    const uint32_t first = incl - k, total = (uint32_t)__shfl((int)incl, 63);
+    for (uint32_t b = 0; b < total; b += cap) {
+        const uint32_t e = min(b + cap, total);
+        for (uint32_t r = b; r < e; r += 64) {
+            const uint32_t g = r + lane;
+            // the piece's ray: the last lane whose first piece is <= g
+            uint32_t own = 0;
+#pragma unroll
+            for (uint32_t step = 32; step; step >>= 1) {
+                const uint32_t f = (uint32_t)__shfl((int)first, (int)(own + step));
+                own = f <= g ? own + step : own;
+            }
+            const V3<float> ro = mk(bperm_f(o.x, own), bperm_f(o.y, own), bperm_f(o.z, own));
+            const V3<float> rd = mk(bperm_f(d.x, own), bperm_f(d.y, own), bperm_f(d.z, own));
+            const float rtn = bperm_f(tn, own), rtf = bperm_f(tf, own), racc = bperm_f(acc, own);
+            const uint32_t rk = (uint32_t)bperm_i((int32_t)k, own), rfirst = (uint32_t)bperm_i((int32_t)first, own);
+            if (g < e) {
+                const uint32_t j = g - rfirst;
+                const float step = (rtf - rtn) / (float)rk;
+                auto t_at = [&](uint32_t q) { return q == 0 ? rtn : __builtin_fmaf((float)q, step, rtn); };
+                const float ra = len2_f32(rd);
+                const float ria = __builtin_amdgcn_rcpf(ra);
+                float part = j == 0 ? racc : 0.f;
+                light_grid_walk_piece(sc, ro, rd, grid_inv(rd.x), grid_inv(rd.y), grid_inv(rd.z), t_at(j),
+                                      t_at(j + 1), j == 0, j + 1 == rk, [&](uint32_t q, float te, float tx) {
+                    const R4<float> L = sc.lg_sph[q];
+                    const float fx = ro.x - L.x, fy = ro.y - L.y, fz = ro.z - L.z;
+                    const float tc = -__builtin_fmaf(rd.z, fz, __builtin_fmaf(rd.y, fy, rd.x * fx)) * ria;
+                    if (light_hit_f32<kRobust>(L, ro, rd, ra, ria) & (tc >= te) & (tc < tx))
+                        part += light_pdf_f32(L, ro);
+                });
+                slots[g - b] = part;
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (k) {
+            const uint32_t g0 = max(first, b), g1 = min(first + k, e);
+            for (uint32_t g = g0; g < g1; ++g) acc = g == first ? slots[g - b] : acc + slots[g - b];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    return acc;
+}
+
 // f64 (parity mode): the hit lights' list indices, summed in LIST order as in
 // lights_pdf_bvh; more than 8 hits falls back to the linear loop.
 template <bool kRobust>
@@ -1856,6 +1956,14 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                                         // scatter's own f64 result, else dither64 of the f32 one)
     uint32_t segs = 0, lambs = 0, nvis = 0, ntest = 0;
     bool active = false, need = true;
+    // kCoopGrid (f32 kernels with the light grid, KParams::grid_piece > 0): a
+    // Lambertian bounce's light pdf is left pending (`pend`) for the wave's
+    // cooperative grid walk at the end of the trip (lights_pdf_grid_coop); the
+    // bounce's att * scattering pdf and half its cosine pdf wait with it
+    constexpr bool kCoopGrid = kLightBvh && sizeof(R) == 4 && !kPrims;
+    bool pend = false;
+    V3<R> pend_aw = zero;
+    R pend_ch = (R)0;
     RTW_PROBE_WAVE_BEGIN();
 
     auto start_sample = [&]() {
@@ -2262,6 +2370,23 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                     const V3<R> ndir = PR::normalize(dir);
                     const R cos_w = PR::over_pi(dot(ndir, uvw.w));
                     R acc;                                                // hittable_list.rs:408-412
+                    // the light grid's walk by the whole wave: deferred to the end of the trip
+                    const bool coop = kCoopGrid && p.light_bvh == 2 && p.grid_piece != 0 && !(kPrims && kargs()->sc.lref);
+                    if (coop) {
+                        const R spdf = PR::max_(PR::over_pi(dot(nrm, ndir)), (R)0);
+                        pend = true;
+                        pend_aw = att * spdf;
+                        pend_ch = PR::max_(cos_w, (R)0) * (R)0.5;
+                        res = res + mult * emitted;
+                        o = pnt;
+                        self_s = next_self;
+                        self_iso = next_iso;
+                        if constexpr (kHit64) {
+                            o64 = pnt64;
+                            d64 = dither64(dir);
+                        }
+                        d = dir;
+                    } else {
                     if (kPrims && kargs()->sc.lref)
                         acc = lights_pdf_mixed(p.sc, li, pnt, dir);
                     else if constexpr (kLightBvh)
@@ -2291,6 +2416,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                         d64 = dither64(dir);
                     }
                     d = dir;
+                    }
                 } else {
                     // Invisible (material.rs:321-325): scatter() == None
                     col = mult * emitted + res;
@@ -2301,6 +2427,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                     if (depth == 0) {                                  // camera.rs:470-472
                         col = zero + res;
                         done = true;
+                        if constexpr (kCoopGrid) pend = false;         // its pdf is not needed
                     }
                 }
             }
@@ -2330,6 +2457,22 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                 } else {
                     active = false;
                     need = true;
+                }
+            }
+        }
+        if constexpr (kCoopGrid) {
+            // the deferred Lambertian light pdfs of this trip, by the whole wave;
+            // then the path throughput as in the Lambertian branch
+            if (__any(pend)) {
+                float* slots = reinterpret_cast<float*>(smem) + wave * p.stack * 64;
+                const R acc = lights_pdf_grid_coop<kRobust>(p.sc, pend, o, d, kargs()->grid_piece, slots,
+                                                            p.stack * 64, lane);
+                if (pend) {
+                    R lpdf = PR::div_(acc, (R)p.sc.n_list);
+                    if (p.sc.light_flags & 1u) lpdf = PR::div_(lpdf * (R)p.sc.n_list, (R)p.sc.n_list);
+                    const R pdf = lpdf * (R)0.5 + pend_ch;
+                    mult = mult * PR::divs(pend_aw, pdf);
+                    pend = false;
                 }
             }
         }

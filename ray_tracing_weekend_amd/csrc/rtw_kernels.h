@@ -207,6 +207,8 @@ struct KParams {
                                       // render's costs); null: t = tile * n_groups + group
     uint32_t* tile_cost;              // non-null: [local tile] += segments of each sample s < cost_spp
     uint32_t cost_spp;                //   (a pilot render, or the first render of a split)
+    uint32_t grid_piece;              // f32 light grid: cells per piece of the wave-cooperative
+                                      // walk (lights_pdf_grid_coop); 0: one lane per ray
 };
 
 // The cost of a sample for the task order (KParams::tile_cost): its BVH node

@@ -106,8 +106,41 @@ int main() {
                     const double tc = -((o.x - l.x) * d.x + (o.y - l.y) * d.y + (o.z - l.z) * d.z) * ia;
                     if (tc >= te && tc < tx && hit_class(&L[4 * g.items[q]], o, d) >= 0) ++count[g.items[q]];
                 });
+                // the same walk cut into pieces (render_kernel.hpp lights_pdf_grid_coop):
+                // k = ceil(cells / P) pieces of equal length in t
+                std::vector<int> pc(3 * n, 0);
+                {
+                    const double ix = rtw::dev::grid_inv(d.x), iy = rtw::dev::grid_inv(d.y), iz = rtw::dev::grid_inv(d.z);
+                    double tn, tf;
+                    uint32_t cells = 0;
+                    const uint32_t Ps[3] = {1, 3, 8};
+                    if (rtw::dev::light_grid_span(sc, o, d, ix, iy, iz, tn, tf, cells)) {
+                        for (int v = 0; v < 3; ++v) {
+                            const uint32_t kp = (cells + Ps[v] - 1) / Ps[v];
+                            const double step = (tf - tn) / (double)kp;
+                            auto t_at = [&](uint32_t q) { return q == 0 ? tn : fma((double)q, step, tn); };
+                            for (uint32_t j = 0; j < kp; ++j)
+                                rtw::dev::light_grid_walk_piece(sc, o, d, ix, iy, iz, t_at(j), t_at(j + 1), j == 0,
+                                                                j + 1 == kp, [&](uint32_t q, double te, double tx) {
+                                    const R4<double>& l = items[q];
+                                    const double tc = -((o.x - l.x) * d.x + (o.y - l.y) * d.y + (o.z - l.z) * d.z) * ia;
+                                    if (tc >= te && tc < tx && hit_class(&L[4 * g.items[q]], o, d) >= 0)
+                                        ++pc[v * n + g.items[q]];
+                                });
+                        }
+                    }
+                    for (uint32_t q = 0; q < g.n_big; ++q)
+                        for (int v = 0; v < 3; ++v) ++pc[v * n + g.items[q]];
+                }
                 for (uint32_t k = 0; k < n; ++k) {
                     const int h = hit_class(&L[4 * k], o, d);
+                    for (int v = 0; v < 3; ++v) {
+                        const bool pok = pc[v * n + k] <= 1 && (h != 1 || pc[v * n + k] == 1);
+                        if (!pok && bad < 10)
+                            printf("pieces %d: scene %d density %g ray %d light %u: counted %d, hit class %d\n", v,
+                                   scene, density, r, k, pc[v * n + k], h);
+                        bad += pok ? 0 : 1;
+                    }
                     ++checked;
                     if (h == 1) ++hits;
                     const bool ok = count[k] <= 1 && (h != 1 || count[k] == 1);

@@ -70,3 +70,36 @@ def test_full_frame_f32_tracks_f64(config, n, spp):
     ra = np.nanmean(np.where(ok[..., None], a, np.nan), axis=(1, 2))
     rb = np.nanmean(np.where(ok[..., None], b, np.nan), axis=(1, 2))
     assert np.corrcoef(ra, rb)[0, 1] > 0.99, config
+
+
+@pytest.mark.parametrize("config,n,spp", [("C3", 50, 4), ("C5", 500, 2)])
+def test_cooperative_grid_walk_matches_lane_walk(config, n, spp):
+    """The wave-cooperative light-grid walk (grid_piece = P > 0, the default:
+    every lane of the wave walks pieces of the pending rays' walks,
+    render_kernel.hpp lights_pdf_grid_coop) against one lane per ray
+    (grid_piece = 0).  Both count the same lights (the pieces partition the
+    walk: tests/native/grid_walk_check.cpp); only the f32 sum of a multi-piece
+    ray's pdfs is associated by piece, so the frames agree to f32 rounding,
+    NaN masks equal -- and the cut depends on the ray alone, so a render is
+    reproduced bit for bit under another scheduling knob."""
+    soa, b = rtw.scenes.simple_soa(SEED_SCENE, n)
+    cam = b.with_image_width(W).with_image_height(H).with_samples_per_pixel(spp).with_max_depth(DEPTH).build()
+    imgs = {}
+    for key, tuning in (("coop", {}), ("lane", {"grid_piece": 0}), ("coop_p3", {"grid_piece": 3}),
+                        ("coop_pixel_major", {"item_order": 0})):
+        with rtw.Renderer(precision=rtw.RTW_F32) as r:
+            for k, v in tuning.items():
+                r.set_tuning(k, v)
+            r.set_scene(soa)
+            imgs[key] = r.render(cam, 17)
+    c, ln = imgs["coop"], imgs["lane"]
+    assert np.array_equal(np.isnan(c).any(-1), np.isnan(ln).any(-1)), config
+    ok = ~np.isnan(ln).any(-1)
+    assert ok.mean() > 0.5
+    rel = np.abs(c[ok] - ln[ok]) / np.maximum(np.abs(ln[ok]), 1e-3)
+    assert rel.max() < 1e-3 and rel.mean() < 1e-6, (config, float(rel.max()), float(rel.mean()))
+    assert (c[ok] == ln[ok]).mean() > 0.9, config
+    same = np.isnan(imgs["coop_pixel_major"]) == np.isnan(c)
+    assert same.all() and np.array_equal(np.nan_to_num(imgs["coop_pixel_major"], nan=-7.0), np.nan_to_num(c, nan=-7.0))
+    p3 = imgs["coop_p3"]
+    assert np.array_equal(np.isnan(p3).any(-1), np.isnan(ln).any(-1))
