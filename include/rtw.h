@@ -214,6 +214,7 @@ int rtw_set_accel(rtw_ctx *ctx, int accel);
  * next rtw_set_scene), "light_bvh_min" (light lists this long or longer take the light grid
  * or light BVH in the BVH kernels, default 64), "light_grid" (light-grid resolution in
  * 1/16 cells per light, default 4; 0 = the light BVH instead; next rtw_set_scene),
+ * "max_group" (longest-first task list: at most this many chunks per task, default 32),
  * "grid_piece" (f32 light-grid walks: cells per piece of the wave's cooperative walk,
  * default 8; 0 = every lane walks its own ray),
  * "light_leaf" (light spheres per light-BVH leaf, 1..15; 0 = 4), "partial_max" (bytes of chunk sums an auto chunk may use, default 8 GiB),

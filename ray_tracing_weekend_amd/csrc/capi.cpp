@@ -95,6 +95,7 @@ struct rtw_ctx {
     // longest-tiles-first task list (pilot render, see lpt_pilot / lpt_tasks)
     uint64_t scene_serial = 0;        // ++ per rtw_upload_scene
     static constexpr uint32_t kMaxGroup = 32;
+    uint32_t max_group = kMaxGroup;   // longest-first task list: at most this many chunks per task
     void* d_lpt = nullptr;            // pilot: [tile cost | chunk sums | tiles]
     size_t lpt_cap = 0;
     bool lpt_valid = false;           // h_lpt_cost is the pilot of (lpt_cam, lpt_serial, rank split, precision)
@@ -826,7 +827,7 @@ int lpt_tasks(rtw_ctx* c, const rtw::KParams<R>& p, uint32_t fixed_group, uint64
         uint32_t g = fixed_group;
         if (!g) {
             const double want = per_task / (double)std::max<uint32_t>(cost[k], 1);
-            g = (uint32_t)std::max(1.0, std::min((double)rtw_ctx::kMaxGroup, std::floor(want + 0.5)));
+            g = (uint32_t)std::max(1.0, std::min((double)std::max(c->max_group, 1u), std::floor(want + 0.5)));
         }
         // the entry holds the chunk count in 12 bits (first chunk < 2^20 in the low 20)
         g = std::min(std::min(g, p.n_chunks), kTaskMaxChunks);
@@ -1158,6 +1159,7 @@ int rtw_set_tuning(rtw_ctx* c, const char* key, int64_t value) {
     else if (k == "lpt_pilot_spp") c->lpt_pilot_spp = (uint32_t)std::min<int64_t>(std::max<int64_t>(value, 1), 64);
     else if (k == "lpt_pilot_depth") c->lpt_pilot_depth = (uint32_t)std::min<int64_t>(value, 1u << 20);
     else if (k == "light_bvh_min") c->light_bvh_min = (uint32_t)std::min<int64_t>(value, 1u << 30);
+    else if (k == "max_group") { c->max_group = (uint32_t)std::min<int64_t>(std::max<int64_t>(value, 1), 4095); c->lpt_tab_valid = false; }
     else if (k == "grid_piece") c->grid_piece = (uint32_t)std::min<int64_t>(value, 1u << 20);
     else if (k == "partial_max") c->partial_max = std::max<size_t>(1 << 20, (size_t)value);
     else if (k == "group") c->group = (uint32_t)value;
