@@ -928,7 +928,9 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
             if (p.sc.lg_on) p.light_bvh = 2;                          // light grid
             else if (light_stack <= rtw::kBvhStack) p.light_bvh = 1;  // light BVH
         }
-        const uint32_t min_stack = p.light_bvh == 1 ? light_stack : 1u;
+        // the light grid's cooperative walk (f32) parks path state in the stack area
+        const uint32_t min_stack = p.light_bvh == 1 ? light_stack
+                                   : (sizeof(R) == 4 && p.light_bvh == 2 ? rtw::kCoopStash + 1u : 1u);
         // binary traversal pushes at most one entry per inner level: a leaf at
         // level `bvh_depth` has that many inner nodes above it (host/bvh.cpp)
         const uint32_t bin_stack = std::max(p.sc.bvh_depth, min_stack);

@@ -2464,9 +2464,44 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
             // the deferred Lambertian light pdfs of this trip, by the whole wave;
             // then the path throughput as in the Lambertian branch
             if (__any(pend)) {
-                float* slots = reinterpret_cast<float*>(smem) + wave * p.stack * 64;
-                const R acc = lights_pdf_grid_coop<kRobust>(p.sc, pend, o, d, kargs()->grid_piece, slots,
-                                                            p.stack * 64, lane);
+                // The walk's registers come on top of the whole path state: the RNG
+                // state and (hit64) the f64 ray wait in the wave's LDS stack area
+                // ([word][lane]; the host sizes p.stack >= kCoopStash + 1) instead of
+                // being spilled to scratch by the compiler; the pieces' slots follow.
+                constexpr uint32_t kStash = kHit64 ? 20u : 8u;
+                static_assert(kStash < kCoopStash + 1, "the host's stack minimum covers the stash");
+                uint32_t* area = reinterpret_cast<uint32_t*>(smem) + wave * p.stack * 64;
+                // hit64: the pending ray is (o64, d64) rounded (o = pnt, d = dir), so o and d
+                // need not stay live to here
+                const V3<R> po = kHit64 ? from64<R>(o64) : o, pd = kHit64 ? from64<R>(d64) : d;
+                auto put = [&](uint32_t k, uint64_t v) {
+                    area[(2 * k) * 64 + lane] = (uint32_t)v;
+                    area[(2 * k + 1) * 64 + lane] = (uint32_t)(v >> 32);
+                };
+                auto get = [&](uint32_t k) {
+                    return (uint64_t)area[(2 * k) * 64 + lane] | ((uint64_t)area[(2 * k + 1) * 64 + lane] << 32);
+                };
+                auto dbits = [](double x) { return (uint64_t)__double_as_longlong(x); };
+                auto bitsd = [](uint64_t x) { return __longlong_as_double((long long)x); };
+                put(0, g.s0);
+                put(1, g.s1);
+                put(2, g.s2);
+                put(3, g.s3);
+                if constexpr (kHit64) {
+                    put(4, dbits(o64.x)); put(5, dbits(o64.y)); put(6, dbits(o64.z));
+                    put(7, dbits(d64.x)); put(8, dbits(d64.y)); put(9, dbits(d64.z));
+                }
+                float* slots = reinterpret_cast<float*>(area + kStash * 64);
+                const R acc = lights_pdf_grid_coop<kRobust>(p.sc, pend, po, pd, kargs()->grid_piece, slots,
+                                                            (p.stack - kStash) * 64, lane);
+                g.s0 = get(0);
+                g.s1 = get(1);
+                g.s2 = get(2);
+                g.s3 = get(3);
+                if constexpr (kHit64) {
+                    o64 = V3<double>{bitsd(get(4)), bitsd(get(5)), bitsd(get(6))};
+                    d64 = V3<double>{bitsd(get(7)), bitsd(get(8)), bitsd(get(9))};
+                }
                 if (pend) {
                     R lpdf = PR::div_(acc, (R)p.sc.n_list);
                     if (p.sc.light_flags & 1u) lpdf = PR::div_(lpdf * (R)p.sc.n_list, (R)p.sc.n_list);

@@ -163,6 +163,10 @@ constexpr uint32_t kBoxRot = 144, kBoxInv = 153, kBoxT = 162, kBoxTi = 165, kBox
                    kBoxOk = 174;
 
 constexpr uint32_t kBvhStack = 32;    // per-lane traversal stack entries (LDS)
+// f32 light-grid kernels: the cooperative walk parks up to this many words of
+// path state per lane in the wave's stack area (render_kernel.hpp), so the
+// host gives them at least kCoopStash + 1 entries
+constexpr uint32_t kCoopStash = 20;
 // Subtree stealing in the while-while traversal (render_kernel.hpp
 // bvh_traverse_steal): per wave the result slots of its 64 rays (f32: a u64
 // key; f64: u64 t bits + u32 id) and 64 rendezvous bytes, in LDS right after

@@ -8,7 +8,8 @@ same hash in the library that is loaded now.
 
 The hash covers the kernel's machine code (its FUNC symbol in the gfx950 code
 object) and its 64-B kernel descriptor (`<name>.kd`: VGPR / SGPR / LDS /
-scratch settings).  Pure Python: the library's `.hip_fatbin` section holds
+scratch settings) with the code-entry offset zeroed (it shifts when another
+kernel of the same code object changes size).  Pure Python: the library's `.hip_fatbin` section holds
 clang offload bundles ("__CLANG_OFFLOAD_BUNDLE__", one per HIP translation
 unit), each with an amdgcn ELF code object per target.
 """
@@ -86,7 +87,10 @@ def kernel_bytes(co: bytes):
         if typ == 2:            # STT_FUNC
             code[name] = body
         elif name.endswith(".kd"):
-            kd[name[:-3]] = body
+            # bytes 16..23: kernel_code_entry_byte_offset, the distance from
+            # the descriptor to the code -- it moves whenever another kernel of
+            # the same code object changes size, the machine code does not
+            kd[name[:-3]] = body[:16] + bytes(8) + body[24:] if len(body) >= 24 else body
     return {k: v + kd.get(k, b"") for k, v in code.items()}
 
 
