@@ -64,7 +64,8 @@ struct rtw_ctx {
     uint32_t lpt_pilot_depth = 0;     // ... and its max depth (0: the camera's); a path's segments
                                       // run one after another, so the pilot lasts as long as its
                                       // longest path
-    uint32_t grid_piece = 8;          // f32 light grid walks: cells per piece of the wave's
+    static constexpr uint32_t kGridPieceAuto = 0xFFFFFFFFu;
+    uint32_t grid_piece = kGridPieceAuto;   // f32 light grid walks: cells per piece of the wave's
                                       // cooperative walk (0: one lane walks its own ray)
     uint32_t light_bvh_min = 64;      // light lists at least this long use the light BVH
                                       // (C2, 19 lights: the linear masked loop is faster)
@@ -971,7 +972,13 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
     // f64 hit points: the f32 kernels of sphere + plane scenes (the launch
     // routes textured / quad / cuboid scenes to kernels without them)
     p.hit64 = c->hit64 ? 1u : 0u;
-    p.grid_piece = c->grid_piece;
+    // auto: walks that cross the whole grid in few pieces give the wave little to
+    // share, short ones pay each piece's setup: a fourteenth of the grid's widest
+    // side, 4..16 cells (C3, 11 cells wide: 4; C5, 112 wide: 8 -- the measured
+    // best of 4 / 6 / 8 for each)
+    p.grid_piece = c->grid_piece != rtw_ctx::kGridPieceAuto
+                       ? c->grid_piece
+                       : std::max(4u, std::min(16u, std::max(p.sc.lg_n[0], std::max(p.sc.lg_n[1], p.sc.lg_n[2])) / 14u));
     p.task_table = nullptr;
     p.tile_cost = nullptr;
     p.cost_spp = 0;
