@@ -213,7 +213,7 @@ int rtw_set_accel(rtw_ctx *ctx, int accel);
  * scenes of >= 100k spheres; takes effect at the
  * next rtw_set_scene), "light_bvh_min" (light lists this long or longer take the light grid
  * or light BVH in the BVH kernels, default 64), "light_grid" (light-grid resolution in
- * 1/16 cells per light, default 4; 0 = the light BVH instead; next rtw_set_scene),
+ * 1/16 cells per light, default 8; 0 = the light BVH instead; next rtw_set_scene),
  * "max_group" (longest-first task list: at most this many chunks per task, default 32),
  * "grid_piece" (f32 light-grid walks: cells per piece of the wave's cooperative walk,
  * default by grid size: its widest side / 14, 4..16; 0 = every lane walks its own ray),

@@ -47,7 +47,7 @@ struct rtw_ctx {
                                       // counter; default: as many as are resident at once);
                                       // 0: one task per wave
     uint32_t light_leaf = 0;          // light spheres per light-BVH leaf; 0 = 4
-    uint32_t light_grid = 4;          // light pdf through the light grid at light_grid / 16
+    uint32_t light_grid = 8;          // light pdf through the light grid at light_grid / 16
                                       // cells per light (set before rtw_set_scene); 0: light BVH
     uint32_t hit64 = 1;               // f32: f64 hit points (the reference's self-intersection odds)
     uint32_t item_order = 1;          // wave item pool: 1 sample-major (C2 +1.3 %, C3 +5 %, C5 +2 %), 0 pixel-major
@@ -974,8 +974,8 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
     p.hit64 = c->hit64 ? 1u : 0u;
     // auto: walks that cross the whole grid in few pieces give the wave little to
     // share, short ones pay each piece's setup: a fourteenth of the grid's widest
-    // side, 4..16 cells (C3, 11 cells wide: 4; C5, 112 wide: 8 -- the measured
-    // best of 4 / 6 / 8 for each)
+    // side, 4..16 cells (at the default 1/2 cell per light: C3, ~16 cells wide:
+    // 4; C5, 158 wide: 11)
     p.grid_piece = c->grid_piece != rtw_ctx::kGridPieceAuto
                        ? c->grid_piece
                        : std::max(4u, std::min(16u, std::max(p.sc.lg_n[0], std::max(p.sc.lg_n[1], p.sc.lg_n[2])) / 14u));

@@ -407,8 +407,9 @@ def test_light_bvh_equals_linear_light_sum(prec):
         .with_max_depth(12).with_lookfrom((8, 3, 8)).with_lookat((0, 0, 0)).with_vfov(45) \
         .with_background((0.7, 0.8, 1.0)).build()
     out = {}
-    # light BVH (light_grid 0), light grid at 1/16, 1/4 (default) and 16 cells per light, linear loop
-    modes = (("bvh", 1, 0), ("grid1", 1, 1), ("grid", 1, 4), ("grid256", 1, 256), ("linear", 1 << 30, 4))
+    # light BVH (light_grid 0), light grid at 1/16, 1/4, 1/2 (default) and 16 cells per light, linear loop
+    modes = (("bvh", 1, 0), ("grid1", 1, 1), ("grid4", 1, 4), ("grid", 1, 8), ("grid256", 1, 256),
+             ("linear", 1 << 30, 8))
     for mode, m, g in modes:
         with rtw.Renderer(device=0, precision=prec) as r:
             r.set_tuning("light_bvh_min", m)
