@@ -942,8 +942,10 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
                                 (size_t)((p.sc.n_sph + 7u) & ~7u) * sizeof(uint32_t) +
                                 (sizeof(R) == 8 ? 32 : 0) +   // (f64: the light list 32-B aligned)
                                 (size_t)p.sc.n_lights * sizeof(rtw::R4<R>) +
-                                // f32: the light pairs of the packed light test
-                                (sizeof(R) == 4 ? (size_t)((p.sc.n_lights + 1u) & ~1u) * sizeof(rtw::R4<R>) : 0);
+                                // f32: the light pairs of the packed light test; f64: the
+                                // lights rounded to f32 for the pre-pass (16 B each)
+                                (sizeof(R) == 4 ? (size_t)((p.sc.n_lights + 1u) & ~1u) * sizeof(rtw::R4<R>)
+                                                : (size_t)p.sc.n_lights * sizeof(rtw::R4<float>));
         if (c->bvh_kind == 2 && p.sc.bvh4_stack + 1 <= rtw::kBvhStack) {
             world = rtw::kWorldBvh4;       // 4-wide, when its stack bound fits
             p.stack = std::max(p.sc.bvh4_stack + 1, min_stack);

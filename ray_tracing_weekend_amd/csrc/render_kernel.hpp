@@ -305,9 +305,13 @@ __device__ __forceinline__ void sweep_spheres_excl(const R4<float>* __restrict__
 // E = 2^-18 (|o|_1 + |c|_1 + r): far above the f32 error of l (a few 2^-24
 // (|o| + |c|)) and of the f64 decision itself (disc's rounding), so every
 // light the f64 test hits stays in.
+// li32 (may be null): the same lights rounded to f32 with |radius| (staged in
+// LDS by the LDS-world kernels): the pre-pass reads them instead of converting
+// the f64 records -- the same f32 values, the same mask
 template <bool kRobust = false>
 __device__ __forceinline__ double lights_pdf_sum(const R4<double>* __restrict__ li, uint32_t n,
-                                                 V3<double> o, V3<double> d) {
+                                                 V3<double> o, V3<double> d,
+                                                 const R4<float>* __restrict__ li32 = nullptr) {
     const float ox = (float)o.x, oy = (float)o.y, oz = (float)o.z;
     const float dx = (float)d.x, dy = (float)d.y, dz = (float)d.z;
     const float a = __builtin_fmaf(dx, dx, __builtin_fmaf(dy, dy, dz * dz));
@@ -319,8 +323,20 @@ __device__ __forceinline__ double lights_pdf_sum(const R4<double>* __restrict__ 
         const uint32_t m = min(32u, n - base);
         uint32_t mask = 0;
         for (uint32_t k = 0; k < m; ++k) {
-            const R4<double> L = li[base + k];
-            const float cx = (float)L.x, cy = (float)L.y, cz = (float)L.z, r = fabsf((float)L.w);
+            float cx, cy, cz, r;
+            if (li32) {
+                const R4<float> L = li32[base + k];
+                cx = L.x;
+                cy = L.y;
+                cz = L.z;
+                r = L.w;
+            } else {
+                const R4<double> L = li[base + k];
+                cx = (float)L.x;
+                cy = (float)L.y;
+                cz = (float)L.z;
+                r = fabsf((float)L.w);
+            }
             const float fx = ox - cx, fy = oy - cy, fz = oz - cz;
             const float hb = __builtin_fmaf(dz, fz, __builtin_fmaf(dy, fy, dx * fx));
             const float tc = -hb * ia;
@@ -1806,6 +1822,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
     const R4<R>* __restrict__ li = kWorld == kWorldLds ? s_li : p.sc.lights;
     R4<R>* l_li = nullptr;   // kWorldBvhLds: the light list in LDS
     R4<R>* l_lp = nullptr;   // kWorldBvhLds, f32: the light list as pairs in LDS
+    R4<float>* l_li32 = nullptr;   // kWorldBvhLds, f64: the lights rounded to f32 (light pre-pass)
     // World view of the closest-hit query.  kWorldBvhLds: the BVH nodes and
     // the leaf-ordered spheres + ids are copied into LDS once per workgroup
     // (after the traversal stacks), so traversal fetches go to the LDS
@@ -1845,6 +1862,13 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                 const R4<R> B = odd ? p.sc.lights[2 * q + 1] : R4<R>{0, 0, 0, 0};
                 l_lp[2 * q] = R4<R>{A.x, B.x, A.y, B.y};
                 l_lp[2 * q + 1] = R4<R>{A.z, B.z, A.w * A.w, odd ? B.w * B.w : (R)-INFINITY};
+            }
+        } else {
+            // the lights rounded to f32 with |radius| (the f32 pre-pass of lights_pdf_sum)
+            l_li32 = reinterpret_cast<R4<float>*>(l_li + p.sc.n_lights);
+            for (uint32_t k = threadIdx.x; k < p.sc.n_lights; k += kBlock) {
+                const R4<R> L = p.sc.lights[k];
+                l_li32[k] = R4<float>{(float)L.x, (float)L.y, (float)L.z, fabsf((float)L.w)};
             }
         }
         __syncthreads();
@@ -2396,6 +2420,8 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                                                             reinterpret_cast<int32_t*>(smem) + wave * p.stack * 64 + lane);
                     else if constexpr (kWorld == kWorldBvhLds && sizeof(R) == 4)
                         acc = lights_pdf_sum_pk<kRobust>(li, l_lp, kargs()->sc.n_lights, pnt, dir);
+                    else if constexpr (kWorld == kWorldBvhLds && sizeof(R) == 8)
+                        acc = lights_pdf_sum<kRobust>(li, kargs()->sc.n_lights, pnt, dir, l_li32);
                     else
                         acc = lights_pdf_sum<kRobust>(li, kargs()->sc.n_lights, pnt, dir);
                     RTW_PROBE_LIGHT_PDF();
