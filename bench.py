@@ -1,12 +1,15 @@
 #!/usr/bin/env python3
 """Benchmark of the hot path: Msamples/s of the reference's ray_colour loop on
 the Book-1 final scene (scenes::simple), BASELINE.json configs[1]:
-1200x800, 500 spp, max_depth 50, f32 arithmetic, one MI355X per rank.  The
-f32 kernel decides the reference's self-intersection coin flips in f64 (f64
-ray origin, own-sphere re-hit, hit t and point, Metal / Dielectric directions:
-tuning hit64 = 1, the default), which is what keeps it within the stated f32
-tolerance of DESIGN.md §2; `modes` adds the f64 parity mode (bit-identical to
-the oracle) and plain f32 (hit64 = 0) as secondary single-GPU lines.
+1200x800, 500 spp, max_depth 50, one MI355X per rank.  The headline runs the
+f64 parity mode -- the reference's own f64 arithmetic,
+bit-identical to the oracle, so the line is the creditable one;
+`modes` adds the f32 speed modes as secondary single-GPU lines: hit64 (f32
+with the reference's self-intersection decisions made in f64, within the
+stated statistical f32 tolerance of DESIGN.md §2b) and plain f32.
+`configs` adds BASELINE configs[2] (C3, 10k spheres, 1920x1080x1024 spp) and
+configs[4] on one GPU (C5, 1M spheres, 1920x1080x256 spp: the HBM/MALL
+roofline point), each in f64 and f32.
 
 A step = one full render of the image (every pixel x every sample) from the
 scene already resident in HBM; the image's 8x8 tiles are interleaved over
@@ -14,7 +17,12 @@ the ranks (tile T -> rank T % N), and for N > 1 the ranks' packed tiles are
 gathered to rank 0 over RCCL and un-interleaved there inside the step.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
-    torchrun --nproc-per-node N bench.py --gpus N ...
+    torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU)
+
+`--gpus N` > 1 without torchrun renders on N GPUs from this one process
+through the C-ABI's multi-device context (rtw_create_devices: one rank per
+GPU, one RCCL gather); it exits non-zero when fewer than N GPUs are visible,
+and under torchrun --gpus must equal WORLD_SIZE.
 
 Rank 0 prints ONE JSON line (see DESIGN.md §Measurement for every field).
 """
@@ -62,11 +70,15 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--precision", choices=["f32", "f64"], default="f32",
-                    help="f32: the headline speed mode (BASELINE configs[1]); f64: the parity mode, "
-                         "bit-identical to the oracle (FP64 roofline)")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0,
-                    help="target CPU time of the cpu_baseline sample")
+    ap.add_argument("--precision", choices=["f32", "f64"], default="f64",
+                    help="f64: the parity mode, the reference's arithmetic, bit-identical to the oracle "
+                         "(the headline; FP64 roofline); f32: the speed mode (hit64)")
+    ap.add_argument("--cpu-seconds", type=float, default=8.0,
+                    help="target CPU time of the cpu_baseline sample (reference-BVH leg; the cached-BVH "
+                         "leg gets a third of it)")
+    ap.add_argument("--configs", default="C3,C5",
+                    help="other BASELINE configs timed on one GPU after the headline (comma list of C3, "
+                         "C5; 'none' to skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-modes", action="store_true",
                     help="skip the secondary single-GPU lines (f64 parity mode, f32 without f64 hit points)")
@@ -163,12 +175,14 @@ def cpu_baseline(scene, target_s):
     sc = O.Scene(**scene.__dict__)
     res = {}
     for name, accel in (("bvh_ref", O.ACCEL_BVH_REF), ("bvh_cached", O.ACCEL_BVH_CACHED)):
-        # pilot: one row, 1/10 of the width, to size the sample
+        # pilot: one row, 1/10 of the width, to size the sample (the cached-BVH
+        # leg is informational: a third of the time)
+        tgt = target_s if name == "bvh_ref" else target_s / 3
         t0 = time.perf_counter()
         _, st = O.render(cam, sc, 99, accel=accel, threads=1, rows=(H // 2, H // 2 + 1, 1),
                          cols=(0, W // 10))
         per_sample = (time.perf_counter() - t0) / max(st.samples, 1)
-        rows = int(max(1, min(H, target_s * threads / (per_sample * W * SPP))))
+        rows = int(max(1, min(H, tgt * threads / (per_sample * W * SPP))))
         step = max(1, H // rows)
         t0 = time.perf_counter()
         img, st = O.render(cam, sc, 99, accel=accel, threads=threads, rows=(0, H, step))
@@ -203,9 +217,9 @@ def parity_on_sample(scene, oracle_rows, seed, ref_full):
     out = {"rows": len(rows), "pixels": len(rows) * W, "spp": SPP, "seed": seed}
     for name, prec in (("f64", rtw.RTW_F64), ("f32", rtw.RTW_F32)):
         with rtw.Renderer(device=torch.cuda.current_device(), precision=prec) as r:
-            # one sample per work item (chunk 1), so the per-pixel fold is the
-            # reference's sample-by-sample fold: f64 can be compared bit for bit
-            r.set_tuning("partial_max", 16 << 30)
+            # the library's defaults, as timed: one sample per work item (chunk 1,
+            # the chunk sums fit in the default partial_max), so the per-pixel
+            # fold is the reference's sample-by-sample fold and f64 compares bit for bit
             r.set_scene(scene)
             t0 = time.perf_counter()
             img = r.render(gcam, seed)[rows]
@@ -259,7 +273,7 @@ def mode_line(scene, cam, precision, tuning, steps, warmup, dev):
     rate = flops / (avg_ms * 1e-3) / 1e12
     line = {"value": round(W * H * SPP * steps / elapsed / 1e6, 3), "unit": "Msamples/s",
             "ms_per_step": round(elapsed / steps * 1e3, 3), "steps": steps, "warmup": warmup, "dtype": precision,
-            "tuning": tuning, "kernel": kname,
+            "tuning": tuning, "kernel": kname, "chunk": int(st.chunk),
             "kernel_ms_avg": round(avg_ms, 3),
             "roofline": {"bound": "valu", "achieved": round(rate, 3), "peak": peak, "unit": "TFLOP/s",
                          "frac": round(rate / peak, 4), "flops_per_launch": int(flops)},
@@ -332,54 +346,164 @@ def make_step(render, assemble, dist, rank, world_size, buf, gathered, image):
     return step
 
 
+CONFIGS = {   # BASELINE configs[2] and configs[4], one GPU each
+    "C3": dict(n=50, w=1920, h=1080, spp=1024, steps=2, warmup=1),
+    "C5": dict(n=500, w=1920, h=1080, spp=256, steps=1, warmup=1),
+}
+
+
+def config_line(name, precision, dev):
+    """BASELINE configs[2] / configs[4] on one GPU: the scenes::simple generator
+    over a 100 x 100 (C3, 10k spheres) or 1000 x 1000 (C5, 1M spheres) grid,
+    1920x1080, 1024 / 256 spp, depth 50; `steps` timed full renders after
+    `warmup` (the same run_steps as the headline).  C3's roofline is the VALU
+    (executed flops, as the headline); C5's is the memory system: the bytes the
+    traversal requests (node visits x node bytes + sphere tests x sphere bytes)
+    per launch over the kernel time, against 8 TB/s (SURVEY.md §8d "C5 is the
+    HBM/MALL point"); `traffic` is the PMC HBM bytes of an ISA-matched profile."""
+    cfg = CONFIGS[name]
+    prec = rtw.RTW_F32 if precision == "f32" else rtw.RTW_F64
+    tdtype = torch.float32 if prec == rtw.RTW_F32 else torch.float64
+    scene, b = rtw.scenes.simple_soa(SCENE_SEED, cfg["n"])
+    cam = b.with_image_width(cfg["w"]).with_image_height(cfg["h"]).with_samples_per_pixel(cfg["spp"]) \
+           .with_max_depth(DEPTH).build()
+    n_pl, n_li = len(scene.plane_mat), len(scene.lights)
+    with rtw.Renderer(device=dev.index, precision=prec) as r:
+        t0 = time.perf_counter()
+        r.set_scene(scene)
+        t_stage = time.perf_counter() - t0
+        buf = torch.empty((rtw.tiles_for_rank(cfg["w"], cfg["h"], 0, 1) * 64 * 3,), dtype=tdtype, device=dev)
+        stream = torch.cuda.current_stream(dev).cuda_stream
+
+        def step(seed):
+            r.render_device(cam, seed, buf.data_ptr(), buf.numel() * buf.element_size(), stream=stream)
+        elapsed = run_steps(step, cfg["steps"], cfg["warmup"], None, lambda: torch.cuda.synchronize(dev))
+        render_ms, _ = r.get_timings(cfg["steps"])
+        st = r.get_stats()
+        kname, sha = kernel_identity(r, precision)
+    avg_ms = float(np.mean(render_ms))
+    samples = cfg["w"] * cfg["h"] * cfg["spp"]
+    workload = f"{name}_simple_grid{2 * cfg['n']}_{cfg['w']}x{cfg['h']}_{cfg['spp']}spp_depth{DEPTH}"
+    line = {"value": round(samples * cfg["steps"] / elapsed / 1e6, 3), "unit": "Msamples/s",
+            "ms_per_step": round(elapsed / cfg["steps"] * 1e3, 3), "steps": cfg["steps"],
+            "warmup": cfg["warmup"], "dtype": precision, "n_gpus": 1,
+            "config": {"workload": workload, "spheres": len(scene.sphere_mat), "lights": n_li,
+                       "width": cfg["w"], "height": cfg["h"], "spp": cfg["spp"], "max_depth": DEPTH,
+                       "chunk": int(st.chunk)},
+            "kernel": kname, "kernel_ms_avg": round(avg_ms, 3), "scene_stage_s": round(t_stage, 3),
+            "segments_per_sample": round(st.segments / max(st.samples, 1), 4),
+            "node_visits_per_segment": round(st.node_visits / max(st.segments, 1), 3),
+            "sphere_tests_per_segment": round(st.sphere_tests / max(st.segments, 1), 3)}
+    if name == "C5":
+        # f32 nodes (both child boxes + links) in both precisions: the f64 kernels cull on the f32 tree;
+        # leaf spheres {c, r^2} f32 (+ the f64 sphere of a candidate in the parity mode)
+        node_b, sph_b = 64, (16 if prec == rtw.RTW_F32 else 16 + 32)
+        req = st.node_visits * node_b + st.sphere_tests * sph_b
+        rate = req / (avg_ms * 1e-3) / 1e9
+        line["roofline"] = {"bound": "hbm", "achieved": round(rate, 2), "peak": 8000.0, "unit": "GB/s",
+                            "frac": round(rate / 8000.0, 4), "bytes_per_launch": int(req),
+                            "basis": f"traversal requests: node visits x {node_b} B + sphere tests x {sph_b} B "
+                                     "(served by L2 / MALL: the 36 MB working set fits the 256 MB MALL)"}
+        attach_pmc(line["roofline"], workload, kname, sha)
+    else:
+        flops = exe_flops_of(st, n_pl, n_li)
+        peak = PEAK_FP32_TFLOPS if prec == rtw.RTW_F32 else PEAK_FP64_TFLOPS
+        rate = flops / (avg_ms * 1e-3) / 1e12
+        line["roofline"] = {"bound": "valu", "achieved": round(rate, 3), "peak": peak, "unit": "TFLOP/s",
+                            "frac": round(rate / peak, 4), "flops_per_launch": int(flops)}
+        attach_pmc(line["roofline"], workload, kname, sha)
+    return line
+
+
+def resolve_launch(gpus, env, visible):
+    """How this run spreads over GPUs: ("torchrun", N) -- one process per GPU,
+    the driver's N > 1 launch (WORLD_SIZE set; --gpus must equal it),
+    ("inproc", N) -- N > 1 GPUs from this one process through the C-ABI's
+    multi-device context (needs N visible GPUs), or ("single", 1).  Raises
+    SystemExit (non-zero) instead of silently timing fewer GPUs than asked."""
+    ws = env.get("WORLD_SIZE")
+    if ws is not None and int(ws) > 1:
+        if gpus != int(ws):
+            raise SystemExit(f"bench.py: --gpus {gpus} but WORLD_SIZE={ws} (torchrun): they must agree")
+        return "torchrun", int(ws)
+    if gpus < 1:
+        raise SystemExit(f"bench.py: --gpus {gpus}: at least one GPU")
+    if gpus > 1:
+        if visible < gpus:
+            raise SystemExit(f"bench.py: --gpus {gpus} but only {visible} GPU(s) visible")
+        return "inproc", gpus
+    return "single", 1
+
+
 def main():
     a = parse()
-    world_size = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    launch, world_size = resolve_launch(a.gpus, os.environ, torch.cuda.device_count())
+    rank = int(os.environ.get("RANK", "0")) if launch == "torchrun" else 0
+    local_rank = int(os.environ.get("LOCAL_RANK", "0")) if launch == "torchrun" else 0
     dist = None
-    if world_size > 1:
+    if launch == "torchrun":
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local_rank}"))
     else:
         torch.cuda.set_device(0)
-    dev = torch.device(f"cuda:{local_rank if world_size > 1 else 0}")
+    dev = torch.device(f"cuda:{local_rank}")
     prec = rtw.RTW_F32 if a.precision == "f32" else rtw.RTW_F64
     tdtype = torch.float32 if prec == rtw.RTW_F32 else torch.float64
 
     scene, builder = rtw.scenes.simple_soa(SCENE_SEED)
     cam = builder.with_image_width(W).with_image_height(H).with_samples_per_pixel(SPP) \
                  .with_max_depth(DEPTH).build()
-    r = rtw.Renderer(device=dev.index, precision=prec)
+    r = rtw.Renderer(device=dev.index, precision=prec,
+                     devices=list(range(world_size)) if launch == "inproc" else None)
     r.set_accel({"auto": rtw.RTW_ACCEL_AUTO, "brute": rtw.RTW_ACCEL_BRUTE, "bvh": rtw.RTW_ACCEL_BVH}[a.accel])
     for kv in filter(None, a.tuning.split(",")):
         k, v = kv.split("=")
         r.set_tuning(k, int(v))
     r.set_scene(scene)
     assert rtw.tile_size() == sharding.TILE
-    # equal-size packed tile buffers (rank 0 holds the most tiles), as the gather needs
-    max_tiles = rtw.tiles_for_rank(W, H, 0, world_size)
-    buf = torch.zeros((max_tiles * 64 * 3,), dtype=tdtype, device=dev)
-    gathered = torch.empty((world_size, buf.numel()), dtype=tdtype, device=dev) if (dist and rank == 0) else None
     image = torch.empty((H, W, 3), dtype=tdtype, device=dev) if rank == 0 else None
     stream = torch.cuda.current_stream(dev).cuda_stream
+    if launch == "inproc":
+        # every GPU renders its tiles, one RCCL gather to GPU 0, assembled there:
+        # all inside rtw_render_image_device (the drop-in's multi-device path)
+        def step(seed):
+            r.render_image_device(cam, seed, image.data_ptr(), image.numel() * image.element_size(),
+                                  stream=stream)
 
-    def render(seed, out):
-        r.render_device(cam, seed, out.data_ptr(), out.numel() * out.element_size(),
-                        rank=rank, nranks=world_size, stream=stream)
+        def sync():
+            for k in range(world_size):
+                torch.cuda.synchronize(k)
+    else:
+        # equal-size packed tile buffers (rank 0 holds the most tiles), as the gather needs
+        max_tiles = rtw.tiles_for_rank(W, H, 0, world_size)
+        buf = torch.zeros((max_tiles * 64 * 3,), dtype=tdtype, device=dev)
+        gathered = torch.empty((world_size, buf.numel()), dtype=tdtype, device=dev) if (dist and rank == 0) else None
 
-    def assemble(ranks, img):
-        r.assemble_tiles(ranks.data_ptr(), ranks.stride(0) * ranks.element_size(), ranks.shape[0], W, H,
-                         img.data_ptr(), stream=stream)
+        def render(seed, out):
+            r.render_device(cam, seed, out.data_ptr(), out.numel() * out.element_size(),
+                            rank=rank, nranks=world_size, stream=stream)
 
-    step = make_step(render, assemble, dist, rank, world_size, buf, gathered, image)
-    elapsed = run_steps(step, a.steps, a.warmup, dist, lambda: torch.cuda.synchronize(dev), device=dev)
+        def assemble(ranks, img):
+            r.assemble_tiles(ranks.data_ptr(), ranks.stride(0) * ranks.element_size(), ranks.shape[0], W, H,
+                             img.data_ptr(), stream=stream)
 
-    # live per-launch kernel times of the timed steps (HIP events on `stream`)
-    render_ms, total_ms = r.get_timings(a.steps)
-    st = r.get_stats()
+        step = make_step(render, assemble, dist, rank, world_size, buf, gathered, image)
+
+        def sync():
+            torch.cuda.synchronize(dev)
+    elapsed = run_steps(step, a.steps, a.warmup, dist, sync, device=dev)
+
+    # live per-launch kernel times of the timed steps (HIP events on the launch
+    # stream) and the counters, of rank 0 (the in-process path: its first device)
+    r0 = r.rank_view(0) if launch == "inproc" else r
+    render_ms, total_ms = r0.get_timings(a.steps)
+    st = r0.get_stats()
+    per_rank_ms = None
+    if launch == "inproc":
+        per_rank_ms = [round(float(np.mean(r.rank_view(k).get_timings(a.steps)[0])), 3)
+                       for k in range(world_size)]
     samples_total = W * H * SPP * a.steps
     value = samples_total / elapsed / 1e6
     ms_per_step = elapsed / a.steps * 1e3
@@ -399,7 +523,7 @@ def main():
     alg_rate = alg_flops / (avg_ms * 1e-3) / 1e12
     exe_rate = exe_flops / (avg_ms * 1e-3) / 1e12
     peak = PEAK_FP32_TFLOPS if prec == rtw.RTW_F32 else PEAK_FP64_TFLOPS
-    kname, sha = kernel_identity(r, a.precision)
+    kname, sha = kernel_identity(r0, a.precision)
     out = {
         "metric": "Msamples/s (pixels x spp) on Book-1 final scene",
         "value": round(value, 3),
@@ -417,10 +541,15 @@ def main():
         "config": {"workload": f"book1_simple_{W}x{H}_{SPP}spp_depth{DEPTH}", "width": W,
                    "height": H, "spp": SPP, "max_depth": DEPTH, "spheres": n_sph,
                    "lights": n_li, "parallelism": f"tile8x8_interleave{world_size}",
+                   "launch": {"torchrun": "one process per GPU (torch.distributed, RCCL gather)",
+                              "inproc": "one process, rtw_create_devices (one rank per GPU, RCCL gather)",
+                              "single": "one GPU"}[launch],
                    "accel": accel if accel != "bvh" else f"bvh{int(st.bvh_width)}",
                    "chunk": int(st.chunk),
-                   "arithmetic": "f32, self-intersection decided in f64 (hit64)" if a.precision == "f32" and
-                   "hit64=0" not in a.tuning else a.precision},
+                   "arithmetic": ("f64, the reference's operation order (bit-identical to the oracle)"
+                                  if a.precision == "f64" else
+                                  "f32, self-intersection decided in f64 (hit64)" if "hit64=0" not in a.tuning
+                                  else "f32")},
         "roofline": {"bound": "valu", "achieved": round(exe_rate, 3), "peak": peak,
                      "unit": "TFLOP/s", "frac": round(exe_rate / peak, 4),
                      "kernel": kname,
@@ -438,13 +567,23 @@ def main():
                      "sphere_tests_per_segment": round(st.sphere_tests / max(st.segments, 1), 3),
                      "lambertian_per_sample": round(st.lambertian / max(st.samples, 1), 4)},
     }
+    if per_rank_ms is not None:
+        out["roofline"]["kernel_ms_per_rank"] = per_rank_ms
     attach_pmc(out["roofline"], out["config"]["workload"], kname, sha)
     if world_size == 1 and not a.no_modes:
         # the same workload in the other arithmetic modes (single GPU, after the timed region)
-        out["modes"] = {"f64_parity": mode_line(scene, cam, "f64", {}, a.steps, a.warmup, dev)}
+        out["modes"] = {}
         if a.precision == "f32":
-            out["modes"]["f32_plain"] = mode_line(scene, cam, "f32", {"hit64": 0}, a.steps, a.warmup, dev)
+            out["modes"]["f64_parity"] = mode_line(scene, cam, "f64", {}, a.steps, a.warmup, dev)
+        else:
+            out["modes"]["f32_hit64"] = mode_line(scene, cam, "f32", {}, a.steps, a.warmup, dev)
+        out["modes"]["f32_plain"] = mode_line(scene, cam, "f32", {"hit64": 0}, a.steps, a.warmup, dev)
         out["cold_render"] = cold_render(scene, cam, prec, dev)
+    if world_size == 1 and a.configs != "none":
+        out["configs"] = {}
+        for name in filter(None, a.configs.split(",")):
+            for p in (a.precision, "f32" if a.precision == "f64" else "f64"):
+                out["configs"][f"{name}_{p}"] = config_line(name, p, dev)
     if world_size == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(scene, a.cpu_seconds)
     print(json.dumps(out), flush=True)

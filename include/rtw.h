@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define RTW_ABI_VERSION 7
+#define RTW_ABI_VERSION 8
 
 /* error codes */
 #define RTW_OK 0
@@ -182,7 +182,33 @@ typedef struct rtw_ctx rtw_ctx;
 
 /* ---- context ---------------------------------------------------------- */
 int rtw_abi_version(void);
+/* A context on one GPU (HIP device index `device`). */
 rtw_ctx *rtw_create(int device, int precision);
+/* A context over several GPUs of this node: SURVEY.md §8(b)(1)'s
+ * rtw_create(device_mask, precision), the drop-in for render_internal's use of
+ * every host core (camera.rs:340-353: one rayon task per pixel over the
+ * global pool) -- here one rank per GPU, all in the calling process.
+ * devices[k] is rank k's HIP device; rank k renders the 8x8 tiles
+ * T = k (mod n_devices) (rtw_tiles_for_rank), and ONE RCCL gather
+ * (ncclGather, rccl.h:745-746, a single-process clique from ncclCommInitAll)
+ * brings the ranks' packed tiles to rank 0's device, which un-interleaves them
+ * (rtw_assemble_tiles).  Every knob (rtw_set_tuning / rtw_set_chunk /
+ * rtw_set_accel) and the scene (rtw_set_scene, staged once) apply to all
+ * ranks; rtw_render and rtw_render_image_device render on all of them, and
+ * the image is bit-identical to a one-GPU render of the same seed.
+ * RTW_E_INVALID: NULL / empty list, a negative, repeated or not visible
+ * device (checked before any HIP call for the first two); RTW_E_DEVICE: a HIP
+ * or RCCL failure (RCCL is loaded at run time: librccl.so.1). */
+int rtw_create_devices(const int *devices, uint32_t n_devices, int precision, rtw_ctx **out);
+/* The same over the devices whose bits are set (bit k = HIP device k, in
+ * increasing order); NULL on error (an empty mask included). */
+rtw_ctx *rtw_create_mask(uint64_t device_mask, int precision);
+/* Ranks of a context (1 for rtw_create), and rank k's per-device context
+ * (k = 0: ctx itself) for rtw_get_stats / rtw_get_timings / rtw_last_kernel
+ * of that rank; owned by ctx (do not destroy).  rtw_device_of: its HIP device. */
+uint32_t rtw_device_count(const rtw_ctx *ctx);
+rtw_ctx *rtw_device_ctx(rtw_ctx *ctx, uint32_t k);
+int rtw_device_of(const rtw_ctx *ctx);
 void rtw_destroy(rtw_ctx *ctx);
 const char *rtw_last_error(const rtw_ctx *ctx);
 int rtw_precision(const rtw_ctx *ctx);
@@ -217,7 +243,7 @@ int rtw_set_accel(rtw_ctx *ctx, int accel);
  * "max_group" (longest-first task list: at most this many chunks per task, default 32),
  * "grid_piece" (f32 light-grid walks: cells per piece of the wave's cooperative walk,
  * default by grid size: its widest side / 14, 4..16; 0 = every lane walks its own ray),
- * "light_leaf" (light spheres per light-BVH leaf, 1..15; 0 = 4), "partial_max" (bytes of chunk sums an auto chunk may use, default 8 GiB),
+ * "light_leaf" (light spheres per light-BVH leaf, 1..15; 0 = 4), "partial_max" (bytes of chunk sums an auto chunk may use, default 24 GiB),
  * "bvh_kind" (3 = binary while-while on the tree staged in LDS, the
  * default, 1 = binary while-while from L1/L2, 2 = 4-wide octant BVH, 0 =
  * binary single loop), "bvh_lds_max" (LDS bytes per workgroup bvh_kind 3 may
@@ -236,9 +262,20 @@ int rtw_set_scene(rtw_ctx *ctx, const rtw_scene *scene);
 
 /* ---- Camera::render (camera.rs:295-297) ------------------------------- */
 /* Synchronous drop-in: uploads `scene` (if non-NULL), renders every pixel and
- * writes H*W*3 doubles (sums, j = 0 bottom row) to host `out_sum`. */
+ * writes H*W*3 doubles (sums, j = 0 bottom row) to host `out_sum`.  On a
+ * multi-device context every GPU renders its share (rtw_create_devices);
+ * `stats` then sums the ranks' counters (kernel_ms: the slowest rank). */
 int rtw_render(rtw_ctx *ctx, const rtw_camera *cam, const rtw_scene *scene,
                uint64_t seed, double *out_sum, rtw_stats *stats);
+
+/* The whole image into device memory of the context's first device: d_image
+ * holds H*W*3 elements of the context's precision (sums, j = 0 bottom row).
+ * Asynchronous on `stream` (a hipStream_t of that device; NULL = the
+ * context's own): rank 0 renders on it, the other ranks on their own
+ * streams; the RCCL gather and the assembly are ordered on `stream` after
+ * every rank's render, so work queued on `stream` afterwards sees the image. */
+int rtw_render_image_device(rtw_ctx *ctx, const rtw_camera *cam, uint64_t seed, void *d_image,
+                            size_t image_bytes, void *stream);
 
 /* Device-resident form for benchmarking and multi-GPU sharding.
  * The image is cut into 8x8 tiles T = ty * tiles_x + tx (tiles_x = ceil(W/8),
@@ -253,7 +290,9 @@ int rtw_render(rtw_ctx *ctx, const rtw_camera *cam, const rtw_scene *scene,
  * inside, except once per (scene, camera, rank split) when tuning "lpt" is on
  * and spp >= "lpt_min_spp": the second render of the key waits for the first,
  * whose tile costs order its tasks, and reads them back (then cached; with
- * "lpt_inline" 0 the first render runs and reads back a 2-spp pilot instead). */
+ * "lpt_inline" 0 the first render runs and reads back a 2-spp pilot instead).
+ * On a multi-device context it renders on the first device only (each rank's
+ * context: rtw_device_ctx). */
 int rtw_render_device(rtw_ctx *ctx, const rtw_camera *cam, uint64_t seed,
                       uint32_t rank, uint32_t nranks, void *d_out, size_t out_bytes,
                       void *stream);

@@ -471,12 +471,14 @@ class Camera:
         return tuple(v) if isinstance(v, C.Array) else v
 
     def render(self, world, lights, *, seed: int = 0x5EED0001, precision: int = RTW_F64,
-               device: int = 0, accel: int = RTW_ACCEL_AUTO) -> np.ndarray:
+               device: int = 0, devices=None, accel: int = RTW_ACCEL_AUTO) -> np.ndarray:
         """Camera::render (camera.rs:295-297) on the GPU: float64 sums [H, W, 3].
         The default is the parity mode (RTW_F64: the reference's f64 arithmetic,
         bit-identical to the oracle); precision=RTW_F32 opts into the faster
-        speed mode, which agrees with the reference statistically."""
-        with Renderer(device=device, precision=precision) as r:
+        speed mode, which agrees with the reference statistically.
+        `devices` (a list of GPU indices) renders on all of them, one rank each
+        (rtw_create_devices) -- the same image bit for bit."""
+        with Renderer(device=device, precision=precision, devices=devices) as r:
             r.set_accel(accel)
             r.set_scene(flatten(world, lights))
             return r.render(self, seed)
@@ -485,16 +487,40 @@ class Camera:
 
 
 class Renderer:
-    """An rtw_ctx: a device, a precision, a resident scene and work buffers."""
+    """An rtw_ctx: a device (or, with `devices`, one rank per listed GPU:
+    rtw_create_devices), a precision, a resident scene and work buffers."""
 
-    def __init__(self, device: int = 0, precision: int = RTW_F32):
-        self.ctx = _lib.rtw_create(device, precision)
-        if not self.ctx:
-            raise RenderError(_capi.RTW_E_DEVICE, f"rtw_create(device={device}) failed: no gfx950 "
-                              "device visible (this library has no CPU path)")
+    def __init__(self, device: int = 0, precision: int = RTW_F32, *, devices=None):
+        self.ctx = None
+        if devices is not None:
+            devs = [int(d) for d in devices]
+            arr = (C.c_int * max(len(devs), 1))(*devs)
+            out = C.c_void_p()
+            rc = _lib.rtw_create_devices(arr, len(devs), precision, C.byref(out))
+            if rc != 0:
+                raise RenderError(rc, f"rtw_create_devices({devs}) failed (code {rc}): an empty, repeated "
+                                  "or not visible device, or a HIP / RCCL failure")
+            self.ctx = out.value
+            device = devs[0]
+        else:
+            self.ctx = _lib.rtw_create(device, precision)
+            if not self.ctx:
+                raise RenderError(_capi.RTW_E_DEVICE, f"rtw_create(device={device}) failed: no gfx950 "
+                                  "device visible (this library has no CPU path)")
         self.device = device
         self.precision = precision
         self.stats = _capi.rtw_stats()
+
+    @property
+    def n_devices(self) -> int:
+        return int(_lib.rtw_device_count(self.ctx))
+
+    def rank_view(self, k: int) -> "_RankView":
+        """Rank k's per-device context (stats / timings / last kernel)."""
+        sub = _lib.rtw_device_ctx(self.ctx, k)
+        if not sub:
+            raise RenderError(_capi.RTW_E_INVALID, f"no rank {k}")
+        return _RankView(sub, int(_lib.rtw_device_of(sub)), self.precision)
 
     def close(self):
         if self.ctx:
@@ -548,6 +574,19 @@ class Renderer:
                                            C.c_void_p(stream) if stream else None),
                     "rtw_render_device")
 
+    def render_image_device(self, cam: Camera, seed: int, image_ptr: int, image_bytes: int, *,
+                            stream: int | None = None):
+        """Asynchronous render of the whole image [H, W, 3] into device memory
+        of the first device (rtw_render_image_device): every device of the
+        context renders its share, one RCCL gather, the assembly on `stream`
+        (torch's current stream of the first device by default)."""
+        if stream is None:
+            stream = _torch_stream(self.device)
+        self._check(_lib.rtw_render_image_device(self.ctx, C.byref(cam.raw), C.c_uint64(seed),
+                                                 C.c_void_p(image_ptr) if image_ptr else None, image_bytes,
+                                                 C.c_void_p(stream) if stream else None),
+                    "rtw_render_image_device")
+
     def assemble_tiles(self, ranks_ptr: int, rank_stride_bytes: int, nranks: int, width: int,
                        height: int, image_ptr: int, *, stream: int | None = None):
         """The ranks' gathered packed tiles -> the image [H, W, 3] on the device
@@ -578,6 +617,21 @@ class Renderer:
     def get_stats(self) -> "_capi.rtw_stats":
         self._check(_lib.rtw_get_stats(self.ctx, C.byref(self.stats)), "rtw_get_stats")
         return self.stats
+
+
+class _RankView(Renderer):
+    """One rank of a multi-device Renderer (not owned: close() is a no-op)."""
+
+    def __init__(self, ctx, device, precision):   # noqa: D107  (no rtw_create)
+        self.ctx = ctx
+        self.device = device
+        self.precision = precision
+        self.stats = _capi.rtw_stats()
+
+    def close(self):
+        self.ctx = None
+
+    __del__ = close
 
 
 def tiles_for_rank(width: int, height: int, rank: int, nranks: int) -> int:

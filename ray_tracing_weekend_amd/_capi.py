@@ -67,7 +67,7 @@ class rtw_scene(C.Structure):
     ]
 
 
-ABI_VERSION = 7     # RTW_ABI_VERSION of include/rtw.h
+ABI_VERSION = 8     # RTW_ABI_VERSION of include/rtw.h
 
 
 class rtw_stats(C.Structure):
@@ -84,6 +84,11 @@ class rtw_stats(C.Structure):
 PROTOTYPES = [
     ("rtw_abi_version", C.c_int, []),
     ("rtw_create", C.c_void_p, [C.c_int, C.c_int]),
+    ("rtw_create_devices", C.c_int, [C.POINTER(C.c_int), C.c_uint32, C.c_int, C.POINTER(C.c_void_p)]),
+    ("rtw_create_mask", C.c_void_p, [C.c_uint64, C.c_int]),
+    ("rtw_device_count", C.c_uint32, [C.c_void_p]),
+    ("rtw_device_ctx", C.c_void_p, [C.c_void_p, C.c_uint32]),
+    ("rtw_device_of", C.c_int, [C.c_void_p]),
     ("rtw_destroy", None, [C.c_void_p]),
     ("rtw_last_error", C.c_char_p, [C.c_void_p]),
     ("rtw_precision", C.c_int, [C.c_void_p]),
@@ -95,6 +100,8 @@ PROTOTYPES = [
     ("rtw_set_scene", C.c_int, [C.c_void_p, C.POINTER(rtw_scene)]),
     ("rtw_render", C.c_int, [C.c_void_p, C.POINTER(rtw_camera), C.POINTER(rtw_scene), C.c_uint64,
                              _f64p, C.POINTER(rtw_stats)]),
+    ("rtw_render_image_device", C.c_int, [C.c_void_p, C.POINTER(rtw_camera), C.c_uint64, C.c_void_p,
+                                          C.c_size_t, C.c_void_p]),
     ("rtw_render_device", C.c_int, [C.c_void_p, C.POINTER(rtw_camera), C.c_uint64, C.c_uint32,
                                     C.c_uint32, C.c_void_p, C.c_size_t, C.c_void_p]),
     ("rtw_tile_size", C.c_uint32, []),

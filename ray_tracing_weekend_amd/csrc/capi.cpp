@@ -1,7 +1,9 @@
 // capi.cpp -- the C-ABI (include/rtw.h): context, scene upload, CameraBuilder::
 // build, the render entry points, scenes::simple and the PPM encoding.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <math.h>
+#include <rccl/rccl.h>   // types only: the functions are resolved at run time (rccl_api)
 #include <stddef.h>
 #include <stdio.h>
 #include <string.h>
@@ -9,6 +11,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cstdlib>
+#include <mutex>
 #include <new>
 #include <type_traits>
 #include <string>
@@ -26,7 +29,10 @@ struct rtw_ctx {
     uint32_t chunk = 0;           // samples per item (0 = auto_chunk)
     uint32_t auto_chunk = 1;      // one sample per item: the chunk fold is then the reference's
                                   // sample-by-sample fold exactly
-    size_t partial_max = (size_t)8 << 30;   // cap of the chunk-sum buffer (auto chunk grows)
+    // cap of the chunk-sum buffer (the auto chunk grows beyond it): 24 GiB of the
+    // 288 GB of HBM keeps every one-GPU BASELINE config at one sample per item --
+    // the reference's fold order exactly (C2 f64: 11.5 GB)
+    size_t partial_max = (size_t)24 << 30;
     uint32_t group = 0;           // chunks per wave task (0 = from target_tasks)
     uint64_t target_tasks = 0;   // auto chunks-per-task: about this many tasks (0: 2^19 with
                                  // persistent waves, 2^17 without), 4..32 chunks per task
@@ -116,6 +122,15 @@ struct rtw_ctx {
     int last_variant = 0;             // render kernel of the last render: launch_render_impl's code
     uint32_t last_n_sph = 0;
     std::string err;
+    // multi-device context (rtw_create_devices): this context is rank 0 on the
+    // first device; peers[k - 1] is the context of rank k on device k of the
+    // list, mirroring every knob and the scene.  One RCCL communicator per rank
+    // (a single-process clique) for the framebuffer gather to rank 0.
+    bool multi = false;
+    std::vector<rtw_ctx*> peers;
+    std::vector<ncclComm_t> comms;
+    void* d_gather = nullptr;         // rank 0's device: the n ranks' packed tiles (gather target)
+    size_t gather_cap = 0;
 };
 
 namespace {
@@ -138,6 +153,52 @@ int hip_fail(rtw_ctx* c, hipError_t e, const char* what) {
     } while (0)
 
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+// RCCL for the multi-device gather, resolved at the first multi-device
+// context: dlopen by SONAME, so a process that already holds PyTorch's
+// librccl.so.1 shares that copy (one RCCL per process); a plain C caller gets
+// ROCm's.  Single-device contexts never load it.
+struct RcclApi {
+    bool ok = false;
+    std::string err;
+    ncclResult_t (*comm_init_all)(ncclComm_t*, int, const int*) = nullptr;
+    ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*gather)(const void*, void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*group_start)() = nullptr;
+    ncclResult_t (*group_end)() = nullptr;
+    const char* (*error_string)(ncclResult_t) = nullptr;
+};
+
+const RcclApi& rccl_api() {
+    static RcclApi api;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        void* h = nullptr;
+        for (const char* name : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"})
+            if ((h = dlopen(name, RTLD_NOW | RTLD_GLOBAL)) != nullptr) break;
+        if (!h) {
+            api.err = std::string("cannot load librccl.so.1: ") + dlerror();
+            return;
+        }
+        auto sym = [&](auto& fn, const char* name) {
+            fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(dlsym(h, name));
+            if (!fn && api.err.empty()) api.err = std::string("librccl.so.1 lacks ") + name;
+        };
+        sym(api.comm_init_all, "ncclCommInitAll");
+        sym(api.comm_destroy, "ncclCommDestroy");
+        sym(api.gather, "ncclGather");
+        sym(api.group_start, "ncclGroupStart");
+        sym(api.group_end, "ncclGroupEnd");
+        sym(api.error_string, "ncclGetErrorString");
+        api.ok = api.err.empty();
+    });
+    return api;
+}
+
+int rccl_fail(rtw_ctx* c, ncclResult_t r, const char* what) {
+    const RcclApi& a = rccl_api();
+    return fail(c, RTW_E_DEVICE, std::string(what) + ": " + (a.error_string ? a.error_string(r) : "RCCL error"));
+}
 
 // Quad::new (quadrilateral.rs:37-56) in f64, in the oracle's operation order
 // (rtw_oracle.c quad_new): out = {Q, u, v, w, normal, area, box lo, box hi}.
@@ -1005,17 +1066,21 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
             c->lpt_prec = (uint32_t)sizeof(R);
         };
         if (!same && c->lpt_inline) {
-            // this render counts its tiles' costs on the way (plain tile order)
+            // this render counts its tiles' costs on the way (plain tile order);
+            // the key is kept and the counts marked pending only once lpt_ev is
+            // recorded after the launch (below), so a failed launch leaves no
+            // pending state behind
             c->lpt_valid = c->lpt_pending = false;
             c->lpt_tab_valid = false;
             const uint32_t nt = p.n_local_tiles;
+            // a counting render of an earlier key may still run on another stream:
+            // the counters are reused only after it
+            if (c->lpt_ev) HIP_TRY(c, hipStreamWaitEvent(stream, c->lpt_ev, 0));
             rc = ensure(c, &c->d_lpt, &c->lpt_cap, align_up((size_t)nt, 64) * sizeof(uint32_t));
             if (rc) return rc;
             HIP_TRY(c, hipMemsetAsync(c->d_lpt, 0, (size_t)nt * sizeof(uint32_t), stream));
             p.tile_cost = reinterpret_cast<uint32_t*>(c->d_lpt);
             p.cost_spp = std::min(p.spp, std::max(c->lpt_pilot_spp, 1u));
-            keep_key();
-            c->lpt_pending = true;   // read back by the next render of the same key (after lpt_ev)
         } else if (!same) {
             c->lpt_valid = c->lpt_pending = false;
             c->lpt_tab_valid = false;
@@ -1030,10 +1095,13 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
         } else if (c->lpt_pending) {
             // the counts of the render before (waits for it: once per key)
             const uint32_t nt = p.n_local_tiles;
+            c->lpt_pending = false;   // (an error below recounts at the next render)
             HIP_TRY(c, hipEventSynchronize(c->lpt_ev));
             c->h_lpt_cost.resize(nt);
-            HIP_TRY(c, hipMemcpy(c->h_lpt_cost.data(), c->d_lpt, (size_t)nt * sizeof(uint32_t), hipMemcpyDeviceToHost));
-            c->lpt_pending = false;
+            // on the context's own (idle, non-blocking) stream: waits for nothing but the copy
+            HIP_TRY(c, hipMemcpyAsync(c->h_lpt_cost.data(), c->d_lpt, (size_t)nt * sizeof(uint32_t),
+                                      hipMemcpyDeviceToHost, c->stream));
+            HIP_TRY(c, hipStreamSynchronize(c->stream));
             c->lpt_valid = true;
             if (dbg) fprintf(stderr, "lpt counts read back %.3f ms (%u tiles)\n",
                              std::chrono::duration<double, std::milli>(now() - t0).count(), nt);
@@ -1077,6 +1145,12 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
     if (p.tile_cost) {   // the counts are complete after this render
         if (!c->lpt_ev) HIP_TRY(c, hipEventCreateWithFlags(&c->lpt_ev, hipEventDisableTiming));
         HIP_TRY(c, hipEventRecord(c->lpt_ev, stream));
+        c->lpt_cam = *cam;   // read back by the next render of the same key (after lpt_ev)
+        c->lpt_serial = c->scene_serial;
+        c->lpt_rank = rank;
+        c->lpt_nranks = nranks;
+        c->lpt_prec = (uint32_t)sizeof(R);
+        c->lpt_pending = true;
     }
     HIP_TRY(c, hipEventRecord(c->ev1, stream));
     HIP_TRY(c, hipEventRecord(ev[2], stream));
@@ -1122,9 +1196,83 @@ rtw_ctx* rtw_create(int device, int precision) {
     return c;
 }
 
+int rtw_create_devices(const int* devices, uint32_t n_devices, int precision, rtw_ctx** out) {
+    if (!out) return RTW_E_INVALID;
+    *out = nullptr;
+    if (!devices || n_devices == 0 || (precision != RTW_F32 && precision != RTW_F64)) return RTW_E_INVALID;
+    // the device list is checked before any HIP call: no negative or repeated
+    // device (one rank per GPU: a repeated device would render its tiles twice
+    // and RCCL rejects a clique with a duplicate device)
+    for (uint32_t a = 0; a < n_devices; ++a) {
+        if (devices[a] < 0) return RTW_E_INVALID;
+        for (uint32_t b = 0; b < a; ++b)
+            if (devices[a] == devices[b]) return RTW_E_INVALID;
+    }
+    int visible = 0;
+    if (hipGetDeviceCount(&visible) != hipSuccess) return RTW_E_DEVICE;
+    for (uint32_t a = 0; a < n_devices; ++a)
+        if (devices[a] >= visible) return RTW_E_INVALID;
+    const RcclApi& api = rccl_api();
+    if (!api.ok) return RTW_E_DEVICE;
+    rtw_ctx* c = rtw_create(devices[0], precision);
+    if (!c) return RTW_E_DEVICE;
+    c->multi = true;
+    for (uint32_t k = 1; k < n_devices; ++k) {
+        rtw_ctx* pk = rtw_create(devices[k], precision);
+        if (!pk) {
+            rtw_destroy(c);
+            return RTW_E_DEVICE;
+        }
+        c->peers.push_back(pk);
+    }
+    c->comms.assign(n_devices, nullptr);
+    const std::vector<int> list(devices, devices + n_devices);
+    if (api.comm_init_all(c->comms.data(), (int)n_devices, list.data()) != ncclSuccess) {
+        c->comms.clear();
+        rtw_destroy(c);
+        return RTW_E_DEVICE;
+    }
+    (void)hipSetDevice(devices[0]);
+    *out = c;
+    return RTW_OK;
+}
+
+rtw_ctx* rtw_create_mask(uint64_t device_mask, int precision) {
+    std::vector<int> list;
+    for (int k = 0; k < 64; ++k)
+        if ((device_mask >> k) & 1u) list.push_back(k);
+    rtw_ctx* c = nullptr;
+    if (list.empty()) return nullptr;
+    return rtw_create_devices(list.data(), (uint32_t)list.size(), precision, &c) == RTW_OK ? c : nullptr;
+}
+
+uint32_t rtw_device_count(const rtw_ctx* c) { return c ? 1u + (uint32_t)c->peers.size() : 0u; }
+
+rtw_ctx* rtw_device_ctx(rtw_ctx* c, uint32_t k) {
+    if (!c) return nullptr;
+    if (k == 0) return c;
+    return k <= c->peers.size() ? c->peers[k - 1] : nullptr;
+}
+
+int rtw_device_of(const rtw_ctx* c) { return c ? c->device : RTW_E_INVALID; }
+
 void rtw_destroy(rtw_ctx* c) {
     if (!c) return;
+    if (!c->comms.empty()) {
+        // the gathers may still run on any rank's stream (rank 0's is the caller's)
+        for (uint32_t k = 0; k < rtw_device_count(c); ++k) {
+            (void)hipSetDevice(rtw_device_ctx(c, k)->device);
+            (void)hipDeviceSynchronize();
+        }
+        const RcclApi& api = rccl_api();
+        for (ncclComm_t m : c->comms)
+            if (m && api.comm_destroy) (void)api.comm_destroy(m);
+        c->comms.clear();
+    }
+    for (rtw_ctx* pk : c->peers) rtw_destroy(pk);
+    c->peers.clear();
     (void)hipSetDevice(c->device);
+    if (c->d_gather) (void)hipFree(c->d_gather);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->d_scene) (void)hipFree(c->d_scene);
     if (c->d_partial) (void)hipFree(c->d_partial);
@@ -1149,10 +1297,15 @@ int rtw_precision(const rtw_ctx* c) { return c ? c->precision : -1; }
 int rtw_set_chunk(rtw_ctx* c, uint32_t chunk) {
     if (!c) return RTW_E_INVALID;
     c->chunk = chunk;
+    for (rtw_ctx* pk : c->peers) pk->chunk = chunk;   // (multi-device: every rank alike)
     return RTW_OK;
 }
 int rtw_set_tuning(rtw_ctx* c, const char* key, int64_t value) {
     if (!c || !key) return RTW_E_INVALID;
+    for (rtw_ctx* pk : c->peers) {   // multi-device: every rank alike
+        const int rc = rtw_set_tuning(pk, key, value);
+        if (rc) return fail(c, rc, pk->err);
+    }
     const std::string k = key;
     if (value < 0) return fail(c, RTW_E_INVALID, "negative tuning value");
     if (k == "chunk") c->chunk = (uint32_t)value;
@@ -1188,6 +1341,7 @@ int rtw_set_accel(rtw_ctx* c, int accel) {
     if (!c) return RTW_E_INVALID;
     if (accel < RTW_ACCEL_AUTO || accel > RTW_ACCEL_BVH) return fail(c, RTW_E_UNSUPPORTED, "accel not available");
     c->accel = accel;
+    for (rtw_ctx* pk : c->peers) pk->accel = accel;
     return RTW_OK;
 }
 
@@ -1272,22 +1426,11 @@ int rtw_camera_build(const rtw_camera_builder* b, rtw_camera* out) {
     return RTW_OK;
 }
 
-int rtw_set_scene(rtw_ctx* c, const rtw_scene* s) {
-    if (!c) return RTW_E_INVALID;
-    int rc = validate_scene(c, s);
-    if (rc) return rc;
+// one device's copy of a staged scene (rtw_set_scene stages once, then
+// uploads to every device of the context)
+static int upload_scene(rtw_ctx* c, const rtw_scene* s, const std::vector<unsigned char>& blob,
+                        rtw::DevScene<float> tmp32, rtw::DevScene<double> tmp64) {
     HIP_TRY(c, hipSetDevice(c->device));
-    // stage once against base 0, then rebase the device pointers (EVERY
-    // pointer member of DevScene must be listed in `rebase`)
-    rtw::DevScene<float> tmp32{};
-    rtw::DevScene<double> tmp64{};
-    const uint32_t leaf = c->bvh_leaf ? c->bvh_leaf : (s->n_spheres >= 100000 ? 8u : 4u);
-    const uint32_t light_leaf = c->light_leaf ? c->light_leaf : rtw::kLeafMax;
-    // the light grid only for light lists long enough to skip the linear loop
-    const double grid = s->n_lights >= c->light_bvh_min ? c->light_grid / 16.0 : 0.0;
-    std::vector<unsigned char> blob = c->precision == RTW_F32
-                                          ? stage_scene<float>(s, &tmp32, 0, leaf, light_leaf, grid)
-                                          : stage_scene<double>(s, &tmp64, 0, leaf, light_leaf, grid);
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     if (c->scene_bytes < blob.size()) {
         if (c->d_scene) (void)hipFree(c->d_scene);
@@ -1351,6 +1494,30 @@ int rtw_set_scene(rtw_ctx* c, const rtw_scene* s) {
     return RTW_OK;
 }
 
+int rtw_set_scene(rtw_ctx* c, const rtw_scene* s) {
+    if (!c) return RTW_E_INVALID;
+    int rc = validate_scene(c, s);
+    if (rc) return rc;
+    // stage once against base 0 (upload_scene rebases the device pointers:
+    // EVERY pointer member of DevScene must be listed in its `rebase`)
+    rtw::DevScene<float> tmp32{};
+    rtw::DevScene<double> tmp64{};
+    const uint32_t leaf = c->bvh_leaf ? c->bvh_leaf : (s->n_spheres >= 100000 ? 8u : 4u);
+    const uint32_t light_leaf = c->light_leaf ? c->light_leaf : rtw::kLeafMax;
+    // the light grid only for light lists long enough to skip the linear loop
+    const double grid = s->n_lights >= c->light_bvh_min ? c->light_grid / 16.0 : 0.0;
+    std::vector<unsigned char> blob = c->precision == RTW_F32
+                                          ? stage_scene<float>(s, &tmp32, 0, leaf, light_leaf, grid)
+                                          : stage_scene<double>(s, &tmp64, 0, leaf, light_leaf, grid);
+    for (uint32_t k = 0; k < rtw_device_count(c); ++k) {   // multi-device: the same scene on every rank
+        rtw_ctx* ck = rtw_device_ctx(c, k);
+        rc = upload_scene(ck, s, blob, tmp32, tmp64);
+        if (rc) return k ? fail(c, rc, ck->err) : rc;
+    }
+    if (!c->peers.empty()) HIP_TRY(c, hipSetDevice(c->device));
+    return RTW_OK;
+}
+
 uint32_t rtw_tile_size(void) { return rtw::kTile; }
 
 uint32_t rtw_tiles_for_rank(uint32_t W, uint32_t H, uint32_t rank, uint32_t nranks) {
@@ -1390,13 +1557,109 @@ int rtw_render_device(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t
                                    : render_device_t<double>(c, cam, seed, rank, nranks, d_out, out_bytes, s);
 }
 
+int rtw_render_image_device(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, void* d_image, size_t image_bytes,
+                            void* stream) {
+    if (!c || !cam) return fail(c, RTW_E_INVALID, "bad argument");
+    if (!c->has_scene) return fail(c, RTW_E_NO_SCENE, "rtw_set_scene was not called");
+    const uint32_t W = cam->image_width, H = cam->image_height, n = rtw_device_count(c);
+    const size_t esz = c->precision == RTW_F32 ? sizeof(float) : sizeof(double);
+    const size_t img = (size_t)W * H * 3 * esz;
+    if (image_bytes < img || (img && !d_image)) return fail(c, RTW_E_INVALID, "d_image is smaller than W*H*3");
+    hipStream_t s0 = stream ? reinterpret_cast<hipStream_t>(stream) : c->stream;
+    // rank k renders the tiles T = k (mod n) into a packed buffer of rank 0's
+    // size (the most tiles: RCCL gathers equal counts)
+    const size_t per = std::max<size_t>((size_t)rtw_tiles_for_rank(W, H, 0, n) * 64 * 3, 1);
+    if (!c->multi) {
+        // one device, no collective: the packed tiles -> the image
+        HIP_TRY(c, hipSetDevice(c->device));
+        int rc = ensure(c, &c->d_out, &c->out_cap, per * esz);
+        if (rc) return rc;
+        rc = rtw_render_device(c, cam, seed, 0, 1, c->d_out, c->out_cap, s0);
+        if (rc) return rc;
+        return img ? rtw_assemble_tiles(c, c->d_out, c->out_cap, 1, W, H, d_image, s0) : RTW_OK;
+    }
+    HIP_TRY(c, hipSetDevice(c->device));
+    int rc = ensure(c, &c->d_gather, &c->gather_cap, (size_t)n * per * esz);
+    if (rc) return rc;
+    // launch every rank's share (asynchronous, each device on its own stream);
+    // rank 0 renders in place into its slot of the gather target
+    for (uint32_t k = 0; k < n; ++k) {
+        rtw_ctx* ck = rtw_device_ctx(c, k);
+        HIP_TRY(c, hipSetDevice(ck->device));
+        void* dst = c->d_gather;
+        if (k) {
+            rc = ensure(ck, &ck->d_out, &ck->out_cap, per * esz);
+            if (rc) return fail(c, rc, ck->err);
+            dst = ck->d_out;
+        }
+        rc = rtw_render_device(ck, cam, seed, k, n, dst, per * esz, k ? ck->stream : s0);
+        if (rc) return k ? fail(c, rc, ck->err) : rc;
+    }
+    // ONE gather of the packed tiles to rank 0 (RCCL over xGMI), ordered after
+    // each rank's render on that rank's stream
+    const RcclApi& api = rccl_api();
+    const ncclDataType_t dt = c->precision == RTW_F32 ? ncclFloat32 : ncclFloat64;
+    ncclResult_t r = api.group_start();
+    if (r != ncclSuccess) return rccl_fail(c, r, "ncclGroupStart");
+    for (uint32_t k = 0; k < n; ++k) {
+        rtw_ctx* ck = rtw_device_ctx(c, k);
+        r = api.gather(k ? ck->d_out : c->d_gather, k ? nullptr : c->d_gather, per, dt, 0, c->comms[k],
+                       k ? ck->stream : s0);
+        if (r != ncclSuccess) {
+            (void)api.group_end();
+            return rccl_fail(c, r, "ncclGather");
+        }
+    }
+    r = api.group_end();
+    if (r != ncclSuccess) return rccl_fail(c, r, "ncclGroupEnd");
+    HIP_TRY(c, hipSetDevice(c->device));
+    // rank 0 un-interleaves the n buffers into the image
+    return img ? rtw_assemble_tiles(c, c->d_gather, per * esz, n, W, H, d_image, s0) : RTW_OK;
+}
+
 int rtw_last_kernel(const rtw_ctx* c) {
     if (!c) return RTW_E_INVALID;
     return c->last_variant & 0xffff;
 }
 
+static int rtw_get_stats_one(rtw_ctx* c, rtw_stats* out);
+
 int rtw_get_stats(rtw_ctx* c, rtw_stats* out) {
     if (!c || !out) return RTW_E_INVALID;
+    if (!c->peers.empty()) {
+        // multi-device: the counters summed over the ranks of the last render,
+        // kernel_ms the slowest rank's; the rest as rank 0 reports it
+        rtw_stats sum{};
+        int worst = RTW_OK;
+        for (uint32_t k = 0; k < rtw_device_count(c); ++k) {
+            rtw_ctx* ck = rtw_device_ctx(c, k);
+            rtw_stats st{};
+            const int rc = rtw_get_stats_one(ck, &st);
+            if (rc == RTW_E_DEVICE || rc == RTW_E_INVALID) return k ? fail(c, rc, ck->err) : rc;
+            if (rc && !worst) {
+                worst = rc;
+                if (k) c->err = ck->err;
+            }
+            if (k == 0) sum = st;
+            else {
+                sum.samples += st.samples;
+                sum.segments += st.segments;
+                sum.lambertian += st.lambertian;
+                sum.node_visits += st.node_visits;
+                sum.sphere_tests += st.sphere_tests;
+                sum.panic_plane_uv += st.panic_plane_uv;
+                sum.panic_no_lights += st.panic_no_lights;
+                sum.kernel_ms = std::max(sum.kernel_ms, st.kernel_ms);
+            }
+        }
+        (void)hipSetDevice(c->device);
+        *out = sum;
+        return worst;
+    }
+    return rtw_get_stats_one(c, out);
+}
+
+static int rtw_get_stats_one(rtw_ctx* c, rtw_stats* out) {
     HIP_TRY(c, hipSetDevice(c->device));
     HIP_TRY(c, hipEventSynchronize(c->ev1));
     unsigned long long h[rtw_ctx::kCounters] = {};
@@ -1447,14 +1710,11 @@ int rtw_render(rtw_ctx* c, const rtw_camera* cam, const rtw_scene* scene, uint64
     if (!c->has_scene) return fail(c, RTW_E_NO_SCENE, "no scene");
     const size_t esz = c->precision == RTW_F32 ? sizeof(float) : sizeof(double);
     const size_t n = (size_t)cam->image_width * cam->image_height * 3;
-    const size_t tiles = (size_t)rtw_tiles_for_rank(cam->image_width, cam->image_height, 0, 1) * 64 * 3;
-    int rc = ensure(c, &c->d_out, &c->out_cap, std::max<size_t>(tiles * esz, 64));
+    HIP_TRY(c, hipSetDevice(c->device));
+    int rc = ensure(c, &c->d_img, &c->img_cap, std::max<size_t>(n * esz, 64));
     if (rc) return rc;
-    rc = ensure(c, &c->d_img, &c->img_cap, std::max<size_t>(n * esz, 64));
-    if (rc) return rc;
-    rc = rtw_render_device(c, cam, seed, 0, 1, c->d_out, c->out_cap, nullptr);
-    if (rc) return rc;
-    rc = rtw_assemble_tiles(c, c->d_out, c->out_cap, 1, cam->image_width, cam->image_height, c->d_img, nullptr);
+    // every device of the context renders its share; the image lands on the first
+    rc = rtw_render_image_device(c, cam, seed, c->d_img, c->img_cap, nullptr);
     if (rc) return rc;
     c->h_out.resize(n * esz);
     if (n) HIP_TRY(c, hipMemcpyAsync(c->h_out.data(), c->d_img, n * esz, hipMemcpyDeviceToHost, c->stream));

@@ -3,7 +3,7 @@
 // scene, applies main.rs:72-79's camera overrides, renders on the GPU and
 // writes image.ppm (P3, rows top to bottom).
 //
-//   rtw <scene> [--debug] [--seed N] [--f64] [--device N] [--config PATH] [--out PATH]
+//   rtw <scene> [--debug] [--seed N] [--f64] [--device N | --device-mask M] [--config PATH] [--out PATH]
 //
 // <scene> is one of clap's ValueEnum names of main.rs:29-38 (cornell-box,
 // debug, checkered-spheres, perlin-spheres, plane, simple, simple-light,
@@ -62,6 +62,7 @@ int main(int argc, char** argv) {
         else if (s == "--f64") opt.precision = RTW_F64;   // (the default)
         else if (s == "--f32") opt.precision = RTW_F32;   // the speed mode
         else if (s == "--device" && a + 1 < argc) opt.device = atoi(argv[++a]);
+        else if (s == "--device-mask" && a + 1 < argc) opt.device_mask = strtoull(argv[++a], nullptr, 0);
         else if (s == "--config" && a + 1 < argc) config = argv[++a];
         else if (s == "--out" && a + 1 < argc) out = argv[++a];
         else if (scene.empty()) scene = s;

@@ -322,8 +322,9 @@ std::vector<std::vector<SampledColour>> Camera::render(const HittableList& world
                                                        const RenderOptions& opt) const {
     FlatScene flat = flatten(world, lights);
     rtw_scene view = flat.view();
-    rtw_ctx* ctx = rtw_create(opt.device, opt.precision);
-    if (!ctx) throw Error(RTW_E_DEVICE, "rtw_create failed (no gfx950 device?)");
+    rtw_ctx* ctx = opt.device_mask ? rtw_create_mask(opt.device_mask, opt.precision)
+                                   : rtw_create(opt.device, opt.precision);
+    if (!ctx) throw Error(RTW_E_DEVICE, "rtw_create failed (no gfx950 device, or a bad device mask?)");
     rtw_set_accel(ctx, opt.accel);
     const uint32_t W = c_.image_width, H = c_.image_height;
     std::vector<double> sums((size_t)W * H * 3);

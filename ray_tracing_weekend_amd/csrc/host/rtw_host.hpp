@@ -209,6 +209,7 @@ class CameraBuilder {
 struct RenderOptions {
     uint64_t seed = 0x5EED0001ULL;  // the reference seeds from thread_rng (non-deterministic)
     int device = 0;
+    uint64_t device_mask = 0;       // != 0: one rank per set bit (rtw_create_mask), `device` unused
     int precision = RTW_F64;        // the parity mode (the reference's sums); RTW_F32: the speed mode
     int accel = RTW_ACCEL_AUTO;
 };

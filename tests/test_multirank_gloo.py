@@ -74,6 +74,49 @@ def _worker(rank, world, port, h, w, q):
         dist.destroy_process_group()
 
 
+def _worker_image_device(rank, world, port, h, w, q):
+    """The orchestration of rtw_render_image_device (capi.cpp) on a
+    multi-device context, one gloo rank per device: every rank renders its
+    tiles into an equal-size buffer of rank 0's tile count -- rank 0 in place,
+    into slot 0 of the gather target (ncclGather's in-place form,
+    rccl.h:729-733); the tails past a rank's own tiles hold garbage (NaN here),
+    which the assembly must never read -- then ONE gather to rank 0 and the
+    assembly with the slot stride."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        full = torch.from_numpy(_image(h, w))
+        per = max(sharding.tiles_for_rank(w, h, 0, world) * 64 * 3, 1)
+        target = torch.full((world, per), np.nan, dtype=torch.float64) if rank == 0 else None
+        send = target[0] if rank == 0 else torch.full((per,), np.nan, dtype=torch.float64)
+        packed = sharding.pack(full, rank, world).reshape(-1)
+        send[: packed.numel()] = packed
+        dist.gather(send, list(target.unbind(0)) if rank == 0 else None, dst=0)
+        ok = True
+        if rank == 0:
+            img = torch.full((h, w, 3), -7.0, dtype=torch.float64)
+            sharding.assemble(img, list(target.unbind(0)))
+            ok = bool(torch.equal(img, full))
+        q.put((rank, ok))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,h,w", [(2, 27, 5), (3, 41, 30), (4, 9, 17)])
+def test_image_device_orchestration_gathers_in_place(world, h, w):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_image_device, args=(r, world, port, h, w, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=120)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    res = dict(q.get(timeout=5) for _ in procs)
+    assert res == {r: True for r in range(world)}
+
+
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
