@@ -259,7 +259,7 @@ def mode_line(scene, cam, precision, tuning, steps, warmup, dev):
             r.set_tuning(k, v)
         r.set_scene(scene)
         buf = torch.empty((rtw.tiles_for_rank(W, H, 0, 1) * 64 * 3,), dtype=tdtype, device=dev)
-        stream = torch.cuda.current_stream(dev).cuda_stream
+        stream = rtw.torch_stream(dev.index)
 
         def step(seed):
             r.render_device(cam, seed, buf.data_ptr(), buf.numel() * buf.element_size(), stream=stream)
@@ -296,7 +296,7 @@ def cold_render(scene, cam, prec, dev):
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
         r.render_device(cam, 7, buf.data_ptr(), buf.numel() * buf.element_size(),
-                        stream=torch.cuda.current_stream(dev).cuda_stream)
+                        stream=rtw.torch_stream(dev.index))
         torch.cuda.synchronize(dev)
         dt = time.perf_counter() - t0
         render_ms, _ = r.get_timings(1)
@@ -373,7 +373,7 @@ def config_line(name, precision, dev):
         r.set_scene(scene)
         t_stage = time.perf_counter() - t0
         buf = torch.empty((rtw.tiles_for_rank(cfg["w"], cfg["h"], 0, 1) * 64 * 3,), dtype=tdtype, device=dev)
-        stream = torch.cuda.current_stream(dev).cuda_stream
+        stream = rtw.torch_stream(dev.index)
 
         def step(seed):
             r.render_device(cam, seed, buf.data_ptr(), buf.numel() * buf.element_size(), stream=stream)
@@ -464,7 +464,7 @@ def main():
     r.set_scene(scene)
     assert rtw.tile_size() == sharding.TILE
     image = torch.empty((H, W, 3), dtype=tdtype, device=dev) if rank == 0 else None
-    stream = torch.cuda.current_stream(dev).cuda_stream
+    stream = rtw.torch_stream(dev.index)
     if launch == "inproc":
         # every GPU renders its tiles, one RCCL gather to GPU 0, assembled there:
         # all inside rtw_render_image_device (the drop-in's multi-device path)

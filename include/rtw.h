@@ -74,6 +74,12 @@ extern "C" {
 #define RTW_LIGHTS_BVH_LEAF 1    /* the light list is a BoundedVolumeHierarchy of <= 5 entries
                                     (a leaf): pdf_value = (sum / n * n) / n, bvh.rs:67-76,191-194 */
 
+/* Stream arguments (hipStream_t as void*): NULL = the context's own stream
+ * (non-blocking); RTW_STREAM_NULL = the device's null (legacy default)
+ * stream, which orders with every blocking stream -- e.g. PyTorch's default
+ * stream, whose handle is 0; anything else is a hipStream_t of that device. */
+#define RTW_STREAM_NULL ((void *)1)
+
 /* World acceleration used by the render kernel */
 #define RTW_ACCEL_AUTO 0         /* pick per scene */
 #define RTW_ACCEL_BRUTE 1        /* every ray tests every sphere, sphere list in LDS */

@@ -643,17 +643,26 @@ def tile_size() -> int:
     return int(_lib.rtw_tile_size())
 
 
-def _torch_stream(device: int) -> int:
-    """hipStream_t of torch's current stream on `device` (the Renderer's
-    device, whatever torch's current device is); 0 -- the context's own
-    stream -- when torch has no GPU."""
+RTW_STREAM_NULL = 1   # include/rtw.h: the device's null (legacy default) stream
+
+
+def torch_stream(device: int) -> int:
+    """The rtw stream argument for torch's current stream on `device` (the
+    Renderer's device, whatever torch's current device is): its hipStream_t,
+    or RTW_STREAM_NULL when that is torch's default stream (handle 0, the
+    device's null stream -- passing 0 would mean the context's own,
+    unordered stream); 0 -- the context's own stream -- when torch has no GPU."""
     try:
         import torch
         if torch.cuda.is_available():
-            return int(torch.cuda.current_stream(device).cuda_stream)
+            h = int(torch.cuda.current_stream(device).cuda_stream)
+            return h if h else RTW_STREAM_NULL
     except ImportError:
         pass
     return 0
+
+
+_torch_stream = torch_stream
 
 
 # ---------------------------------------------------------------- scenes

@@ -195,6 +195,14 @@ const RcclApi& rccl_api() {
     return api;
 }
 
+// the caller's stream argument: NULL = the context's own stream,
+// RTW_STREAM_NULL = the device's null (legacy default) stream, else a hipStream_t
+hipStream_t resolve_stream(const rtw_ctx* c, void* stream) {
+    if (!stream) return c->stream;
+    if (stream == RTW_STREAM_NULL) return nullptr;
+    return reinterpret_cast<hipStream_t>(stream);
+}
+
 int rccl_fail(rtw_ctx* c, ncclResult_t r, const char* what) {
     const RcclApi& a = rccl_api();
     return fail(c, RTW_E_DEVICE, std::string(what) + ": " + (a.error_string ? a.error_string(r) : "RCCL error"));
@@ -347,7 +355,9 @@ std::vector<unsigned char> stage_scene(const rtw_scene* s, rtw::DevScene<R>* ds,
     constexpr bool k64 = std::is_same<R, float>::value;
     const size_t o_s64 = reserve(k64 ? sizeof(double) * 4 * s->n_spheres : 0);
     const size_t o_pl64 = reserve(k64 ? sizeof(double) * 8 * s->n_planes : 0);
-    const size_t o_m64 = reserve(k64 ? sizeof(double) * 4 * s->n_materials : 0);
+    // the per-material f64 scatter record: both precisions (the f64 kernels' one-pass
+    // Metal / Dielectric scatter reads it too)
+    const size_t o_m64 = reserve(sizeof(double) * 4 * s->n_materials);
     const size_t o_r = reserve(sizeof(R) * s->n_spheres);
     const size_t o_smat = reserve(sizeof(uint32_t) * s->n_spheres);
     const size_t o_sshade = reserve(sizeof(R4) * s->n_spheres);
@@ -522,14 +532,16 @@ std::vector<unsigned char> stage_scene(const rtw_scene* s, rtw::DevScene<R>* ds,
     ds->perlin_vec = reinterpret_cast<const R4*>(base + o_pvec);
     ds->perlin_perm = reinterpret_cast<const uint32_t*>(base + o_pperm);
     ds->light_flags = s->light_flags;
+    ds->emissive = 0;
+    for (uint32_t k = 0; k < s->n_materials; ++k)
+        if (s->mat_type[k] == RTW_DIFFUSE_LIGHT) ds->emissive = 1;
     for (uint32_t k = 0; k < s->n_materials; ++k) {
         const double* m = s->mat_params + 5 * k;
         const uint32_t t = s->mat_type[k];
         // the f64 scatter constants of kOptHit64 (dielectric_dir64): Dialectric's
         // index_of_refraction.recip() and reflectance's r0 for both faces, with the
         // reference's operations (material.rs:450-454, 464-468); Metal's fuzz
-        double m64s[4];
-        double* m64 = k64 ? reinterpret_cast<double*>(b + o_m64) + 4 * k : m64s;
+        double* m64 = reinterpret_cast<double*>(b + o_m64) + 4 * k;
         if (t == RTW_DIELECTRIC) {
             const double ior = m[4], rf = 1.0 / ior;
             const double r0f = (1.0 - rf) / (1.0 + rf), r0b = (1.0 - ior) / (1.0 + ior);
@@ -912,6 +924,8 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
     p.sc = *reinterpret_cast<const rtw::DevScene<R>*>(
         std::is_same<R, float>::value ? (const void*)&c->sc32 : (const void*)&c->sc64);
     fill_camera(p, cam);
+    // the kernel holds a lane's pixel as i | j << 16
+    if (p.W > 65535 || p.H > 65535) return fail(c, RTW_E_UNSUPPORTED, "image width or height beyond 65535");
     p.seed = seed;
     p.rank = rank;
     p.nranks = nranks;
@@ -961,7 +975,6 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
     if (rc) return rc;
     p.partial = reinterpret_cast<R*>(c->d_partial);
     p.counters = c->d_counters;
-    if (!stream) stream = c->stream;
     HIP_TRY(c, hipMemsetAsync(c->d_counters, 0, rtw_ctx::kCounters * sizeof(unsigned long long), stream));
     const size_t lds = (size_t)(p.sc.n_sph + p.sc.n_lights) * sizeof(rtw::R4<R>);
     int accel = c->accel == RTW_ACCEL_AUTO ? c->auto_accel : c->accel;
@@ -1536,7 +1549,7 @@ int rtw_assemble_tiles(rtw_ctx* c, const void* d_ranks, size_t rank_stride_bytes
     if (rank_stride_bytes < (size_t)rtw_tiles_for_rank(W, H, 0, nranks) * 64 * 3 * esz)
         return fail(c, RTW_E_INVALID, "rank stride is smaller than tiles_for_rank(rank 0)*64*3");
     HIP_TRY(c, hipSetDevice(c->device));
-    hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : c->stream;
+    hipStream_t s = resolve_stream(c, stream);
     const size_t stride = rank_stride_bytes / esz;
     const int rc = c->precision == RTW_F32
                        ? rtw::launch_assemble_f32(reinterpret_cast<const float*>(d_ranks), stride, nranks, W, H,
@@ -1552,7 +1565,7 @@ int rtw_render_device(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t
     if (!c || !cam || nranks == 0 || rank >= nranks) return fail(c, RTW_E_INVALID, "bad argument");
     if (!c->has_scene) return fail(c, RTW_E_NO_SCENE, "rtw_set_scene was not called");
     HIP_TRY(c, hipSetDevice(c->device));
-    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    hipStream_t s = resolve_stream(c, stream);
     return c->precision == RTW_F32 ? render_device_t<float>(c, cam, seed, rank, nranks, d_out, out_bytes, s)
                                    : render_device_t<double>(c, cam, seed, rank, nranks, d_out, out_bytes, s);
 }
@@ -1565,7 +1578,7 @@ int rtw_render_image_device(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, vo
     const size_t esz = c->precision == RTW_F32 ? sizeof(float) : sizeof(double);
     const size_t img = (size_t)W * H * 3 * esz;
     if (image_bytes < img || (img && !d_image)) return fail(c, RTW_E_INVALID, "d_image is smaller than W*H*3");
-    hipStream_t s0 = stream ? reinterpret_cast<hipStream_t>(stream) : c->stream;
+    hipStream_t s0 = resolve_stream(c, stream);
     // rank k renders the tiles T = k (mod n) into a packed buffer of rank 0's
     // size (the most tiles: RCCL gathers equal counts)
     const size_t per = std::max<size_t>((size_t)rtw_tiles_for_rank(W, H, 0, n) * 64 * 3, 1);
@@ -1574,9 +1587,9 @@ int rtw_render_image_device(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, vo
         HIP_TRY(c, hipSetDevice(c->device));
         int rc = ensure(c, &c->d_out, &c->out_cap, per * esz);
         if (rc) return rc;
-        rc = rtw_render_device(c, cam, seed, 0, 1, c->d_out, c->out_cap, s0);
+        rc = rtw_render_device(c, cam, seed, 0, 1, c->d_out, c->out_cap, stream);
         if (rc) return rc;
-        return img ? rtw_assemble_tiles(c, c->d_out, c->out_cap, 1, W, H, d_image, s0) : RTW_OK;
+        return img ? rtw_assemble_tiles(c, c->d_out, c->out_cap, 1, W, H, d_image, stream) : RTW_OK;
     }
     HIP_TRY(c, hipSetDevice(c->device));
     int rc = ensure(c, &c->d_gather, &c->gather_cap, (size_t)n * per * esz);
@@ -1592,7 +1605,7 @@ int rtw_render_image_device(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, vo
             if (rc) return fail(c, rc, ck->err);
             dst = ck->d_out;
         }
-        rc = rtw_render_device(ck, cam, seed, k, n, dst, per * esz, k ? ck->stream : s0);
+        rc = rtw_render_device(ck, cam, seed, k, n, dst, per * esz, k ? (void*)ck->stream : stream);
         if (rc) return k ? fail(c, rc, ck->err) : rc;
     }
     // ONE gather of the packed tiles to rank 0 (RCCL over xGMI), ordered after
@@ -1614,7 +1627,7 @@ int rtw_render_image_device(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, vo
     if (r != ncclSuccess) return rccl_fail(c, r, "ncclGroupEnd");
     HIP_TRY(c, hipSetDevice(c->device));
     // rank 0 un-interleaves the n buffers into the image
-    return img ? rtw_assemble_tiles(c, c->d_gather, per * esz, n, W, H, d_image, s0) : RTW_OK;
+    return img ? rtw_assemble_tiles(c, c->d_gather, per * esz, n, W, H, d_image, stream) : RTW_OK;
 }
 
 int rtw_last_kernel(const rtw_ctx* c) {

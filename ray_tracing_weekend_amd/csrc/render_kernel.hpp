@@ -308,6 +308,74 @@ __device__ __forceinline__ void sweep_spheres_excl(const R4<float>* __restrict__
 // li32 (may be null): the same lights rounded to f32 with |radius| (staged in
 // LDS by the LDS-world kernels): the pre-pass reads them instead of converting
 // the f64 records -- the same f32 values, the same mask
+// the pre-pass test of one light {c, |r|} (rounded to f32) against the f32 ray
+__device__ __forceinline__ bool light_may_hit(float cx, float cy, float cz, float r, float ox, float oy, float oz,
+                                              float dx, float dy, float dz, float ia, float on, float dn) {
+    const float fx = ox - cx, fy = oy - cy, fz = oz - cz;
+    const float hb = __builtin_fmaf(dz, fz, __builtin_fmaf(dy, fy, dx * fx));
+    const float tc = -hb * ia;
+    const float lx = __builtin_fmaf(tc, dx, fx), ly = __builtin_fmaf(tc, dy, fy), lz = __builtin_fmaf(tc, dz, fz);
+    const float l2 = __builtin_fmaf(lx, lx, __builtin_fmaf(ly, ly, lz * lz));
+    const float f2 = __builtin_fmaf(fx, fx, __builtin_fmaf(fy, fy, fz * fz));
+    const float e = 0x1p-18f * (on + fabsf(cx) + fabsf(cy) + fabsf(cz) + r);
+    const float rr = (r + e) * (r + e);
+    // NaN anywhere (a NaN ray): no candidate; the f64 test gives 0 too
+    return (l2 <= rr) & ((hb <= 2.0f * e * dn) | (f2 <= rr));
+}
+// The f32 ray of the pre-pass: o, d rounded, 1 / (d . d), |o|_1, |d|_1
+struct LightPre {
+    float ox, oy, oz, dx, dy, dz, ia, on, dn;
+    __device__ __forceinline__ LightPre(V3<double> o, V3<double> d)
+        : ox((float)o.x), oy((float)o.y), oz((float)o.z), dx((float)d.x), dy((float)d.y), dz((float)d.z) {
+        ia = __builtin_amdgcn_rcpf(__builtin_fmaf(dx, dx, __builtin_fmaf(dy, dy, dz * dz)));
+        on = fabsf(ox) + fabsf(oy) + fabsf(oz);
+        dn = fabsf(dx) + fabsf(dy) + fabsf(dz);
+    }
+    __device__ __forceinline__ bool may_hit(const R4<double>& L) const {
+        return light_may_hit((float)L.x, (float)L.y, (float)L.z, fabsf((float)L.w), ox, oy, oz, dx, dy, dz, ia, on, dn);
+    }
+};
+
+// HittableList::pdf_value's sum over the hit lights in LIST order (f64) when
+// an acceleration structure finds them in another order: `walk(lo, add)` calls
+// add(id) once for every light the ray hits, in any order, and each pass keeps
+// the kMax smallest list indices >= lo; their pdfs are added in index order
+// and, when the pass had to drop hits, the next pass continues above the last
+// index summed.  (A ray skimming C5's flat light layer hits ~10 lights.)
+template <typename Walk>
+__device__ __forceinline__ double lights_sum_in_list_order(const R4<double>* __restrict__ lights, V3<double> o,
+                                                           V3<double> d, Walk&& walk) {
+    constexpr uint32_t kMax = 8;
+    double acc = 0.0;
+    uint32_t lo = 0;
+    for (;;) {
+        uint32_t ids[kMax];
+        uint32_t n = 0;
+        bool dropped = false;
+        walk([&](uint32_t id) {
+            if (id < lo) return;
+            if (n == kMax) {
+                dropped = true;
+                if (id > ids[kMax - 1]) return;
+                --n;                       // the largest gives way
+            }
+            uint32_t q = n;                // insertion by list index
+            while (q > 0 && ids[q - 1] > id) {
+                ids[q] = ids[q - 1];
+                --q;
+            }
+            ids[q] = id;
+            ++n;
+        });
+        for (uint32_t q = 0; q < n; ++q) {
+            const R4<double> L = lights[ids[q]];
+            acc = acc + sphere_pdf_value(mk(L.x, L.y, L.z), L.w, o, d);
+        }
+        if (!dropped) return acc;
+        lo = ids[kMax - 1] + 1u;
+    }
+}
+
 template <bool kRobust = false>
 __device__ __forceinline__ double lights_pdf_sum(const R4<double>* __restrict__ li, uint32_t n,
                                                  V3<double> o, V3<double> d,
@@ -337,18 +405,7 @@ __device__ __forceinline__ double lights_pdf_sum(const R4<double>* __restrict__ 
                 cz = (float)L.z;
                 r = fabsf((float)L.w);
             }
-            const float fx = ox - cx, fy = oy - cy, fz = oz - cz;
-            const float hb = __builtin_fmaf(dz, fz, __builtin_fmaf(dy, fy, dx * fx));
-            const float tc = -hb * ia;
-            const float lx = __builtin_fmaf(tc, dx, fx), ly = __builtin_fmaf(tc, dy, fy),
-                        lz = __builtin_fmaf(tc, dz, fz);
-            const float l2 = __builtin_fmaf(lx, lx, __builtin_fmaf(ly, ly, lz * lz));
-            const float f2 = __builtin_fmaf(fx, fx, __builtin_fmaf(fy, fy, fz * fz));
-            const float e = 0x1p-18f * (on + fabsf(cx) + fabsf(cy) + fabsf(cz) + r);
-            const float rr = (r + e) * (r + e);
-            // NaN anywhere (a NaN ray): no candidate; the f64 test gives 0 too
-            const bool cand = (l2 <= rr) & ((hb <= 2.0f * e * dn) | (f2 <= rr));
-            mask |= (cand ? 1u : 0u) << k;
+            mask |= (light_may_hit(cx, cy, cz, r, ox, oy, oz, dx, dy, dz, ia, on, dn) ? 1u : 0u) << k;
         }
         while (mask) {
             const uint32_t k = (uint32_t)__builtin_ctz(mask);
@@ -1208,6 +1265,7 @@ __device__ __forceinline__ V3<double> ray_at64(V3<double> o, V3<double> d, doubl
     return V3<double>{o.x + d.x * t, o.y + d.y * t, o.z + d.z * t};
 }
 __device__ __forceinline__ V3<double> to64(V3<float> v) { return V3<double>{v.x, v.y, v.z}; }
+__device__ __forceinline__ V3<double> to64(V3<double> v) { return v; }
 // An f32 direction as a GENERIC f64 value: the f32 value with pseudo-random
 // bits below its 24-bit mantissa (a relative change < 2^-25: the same f32
 // value).  The reference's directions are f64 results with rounding noise in
@@ -1295,11 +1353,18 @@ __device__ __forceinline__ V3<double> dielectric_dir64(V3<double> u, V3<double> 
 // the draws and operations are metal_dir64's / dielectric_dir64's:
 // Dialectric's cos_theta = min(u . -n, 1) is min(-(u . n), 1) bit for bit
 // (negation is exact and round-to-nearest symmetric).
+// `kRefSphere`: Metal's UnitSphere by the reference's rejection loop in f64
+// (the f64 parity kernels), else the f32 kernels' direct sampler carried into
+// f64 (dither64).
+template <bool kRefSphere = false>
 __device__ __forceinline__ V3<double> specular_dir64(bool metal, V3<double> d, V3<double> n, bool front,
                                                      const R4<double>& M, Rng& g, bool& keep) {
 #pragma clang fp contract(off)
     V3<double> us = {0.0, 0.0, 0.0};
-    if (metal) us = dither64(unit_sphere<float>(g));
+    if (metal) {
+        if constexpr (kRefSphere) us = unit_sphere<double>(g);
+        else us = dither64(unit_sphere<float>(g));
+    }
     const V3<double> u = unit64(d);
     const double vn = u.x * n.x + u.y * n.y + u.z * n.z;
     const V3<double> r = {u.x - (n.x * 2.0) * vn, u.y - (n.y * 2.0) * vn, u.z - (n.z * 2.0) * vn};
@@ -1498,35 +1563,14 @@ __device__ __forceinline__ float lights_pdf_bvh(const DevScene<float>& sc, V3<fl
 template <bool kRobust>
 __device__ __forceinline__ double lights_pdf_bvh(const DevScene<double>& sc, V3<double> o, V3<double> d,
                                                  int32_t* __restrict__ stk) {
-    constexpr uint32_t kMax = 8;
-    uint32_t ids[kMax];
-    uint32_t n = 0;
-    bool overflow = false;
-    light_bvh_walk(sc, o, d, stk, [&](uint32_t k) {
-        const R4<double> L = sc.lsph[k];
-        double t;
-        if (sphere_t(mk(L.x, L.y, L.z), L.w * L.w, o, d, 0.0, t)) {
-            if (n < kMax) {
-                // insertion by list index
-                uint32_t id = sc.lid[k], q = n;
-                while (q > 0 && ids[q - 1] > id) {
-                    ids[q] = ids[q - 1];
-                    --q;
-                }
-                ids[q] = id;
-                ++n;
-            } else {
-                overflow = true;
-            }
-        }
+    const LightPre pre(o, d);
+    return lights_sum_in_list_order(sc.lights, o, d, [&](auto&& add) {
+        light_bvh_walk(sc, o, d, stk, [&](uint32_t k) {
+            const R4<double> L = sc.lsph[k];
+            double t;
+            if (pre.may_hit(L) && sphere_t(mk(L.x, L.y, L.z), L.w * L.w, o, d, 0.0, t)) add(sc.lid[k]);
+        });
     });
-    if (overflow) return lights_pdf_sum(sc.lights, sc.n_lights, o, d);
-    double acc = 0.0;
-    for (uint32_t q = 0; q < n; ++q) {
-        const R4<double> L = sc.lights[ids[q]];
-        acc = acc + sphere_pdf_value(mk(L.x, L.y, L.z), L.w, o, d);
-    }
-    return acc;
 }
 
 // f32: the big list, then the walk; a light counts in the cell whose interval
@@ -1635,48 +1679,27 @@ __device__ __forceinline__ float lights_pdf_grid_coop(const DevScene<float>& sc,
     return acc;
 }
 
-// f64 (parity mode): the hit lights' list indices, summed in LIST order as in
-// lights_pdf_bvh; more than 8 hits falls back to the linear loop.
+// f64 (parity mode): the hit lights' list indices, summed in LIST order
+// (lights_sum_in_list_order) as in lights_pdf_bvh.
 template <bool kRobust>
 __device__ __forceinline__ double lights_pdf_grid(const DevScene<double>& sc, V3<double> o, V3<double> d) {
-    constexpr uint32_t kMax = 8;
-    uint32_t ids[kMax];
-    uint32_t n = 0;
-    bool overflow = false;
-    auto add = [&](uint32_t id) {
-        if (n < kMax) {
-            uint32_t q = n;
-            while (q > 0 && ids[q - 1] > id) {
-                ids[q] = ids[q - 1];
-                --q;
-            }
-            ids[q] = id;
-            ++n;
-        } else {
-            overflow = true;
-        }
-    };
-    for (uint32_t k = 0; k < sc.lg_big; ++k) {
-        const R4<double> L = sc.lg_sph[k];
-        double t;
-        if (sphere_t(mk(L.x, L.y, L.z), L.w * L.w, o, d, 0.0, t)) add(sc.lg_id[k]);
-    }
+    const LightPre pre(o, d);   // the f32 pre-pass rules out the lights the ray misses
     const double ia = 1.0 / (d.x * d.x + d.y * d.y + d.z * d.z);
-    light_grid_walk(sc, o, d, [&](uint32_t k, double te, double tx) {
-        const R4<double> L = sc.lg_sph[k];
-        double t;
-        if (sphere_t(mk(L.x, L.y, L.z), L.w * L.w, o, d, 0.0, t)) {
-            const double tc = -((o.x - L.x) * d.x + (o.y - L.y) * d.y + (o.z - L.z) * d.z) * ia;
-            if (tc >= te && tc < tx) add(sc.lg_id[k]);
+    return lights_sum_in_list_order(sc.lights, o, d, [&](auto&& add) {
+        for (uint32_t k = 0; k < sc.lg_big; ++k) {
+            const R4<double> L = sc.lg_sph[k];
+            double t;
+            if (pre.may_hit(L) && sphere_t(mk(L.x, L.y, L.z), L.w * L.w, o, d, 0.0, t)) add(sc.lg_id[k]);
         }
+        light_grid_walk(sc, o, d, [&](uint32_t k, double te, double tx) {
+            const R4<double> L = sc.lg_sph[k];
+            double t;
+            if (pre.may_hit(L) && sphere_t(mk(L.x, L.y, L.z), L.w * L.w, o, d, 0.0, t)) {
+                const double tc = -((o.x - L.x) * d.x + (o.y - L.y) * d.y + (o.z - L.z) * d.z) * ia;
+                if (tc >= te && tc < tx) add(sc.lg_id[k]);
+            }
+        });
     });
-    if (overflow) return lights_pdf_sum(sc.lights, sc.n_lights, o, d);
-    double acc = 0.0;
-    for (uint32_t q = 0; q < n; ++q) {
-        const R4<double> L = sc.lights[ids[q]];
-        acc = acc + sphere_pdf_value(mk(L.x, L.y, L.z), L.w, o, d);
-    }
-    return acc;
 }
 
 // Light list with quads (DevScene::lref set): HittableList::pdf_value over
@@ -1784,6 +1807,36 @@ enum : int { kOptRobust = 1, kOptLightBvh = 2, kOptTex = 4, kOptPrims = 8, kOptH
 #ifndef RTW_STEAL_TOP
 #define RTW_STEAL_TOP 0
 #endif
+// ray_colour_tail_call's accumulator `res` (camera.rs:459-522): res += mult *
+// emitted at every scatter, added to the sample's colour where it ends.
+// Kernels for scenes without a DiffuseLight (kEmit false; the host routes a
+// scene with one to the kOptPrims kernels) know emitted() = (0, 0, 0) on every
+// hit (material.rs:42-44): res starts at +0 and gains mult * (+0), which is
+// +0 or -0 -- no change, +0 + -0 = +0 -- while mult is finite and NaN once it
+// is not, and then stays NaN.  So res is +0 or NaN per component: three bits
+// instead of three registers, and value() is exactly res.
+template <typename R, bool kEmit>
+struct ResAcc;
+template <typename R>
+struct ResAcc<R, true> {
+    V3<R> v;
+    __device__ __forceinline__ void reset() { v = mk<R>(0, 0, 0); }
+    __device__ __forceinline__ void add(V3<R> mult, V3<R> emitted) { v = v + mult * emitted; }
+    __device__ __forceinline__ V3<R> value() const { return v; }
+};
+template <typename R>
+struct ResAcc<R, false> {
+    uint32_t nan;
+    __device__ __forceinline__ void reset() { nan = 0; }
+    __device__ __forceinline__ void add(V3<R> mult, V3<R>) {   // emitted is (0, 0, 0) here
+        nan |= (__builtin_isfinite(mult.x) ? 0u : 1u) | (__builtin_isfinite(mult.y) ? 0u : 2u) |
+               (__builtin_isfinite(mult.z) ? 0u : 4u);
+    }
+    __device__ __forceinline__ V3<R> value() const {
+        return mk<R>((nan & 1u) ? (R)NAN : (R)0, (nan & 2u) ? (R)NAN : (R)0, (nan & 4u) ? (R)NAN : (R)0);
+    }
+};
+
 template <typename R, int kWorld, int kOpt>
 // f32: ask for 5 waves per SIMD (<= 96 VGPRs), 4 for the hit64 kernels.
 #ifndef RTW_WAVES
@@ -1807,6 +1860,9 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
     constexpr bool kTex = (kOpt & kOptTex) != 0;
     constexpr bool kPrims = (kOpt & kOptPrims) != 0;
     constexpr bool kHit64 = (kOpt & kOptHit64) != 0 && sizeof(R) == 4 && !kTex && !kPrims;
+    // DiffuseLight materials only in the kOptPrims / kOptTex kernels (the host
+    // routes scenes with one there): the others know emitted() is black
+    constexpr bool kEmit = kPrims || kTex;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     R4<R>* s_sph = reinterpret_cast<R4<R>*>(smem);
     R4<R>* s_li = s_sph + p.sc.n_sph;
@@ -1966,11 +2022,17 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
     // per-lane item state
     uint32_t q = lane;            // item index in the task's pool
     uint32_t next_q = 0;          // wave-uniform: first unassigned item
-    uint32_t px = 0, i = 0, j = 0, c = 0, s = 0, s_end = 0;
-    uint32_t my_lt = 0;           // local tile of the lane's item
-    uint64_t pix = 0;
+    // (kept small: it is live across the whole segment loop) the pixel (i, j)
+    // as i | j << 16 (W, H < 2^16, checked by the host), the item's chunk-sum
+    // slot lt * 64 + px (its local tile lt = slot >> 6), its chunk c and the
+    // current sample s; the chunk's samples end at min((c + 1) chunk, spp)
+    uint32_t ij = 0, slot = 0, c = 0, s = 0;
+    auto pix_now = [&]() { return (uint64_t)(ij >> 16) * p.W + (ij & 0xffffu); };   // pixel index
+    (void)pix_now;                // (probe builds)
     Rng g;
-    V3<R> o = zero, d = zero, mult = zero, res = zero;
+    V3<R> o = zero, d = zero, mult = zero;
+    ResAcc<R, kEmit> res;
+    res.reset();
     uint32_t depth = 0;
     int32_t self_s = -1;          // isolated sphere the current ray starts on (else -1); kHit64:
                                   // the sphere it starts on, isolated or not
@@ -1978,6 +2040,8 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
     V3<double> o64 = {0.0, 0.0, 0.0};   // kHit64: the ray origin in f64
     V3<double> d64 = {0.0, 0.0, 0.0};   // kHit64: the ray direction in f64 (a Metal / Dielectric
                                         // scatter's own f64 result, else dither64 of the f32 one)
+    // segments and Lambertian bounces are counted per wave (scalar: a ballot's
+    // popcount per trip), node visits and sphere tests per lane (the tile costs)
     uint32_t segs = 0, lambs = 0, nvis = 0, ntest = 0;
     bool active = false, need = true;
     // kCoopGrid (f32 kernels with the light grid, KParams::grid_piece > 0): a
@@ -1996,10 +2060,11 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
         // its end minus at its start -- subtracted here, added at the end (a
         // u32 sum: exact modulo 2^32, no register kept)
         if (k->tile_cost) {
-            if (s < k->cost_spp) atomicSub(k->tile_cost + my_lt, nvis + ntest);
+            if (s < k->cost_spp) atomicSub(k->tile_cost + (slot >> 6), nvis + ntest);
         }
         // Camera::get_ray, camera.rs:274-293 + ray_colour_call, camera.rs:439-457
-        g.seed(k->seed, pix, s);
+        const uint32_t i = ij & 0xffffu, j = ij >> 16;
+        g.seed(k->seed, (uint64_t)j * k->W + i, s);
         R ox = PR::u_incl(g.next(), (R)-0.5, k->u_scale);
         R oy = PR::u_incl(g.next(), (R)-0.5, k->u_scale);
         V3<R> ps = (mk(k->p00[0], k->p00[1], k->p00[2]) + mk(k->du[0], k->du[1], k->du[2]) * ((R)i + ox)) +
@@ -2018,7 +2083,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
             d64 = dither64(d);
         }
         mult = mk<R>(1, 1, 1);
-        res = zero;
+        res.reset();
         depth = k->max_depth;
         self_s = -1;
         self_iso = false;
@@ -2053,14 +2118,13 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                     (uint32_t)(want >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)want, 0u));
                 q = next_q + below;
                 if (q < n_items) {
+                    uint32_t px;
                     decode(q, px, c);
-                    i = tx * kTile + (px & 7u);
-                    j = ty * kTile + (px >> 3);
+                    const uint32_t i = tx * kTile + (px & 7u), j = ty * kTile + (px >> 3);
                     if (i < k->W && j < k->H) {
-                        my_lt = lt;
-                        pix = (uint64_t)j * k->W + i;
+                        ij = i | (j << 16);
+                        slot = lt * 64u + px;
                         s = c * k->chunk;
-                        s_end = min(s + k->chunk, k->spp);
                         active = true;
                         need = false;
                         start_sample();
@@ -2073,7 +2137,11 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
     // the first 64 items of the first task go to lanes 0..63 in order
     acquire();
 
-    while (__ballot(active) != 0) {
+    for (;;) {
+        const uint64_t live = __ballot(active);
+        if (live == 0) break;
+        segs += (uint32_t)__popcll(live);   // every active lane runs one segment of this trip
+        bool lamb = false;                  // the lane's segment ended in a Lambertian scatter
         RTW_PROBE_LANES(3);
         if (active) {
             RTW_PROBE_LANES(4);
@@ -2091,6 +2159,10 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
             for (int32_t k = 0; k < nplanes; ++k) {
                 R t;
                 const R* pl = kargs()->sc.planes + kPlaneR * k;
+                // plane_t's one-sided test (plane.rs:62-63) first: it fails for every
+                // ray that leaves the Book-1 ground downwards, and then the box test
+                // (side-effect free, bounded_hit's first half) cannot change the outcome
+                if (!(dot(d, mk(pl[3], pl[4], pl[5])) > PR::kEps)) continue;
                 const bool box_hit = aabb_hit_plane(pl + 6, pl + 9, o, d, tmin);
                 if (box_hit && plane_t(pl, o, d, tmin, t, p.counters + 4) &&
                     (best < 0 || t < tb)) {
@@ -2181,14 +2253,13 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
             } else {
                 sweep_spheres<kRobust>(sph, kargs()->sc.n_sph, sbase, o, d, tmin, tb, best);
             }
-            ++segs;
             RTW_PROBE_SEGMENT();
 
             bool done = false;
             V3<R> col = zero;
             if (best < 0) {
                 const KArgs* k = kargs();
-                col = mult * mk(k->bg[0], k->bg[1], k->bg[2]) + res;   // camera.rs:473-475
+                col = mult * mk(k->bg[0], k->bg[1], k->bg[2]) + res.value();   // camera.rs:473-475
                 done = true;
             } else {
                 // HitRecord::new, hittable.rs:101-129
@@ -2293,7 +2364,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                     if (mtype == kMatDiffuseLight || mtype == kMatLambertian)
                         colour = tex_colour(p.sc, kargs()->sc.mat_tex[m], hu, hv, pnt);
                 }
-                const V3<R> emitted = mtype == kMatDiffuseLight ? colour : zero;
+                const V3<R> emitted = kEmit && mtype == kMatDiffuseLight ? colour : zero;
                 if (kHit64 && sph_hit) {
                     // Metal / Dielectric sphere: the f64 scatter of both in one pass
                     RTW_PROBE_LANES(7);
@@ -2302,7 +2373,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                     RTW_PROBE_SCATTER64(specular_dir64(metal, d64, n64, front, kargs()->sc.mat64[m], g2, keep2).y);
                     d64 = specular_dir64(metal, d64, n64, front, kargs()->sc.mat64[m], g, keep);
                     if (!keep) {
-                        col = mult * emitted + res;
+                        col = mult * emitted + res.value();
                         done = true;
                     } else {
                         if (metal) mult = mult * mk(mp.x, mp.y, mp.z);   // Reflect, camera.rs:488-500
@@ -2312,13 +2383,34 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                         o64 = pnt64;
                         d = from64<R>(d64);
                     }
+                } else if (sizeof(R) == 8 && (mtype == kMatMetal || mtype == kMatDielectric)) {
+                    // f64: Metal::scatter and Dialectric::scatter (material.rs:407-421,
+                    // 458-487) in one pass (specular_dir64 with the reference's
+                    // UnitSphere loop and the material's f64 record: 1 / ior and both
+                    // faces' Schlick r0 computed on the host with the reference's
+                    // operations), so a wave whose lanes hit both runs it once
+                    RTW_PROBE_LANES(7);
+                    const bool metal = mtype == kMatMetal;
+                    bool keep;
+                    const V3<double> dir = specular_dir64<true>(metal, to64(d), to64(nrm), front,
+                                                                kargs()->sc.mat64[m], g, keep);
+                    if (!keep) {
+                        col = mult * emitted + res.value();
+                        done = true;
+                    } else {
+                        if (metal) mult = mult * mk(mp.x, mp.y, mp.z);   // Reflect, camera.rs:488-500
+                        o = pnt;                                          // (Dielectric: mult * (1, 1, 1) = mult)
+                        self_s = next_self;
+                        self_iso = next_iso;
+                        d = from64<R>(dir);
+                    }
                 } else if (mtype == kMatMetal) {
                     RTW_PROBE_LANES(7);
                     // Metal::scatter, material.rs:407-421
                     V3<R> refl = reflect(PR::normalize(d), nrm);
                     const V3<R> dir = refl + unit_sphere<R>(g) * mp.w;
                     if (!(dot(dir, nrm) > (R)0)) {
-                        col = mult * emitted + res;
+                        col = mult * emitted + res.value();
                         done = true;
                     } else {
                         mult = mult * mk(mp.x, mp.y, mp.z);            // Reflect, camera.rs:488-500
@@ -2355,7 +2447,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                     RTW_PROBE_LANES(9);
                     // Lambertian + MixturePdf(HittablePdf(lights), CosinePdf):
                     // material.rs:357-376, pdf.rs:33-101, camera.rs:504-521
-                    ++lambs;
+                    lamb = true;
                     const V3<R> att = colour;
                     const Onb<R> uvw(nrm);
                     V3<R> dir;
@@ -2401,7 +2493,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                         pend = true;
                         pend_aw = att * spdf;
                         pend_ch = PR::max_(cos_w, (R)0) * (R)0.5;
-                        res = res + mult * emitted;
+                        res.add(mult, emitted);
                         o = pnt;
                         self_s = next_self;
                         self_iso = next_iso;
@@ -2432,7 +2524,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                     const R spdf = PR::max_(PR::over_pi(dot(nrm, ndir)), (R)0);
                     const V3<R> w = PR::divs(att * spdf, pdf);
                     const V3<R> new_mult = mult * w;
-                    res = res + mult * emitted;
+                    res.add(mult, emitted);
                     mult = new_mult;
                     o = pnt;
                     self_s = next_self;
@@ -2445,13 +2537,13 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                     }
                 } else {
                     // Invisible (material.rs:321-325): scatter() == None
-                    col = mult * emitted + res;
+                    col = mult * emitted + res.value();
                     done = true;
                 }
                 if (!done) {
                     depth -= 1;
                     if (depth == 0) {                                  // camera.rs:470-472
-                        col = zero + res;
+                        col = zero + res.value();
                         done = true;
                         if constexpr (kCoopGrid) pend = false;         // its pdf is not needed
                     }
@@ -2462,7 +2554,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                 // registers: (0 + s_first) on the first sample, then slot + s
                 // -- the fold of camera.rs:323-335 in the same order
                 const KArgs* k = kargs();
-                R* dst = k->partial + (((size_t)my_lt * 64 + px) * k->n_chunks + c) * 3;
+                R* dst = k->partial + ((size_t)slot * k->n_chunks + c) * 3;
                 V3<R> prev = zero;
                 if (k->chunk > 1) {   // (wave-uniform: one sample per item never reads the slot)
                     if (s != c * k->chunk) prev = mk(dst[0], dst[1], dst[2]);
@@ -2473,10 +2565,10 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                 dst[2] = part.z;
                 if (k->tile_cost) {   // tile costs for the task order: this sample's work
                     if (s < k->cost_spp)
-                        atomicAdd(k->tile_cost + my_lt, nvis + ntest + kCostPerSegment * (k->max_depth - depth + 1u));
+                        atomicAdd(k->tile_cost + (slot >> 6), nvis + ntest + kCostPerSegment * (k->max_depth - depth + 1u));
                 }
                 ++s;
-                if (s < s_end) {
+                if (s < min((c + 1u) * k->chunk, k->spp)) {
                     RTW_PROBE_SEED();
                     start_sample();
                 RTW_PROBE_LANES(10);
@@ -2486,6 +2578,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                 }
             }
         }
+        lambs += (uint32_t)__popcll(__ballot(lamb));
         if constexpr (kCoopGrid) {
             // the deferred Lambertian light pdfs of this trip, by the whole wave;
             // then the path throughput as in the Lambertian branch
@@ -2541,12 +2634,10 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
     }
 
     RTW_PROBE_WAVE_END();
-    // wave-reduce the counters, one atomic per wave
+    // wave-reduce the per-lane counters (segs, lambs are per wave), one atomic per wave
     for (int off = 32; off > 0; off >>= 1) {
-        segs += __shfl_xor(segs, off);
         nvis += __shfl_xor(nvis, off);
         ntest += __shfl_xor(ntest, off);
-        lambs += __shfl_xor(lambs, off);
     }
     if (lane == 0 && p.counters) {
         atomicAdd(p.counters + 0, (unsigned long long)segs);
@@ -2738,8 +2829,9 @@ inline int launch_render_impl(const KParams<R>& p, int world, size_t lds_bytes, 
         const bool robust = sizeof(R) == 4 && p.sc.robust;
         const bool lbvh = p.light_bvh != 0;
         // kOptPrims: always for textured kernels; the Book-1 kernels go
-        // without when the scene has no quads, cuboids or mixed list
-        const bool prims = p.sc.n_quads || p.sc.n_boxes || p.sc.lref;
+        // without when the scene has no quads, cuboids, mixed list or
+        // DiffuseLight (their emission accumulator is three bits, ResAcc)
+        const bool prims = p.sc.n_quads || p.sc.n_boxes || p.sc.lref || p.sc.emissive;
         constexpr int T = dev::kOptTex | dev::kOptPrims, Pr = dev::kOptPrims;
         if (p.sc.mat_tex) {
             if constexpr (sizeof(R) == 4) {

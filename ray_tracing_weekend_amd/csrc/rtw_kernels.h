@@ -113,7 +113,7 @@ struct DevScene : DevSceneCull<R> {
     const R4<double>* sph64;          // spheres {cx, cy, cz, radius} as given (f64): the f32
                                       // kernels' f64 hit points (kOptHit64)
     const R4<double>* pl64;           // planes {point, 0}, {normal, 0} as given (f64): kOptHit64
-    const R4<double>* mat64;          // per material (f64, kOptHit64): {1/ior, r0 at 1/ior, r0 at ior,
+    const R4<double>* mat64;          // per material (f64; kOptHit64 and the f64 kernels): {1/ior, r0 at 1/ior, r0 at ior,
                                       // ior} (Dialectric), {-, -, -, fuzz} (Metal)
     const uint32_t* lref;             // light list in order (kLref* bits | index; null when the
                                       // list is spheres only)
@@ -132,6 +132,8 @@ struct DevScene : DevSceneCull<R> {
     uint32_t n_quads, n_lquads, n_list;   // world quads, light quads, light-list length
     uint32_t n_boxes;
     uint32_t light_flags;             // RTW_LIGHTS_BVH_LEAF
+    uint32_t emissive;                // a DiffuseLight material exists (its scenes run the kOptPrims
+                                      // kernels, which keep the emission accumulator)
     // light grid (host/bvh.hpp LightGrid): box lo / hi, cell size and its
     // inverse, cells per axis, big-list length, 1 when staged
     R lg_lo[3], lg_hi[3], lg_cell[3], lg_inv[3];

@@ -109,7 +109,7 @@ extern "C" int rtw_probe_timeline_read(unsigned long long* out, size_t n, int re
             const R* pl = p.sc.planes + kPlaneR * k; \
             if (aabb_hit_ref(pl + 6, pl + 9, o, mk(d.y, d.x, d.z), tmin) && \
                 plane_t(pl, o, mk(d.y, d.x, d.z), tmin, t, nullptr) && t == (R)-7) \
-                ++segs; \
+                ++ntest; \
         } \
     } while (0)
 #else
@@ -126,7 +126,7 @@ extern "C" int rtw_probe_timeline_read(unsigned long long* out, size_t n, int re
             bvh_closest<kWorld == kWorldBvhLds ? kWorldBvhWW : kWorld, kRobust>(scw, sbase, o, d2, tmin, tb2, best2, \
                                 reinterpret_cast<int32_t*>(smem) + wave * p.stack * 64 + lane, nvis, \
                                 ntest, self_s); \
-            segs += best2 == -7 ? 1u : 0u; \
+            ntest += best2 == -7 ? 1u : 0u; \
         } \
     } while (0)
 #else
@@ -145,7 +145,7 @@ extern "C" int rtw_probe_timeline_read(unsigned long long* out, size_t n, int re
             } else { \
                 dir2 = uvw.transform(cosine_hemisphere<R>(g2)); \
             } \
-            segs += dir2.x == (R)-7 ? 1u : 0u; \
+            ntest += dir2.x == (R)-7 ? 1u : 0u; \
         } \
     } while (0)
 #else
@@ -156,13 +156,13 @@ extern "C" int rtw_probe_timeline_read(unsigned long long* out, size_t n, int re
 #define RTW_PROBE_LIGHT_PDF() \
     do { \
         if constexpr (kLightBvh) \
-            segs += (p.light_bvh == 2 \
+            ntest += (p.light_bvh == 2 \
                          ? lights_pdf_grid<kRobust>(p.sc, pnt, RTW_EXP == 7 ? dir : mk(dir.y, dir.z, dir.x)) \
                          : lights_pdf_bvh<kRobust>(p.sc, pnt, RTW_EXP == 7 ? dir : mk(dir.y, dir.z, dir.x), \
                                                    reinterpret_cast<int32_t*>(smem) + wave * p.stack * 64 + \
                                                        lane)) == (R)-7 ? 1u : 0u; \
         else \
-            segs += lights_pdf_sum<kRobust>(li, p.sc.n_lights, pnt, mk(dir.y, dir.z, dir.x)) == (R)-7 ? 1u : 0u; \
+            ntest += lights_pdf_sum<kRobust>(li, p.sc.n_lights, pnt, mk(dir.y, dir.z, dir.x)) == (R)-7 ? 1u : 0u; \
     } while (0)
 #else
 #define RTW_PROBE_LIGHT_PDF()
@@ -173,8 +173,8 @@ extern "C" int rtw_probe_timeline_read(unsigned long long* out, size_t n, int re
     do { \
         { \
             Rng g2; \
-            g2.seed(p.seed ^ 0x55u, pix, s); \
-            segs += (g2.next() & 0xfffu) == 7u ? 1u : 0u; \
+            g2.seed(p.seed ^ 0x55u, pix_now(), s); \
+            ntest += (g2.next() & 0xfffu) == 7u ? 1u : 0u; \
         } \
     } while (0)
 #else
@@ -187,7 +187,7 @@ extern "C" int rtw_probe_timeline_read(unsigned long long* out, size_t n, int re
         const V3<double> dp_ = {d64.y, d64.z, d64.x}; \
         double t2_ = 0.0; \
         if (RTW_EXP == 8 && self_s >= 0) { \
-            if (sphere_t_ref64(p.sc.sph64[self_s], o64, dp_, t2_) && t2_ == -7.0) ++segs; \
+            if (sphere_t_ref64(p.sc.sph64[self_s], o64, dp_, t2_) && t2_ == -7.0) ++ntest; \
         } \
         if (RTW_EXP == 9) { \
             float tb2_ = (float)INFINITY; \
@@ -197,10 +197,10 @@ extern "C" int rtw_probe_timeline_read(unsigned long long* out, size_t n, int re
                 bvh_closest_excl<kWorld == kWorldBvhLds ? kWorldBvhWW : kWorld, kRobust>( \
                     scw, sbase, o, mk(d.y, d.z, d.x), tmin, tb2_, b2_, stk2_, nvis, ntest, -1); \
             } \
-            if (b2_ == -7) ++segs; \
+            if (b2_ == -7) ++ntest; \
         } \
         if (RTW_EXP == 10 && best >= sbase) { \
-            if (sphere_t_ref64(p.sc.sph64[best - sbase], o64, dp_, t2_) && t2_ == -7.0) ++segs; \
+            if (sphere_t_ref64(p.sc.sph64[best - sbase], o64, dp_, t2_) && t2_ == -7.0) ++ntest; \
         } \
     } while (0)
 #else
@@ -213,7 +213,7 @@ extern "C" int rtw_probe_timeline_read(unsigned long long* out, size_t n, int re
         bool keep2; \
         Rng g2 = g; \
         (void)keep2; \
-        if ((expr) == -7.0) ++segs; \
+        if ((expr) == -7.0) ++ntest; \
     } while (0)
 #else
 #define RTW_PROBE_SCATTER64(expr)
@@ -244,7 +244,7 @@ extern "C" int RTW_CAT(rtw_probe_trace_read_, RTW_TRACE)(double* out, size_t n) 
 // {object id (-1 miss), t, origin xyz, direction xyz} of segment max_depth - depth
 #define RTW_PROBE_SEGMENT() \
     do { \
-        if (pix == g_trace_pix && s < kTraceSamples && p.max_depth - depth < kTraceSegs) { \
+        if (pix_now() == g_trace_pix && s < kTraceSamples && p.max_depth - depth < kTraceSegs) { \
             double* rec = g_trace + ((size_t)s * kTraceSegs + (p.max_depth - depth)) * kTraceRec; \
             double t64 = (double)tb, ox = (double)o.x, oy = (double)o.y, oz = (double)o.z; \
             if constexpr (kHit64) { t64 = tb64; ox = o64.x; oy = o64.y; oz = o64.z; } \

@@ -60,7 +60,7 @@ def test_mask_context_and_image_device_match():
         s, keep = scene.as_c()
         assert rtw._lib.rtw_set_scene(ctx, C.byref(s)) == 0
         img = torch.full((cam.image_height, cam.image_width, 3), float("nan"), dtype=torch.float64, device="cuda:0")
-        stream = torch.cuda.current_stream(0).cuda_stream
+        stream = rtw.torch_stream(0)
         rc = rtw._lib.rtw_render_image_device(ctx, C.byref(cam.raw), C.c_uint64(3), C.c_void_p(img.data_ptr()),
                                               img.numel() * 8, C.c_void_p(stream))
         assert rc == 0, rtw._lib.rtw_last_error(ctx)
@@ -77,7 +77,7 @@ def test_mask_context_and_image_device_match():
 def test_repeated_device_rejected():
     with pytest.raises(rtw.RenderError) as e:
         rtw.Renderer(precision=rtw.RTW_F64, devices=[0, 0])
-    assert e.value.args[0] == rtw._capi.RTW_E_INVALID
+    assert e.value.code == rtw._capi.RTW_E_INVALID
     n = torch.cuda.device_count()
     with pytest.raises(rtw.RenderError):
         rtw.Renderer(precision=rtw.RTW_F64, devices=[0, n])      # not visible

@@ -720,7 +720,7 @@ def test_c2_full_frame_rank_split_is_the_single_render(nranks, lpt):
     soa, b = _scene()
     H, W = 800, 1200
     cam = b.with_image_width(W).with_image_height(H).with_samples_per_pixel(2).with_max_depth(50).build()
-    s = torch.cuda.current_stream().cuda_stream
+    s = rtw.torch_stream(torch.cuda.current_device())
     with rtw.Renderer(precision=rtw.RTW_F32) as r:
         r.set_tuning("lpt", lpt)
         r.set_tuning("lpt_min_spp", 1)

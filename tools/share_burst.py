@@ -33,7 +33,7 @@ def main():
         r.set_tuning(k, int(v))
     r.set_scene(scene)
     buf = torch.empty((rtw.tiles_for_rank(W, H, 0, 1) * 64 * 3,), dtype=torch.float32, device="cuda:0")
-    stream = torch.cuda.current_stream().cuda_stream
+    stream = rtw.torch_stream(torch.cuda.current_device())
     r.render_device(cam, 1, buf.data_ptr(), buf.numel() * 4, stream=stream)
     torch.cuda.synchronize()
     for n in (int(x) for x in a.ns.split(",")):
