@@ -128,7 +128,7 @@ def attach_pmc(roof, workload, kname, sha):
     roof["isa_sha"] = sha
     roof["traffic"] = t["bytes_per_launch"] if t else None
     roof["traffic_source"] = t["file"] if t else None
-    for k in ("valu_issue_frac", "lanes_active_frac", "wave_wait_frac", "scratch_write_frac"):
+    for k in ("valu_issue_frac", "lanes_active_frac", "wave_wait_frac", "mem_wait_frac", "scratch_write_frac"):
         roof[k] = t.get(k) if t else None
     return roof
 

@@ -34,11 +34,16 @@ namespace dev {
 
 // Experiment hooks: every RTW_PROBE_* below expands to nothing in the product
 // build; the profiling builds of tools/exp_cost.sh (RTW_EXP) and
-// tools/trace_paths.py (RTW_TRACE) and tools/lane_profile.py (RTW_PROF)
-// define them in rtw_probes.hpp.
-#if defined(RTW_EXP) || defined(RTW_TRACE) || defined(RTW_PROF) || defined(RTW_TIMELINE) || defined(RTW_ABL)
+// tools/trace_paths.py (RTW_TRACE), tools/lane_profile.py (RTW_PROF) and
+// tools/clock_profile.py (RTW_CLOCK) define them in rtw_probes.hpp.
+#if defined(RTW_EXP) || defined(RTW_TRACE) || defined(RTW_PROF) || defined(RTW_TIMELINE) || defined(RTW_ABL) || \
+    defined(RTW_CLOCK) || defined(RTW_NANORIGIN)
 #include "rtw_probes.hpp"
 #else
+#define RTW_PROBE_NAN_LAMBERT(was, now, obj)
+#define RTW_PROBE_CLK_INIT()
+#define RTW_PROBE_CLK(id)
+#define RTW_PROBE_CLK_END()
 #define RTW_PROBE_WAVE_BEGIN()
 #define RTW_PROBE_WAVE_TASK()
 #define RTW_PROBE_WAVE_END()
@@ -531,6 +536,53 @@ __device__ __forceinline__ float lights_pdf_sum_pk(const R4<float>* __restrict__
     return acc;
 }
 
+// lights_pdf_sum (f64) with the pre-pass on packed FP32, two lights per
+// instruction (the light_may_hit arithmetic per component).  lp = the lights as
+// pairs, three R4 per pair {x0, x1, y0, y1}, {z0, z1, |r0|, |r1|}, {L0, L1, -, -}
+// with L = |cx| + |cy| + |cz| + |r| (an odd list ends with a NaN light: never
+// a candidate), staged in LDS.  The slack e = 2^-18 (|o|_1 + L) differs from
+// the scalar pre-pass's only in the order of its additions (an ulp of e):
+// the same bound, far above the f32 error.
+__device__ __forceinline__ double lights_pdf_sum_pk64(const R4<double>* __restrict__ li,
+                                                      const R4<float>* __restrict__ lp, uint32_t n,
+                                                      V3<double> o, V3<double> d) {
+    const LightPre pre(o, d);
+    const f2v ox = {pre.ox, pre.ox}, oy = {pre.oy, pre.oy}, oz = {pre.oz, pre.oz};
+    const f2v dx = {pre.dx, pre.dx}, dy = {pre.dy, pre.dy}, dz = {pre.dz, pre.dz};
+    const f2v ia2 = {pre.ia, pre.ia}, on2 = {pre.on, pre.on}, dn2 = {2.0f * pre.dn, 2.0f * pre.dn};
+    const f2v k18 = {0x1p-18f, 0x1p-18f};
+    double acc = 0.0;
+    for (uint32_t base = 0; base < n; base += 32) {
+        const uint32_t m = min(32u, n - base);
+        uint32_t mask = 0;
+#pragma unroll 2
+        for (uint32_t k = 0; k < m; k += 2) {
+            const R4<float> A = lp[(base + k) / 2 * 3], B = lp[(base + k) / 2 * 3 + 1], C = lp[(base + k) / 2 * 3 + 2];
+            const f2v fx = ox - f2v{A.x, A.y}, fy = oy - f2v{A.z, A.w}, fz = oz - f2v{B.x, B.y};
+            const f2v r = {B.z, B.w};
+            const f2v hb = __builtin_elementwise_fma(dz, fz, __builtin_elementwise_fma(dy, fy, dx * fx));
+            const f2v tc = -hb * ia2;
+            const f2v lx = __builtin_elementwise_fma(tc, dx, fx), ly = __builtin_elementwise_fma(tc, dy, fy),
+                      lz = __builtin_elementwise_fma(tc, dz, fz);
+            const f2v l2 = __builtin_elementwise_fma(lx, lx, __builtin_elementwise_fma(ly, ly, lz * lz));
+            const f2v f2 = __builtin_elementwise_fma(fx, fx, __builtin_elementwise_fma(fy, fy, fz * fz));
+            const f2v e = k18 * (on2 + f2v{C.x, C.y});
+            const f2v re = r + e, rr = re * re, ed = e * dn2;
+            const bool h0 = (l2.x <= rr.x) & ((hb.x <= ed.x) | (f2.x <= rr.x));
+            const bool h1 = (l2.y <= rr.y) & ((hb.y <= ed.y) | (f2.y <= rr.y));
+            mask |= ((h0 ? 1u : 0u) | (h1 ? 2u : 0u)) << k;
+        }
+        mask &= m == 32 ? 0xffffffffu : ((1u << m) - 1u);
+        while (mask) {
+            const uint32_t k = (uint32_t)__builtin_ctz(mask);
+            mask &= mask - 1u;
+            const R4<double> L = li[base + k];
+            acc = acc + sphere_pdf_value(mk(L.x, L.y, L.z), L.w, o, d);
+        }
+    }
+    return acc;
+}
+
 // ---------------------------------------------------------------------------
 // BVH closest hit (RTW_ACCEL_BVH).  Box tests only cull; every surviving
 // sphere goes through the same per-sphere arithmetic as the brute-force
@@ -973,42 +1025,65 @@ struct StealSlots<float> {
 };
 template <>
 struct StealSlots<double> {
+    // per ray: the exact result (t bits, id) -- lowered only by full folds, so
+    // its id always belongs to its t -- and a culling bound (t bits) that the
+    // lanes on the ray lower after every leaf phase with one atomic
     unsigned long long* tb;
     uint32_t* id;
+    unsigned long long* cull;
+    // a lane whose bound came from another lane's hit holds no hit at that t:
+    // its id is above every real id (ties at that t go to the real hit; the
+    // full fold's id step never picks it)
+    static constexpr int32_t kForeign = 0x7fffffff;
     __device__ __forceinline__ explicit StealSlots(unsigned char* area)
-        : tb(reinterpret_cast<unsigned long long*>(area)), id(reinterpret_cast<uint32_t*>(area + 64 * 8)) {}
+        : tb(reinterpret_cast<unsigned long long*>(area)), id(reinterpret_cast<uint32_t*>(area + 64 * 8)),
+          cull(reinterpret_cast<unsigned long long*>(area + 64 * 12)) {}
     static __device__ __forceinline__ uint64_t bits(double t) { return (uint64_t)__double_as_longlong(t); }
     template <typename TT>
     __device__ __forceinline__ void init(uint32_t lane, const TT& T) {
         tb[lane] = bits(T.tb);
         id[lane] = (uint32_t)T.best;
+        cull[lane] = bits(T.tb);
     }
+    // the exact (t, id) into the owner's result, in the tester's order
+    // (smallest t, then lowest id; best = -1 above every id): an atomic min of
+    // t, then the id of a lane whose t is the new minimum (stored by the lane
+    // that lowered it, atomic min among equal t).  Every lane of the wave calls
+    // it (`on` selects the folding lanes).
     template <typename TT>
-    __device__ __forceinline__ void fold(bool on, int32_t owner, TT& T, bool share) {
+    __device__ __forceinline__ void fold(bool on, int32_t owner, TT& T, bool) {
         const uint64_t t = bits(T.tb);
         bool lowered = false;
-        if (on) lowered = t < atomicMin(tb + owner, (unsigned long long)t);
+        if (on) {
+            lowered = t < atomicMin(tb + owner, (unsigned long long)t);
+            atomicMin(cull + owner, (unsigned long long)t);
+        }
         __builtin_amdgcn_wave_barrier();
         const uint64_t cur = on ? tb[owner] : 0;
         if (on && t == cur && lowered) id[owner] = (uint32_t)T.best;
         __builtin_amdgcn_wave_barrier();
         if (on && t == cur) atomicMin(id + owner, (uint32_t)T.best);
-        if (share) {
-            __builtin_amdgcn_wave_barrier();
-            if (on) {
-                T.tb = __longlong_as_double((long long)cur);
-                T.best = (int32_t)id[owner];
+    }
+    // after a leaf phase: share the bound only (one returning atomic); a lane
+    // whose t is above the ray's bound takes it with the foreign id
+    template <typename TT>
+    __device__ __forceinline__ void share(bool on, int32_t owner, TT& T) {
+        if (on) {
+            const uint64_t t = bits(T.tb);
+            const uint64_t prev = atomicMin(cull + owner, (unsigned long long)t);
+            if (prev < t) {
+                T.tb = __longlong_as_double((long long)prev);
+                T.best = kForeign;
             }
         }
     }
     template <typename TT>
     __device__ __forceinline__ void refresh(bool on, int32_t owner, TT& T) {
         if (on) {
-            const uint64_t t = tb[owner];
-            const uint32_t i = id[owner];
-            if (t < bits(T.tb) || (t == bits(T.tb) && i < (uint32_t)T.best)) {
+            const uint64_t t = cull[owner];
+            if (t < bits(T.tb)) {
                 T.tb = __longlong_as_double((long long)t);
-                T.best = (int32_t)i;
+                T.best = kForeign;
             }
         }
     }
@@ -1018,6 +1093,14 @@ struct StealSlots<double> {
         T.best = (int32_t)id[lane];
     }
 };
+template <typename TT>
+__device__ __forceinline__ void steal_share(StealSlots<float>& S, bool on, int32_t owner, TT& T) {
+    S.fold(on, owner, T, true);
+}
+template <typename TT>
+__device__ __forceinline__ void steal_share(StealSlots<double>& S, bool on, int32_t owner, TT& T) {
+    S.share(on, owner, T);
+}
 
 // bvh_traverse_ww with intra-wave subtree stealing.  A lane with nothing left
 // to traverse -- its ray done, or never started (the own-sphere shortcut) --
@@ -1152,8 +1235,9 @@ __device__ __forceinline__ void bvh_traverse_steal(const DevScene<R>& sc, int32_
             leaf = 0;
         }
         // share the bound: every lane on this ray culls with the best hit any
-        // of them has found so far
-        slots.fold(tested, owner, T, true);
+        // of them has found so far (f32: the exact key; f64: the bound only,
+        // the exact (t, id) is folded when a lane leaves the ray)
+        steal_share(slots, tested, owner, T);
         if (tested) bound();
     }
     slots.fold(true, owner, T, false);
@@ -1920,11 +2004,28 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                 l_lp[2 * q + 1] = R4<R>{A.z, B.z, A.w * A.w, odd ? B.w * B.w : (R)-INFINITY};
             }
         } else {
-            // the lights rounded to f32 with |radius| (the f32 pre-pass of lights_pdf_sum)
+            // the lights rounded to f32 as pairs (the packed pre-pass of lights_pdf_sum_pk64)
             l_li32 = reinterpret_cast<R4<float>*>(l_li + p.sc.n_lights);
-            for (uint32_t k = threadIdx.x; k < p.sc.n_lights; k += kBlock) {
-                const R4<R> L = p.sc.lights[k];
-                l_li32[k] = R4<float>{(float)L.x, (float)L.y, (float)L.z, fabsf((float)L.w)};
+            const uint32_t n = p.sc.n_lights;
+            for (uint32_t q = threadIdx.x; 2 * q < n; q += kBlock) {
+                auto f32 = [&](uint32_t k, float& x, float& y, float& z, float& r) {
+                    if (k < n) {
+                        const R4<R> L = p.sc.lights[k];
+                        x = (float)L.x;
+                        y = (float)L.y;
+                        z = (float)L.z;
+                        r = fabsf((float)L.w);
+                    } else {
+                        x = y = z = r = __builtin_nanf("");
+                    }
+                };
+                float ax, ay, az, ar, bx, by, bz, br;
+                f32(2 * q, ax, ay, az, ar);
+                f32(2 * q + 1, bx, by, bz, br);
+                l_li32[3 * q] = R4<float>{ax, bx, ay, by};
+                l_li32[3 * q + 1] = R4<float>{az, bz, ar, br};
+                l_li32[3 * q + 2] = R4<float>{fabsf(ax) + fabsf(ay) + fabsf(az) + ar,
+                                              fabsf(bx) + fabsf(by) + fabsf(bz) + br, 0.0f, 0.0f};
             }
         }
         __syncthreads();
@@ -2053,6 +2154,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
     V3<R> pend_aw = zero;
     R pend_ch = (R)0;
     RTW_PROBE_WAVE_BEGIN();
+    RTW_PROBE_CLK_INIT();
 
     auto start_sample = [&]() {
         const KArgs* k = kargs();
@@ -2136,12 +2238,14 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
     };
     // the first 64 items of the first task go to lanes 0..63 in order
     acquire();
+    RTW_PROBE_CLK(0);
 
     for (;;) {
         const uint64_t live = __ballot(active);
         if (live == 0) break;
         segs += (uint32_t)__popcll(live);   // every active lane runs one segment of this trip
         bool lamb = false;                  // the lane's segment ended in a Lambertian scatter
+        RTW_PROBE_CLK(12);
         RTW_PROBE_LANES(3);
         if (active) {
             RTW_PROBE_LANES(4);
@@ -2192,6 +2296,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                     best = bbase + k;
                 }
             }
+            RTW_PROBE_CLK(1);
             if constexpr (kHit64) {
                 // the own sphere's re-hit in f64, the others in f32 (it excluded), the
                 // winner's t again in f64
@@ -2253,6 +2358,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
             } else {
                 sweep_spheres<kRobust>(sph, kargs()->sc.n_sph, sbase, o, d, tmin, tb, best);
             }
+            RTW_PROBE_CLK(2);
             RTW_PROBE_SEGMENT();
 
             bool done = false;
@@ -2365,6 +2471,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                         colour = tex_colour(p.sc, kargs()->sc.mat_tex[m], hu, hv, pnt);
                 }
                 const V3<R> emitted = kEmit && mtype == kMatDiffuseLight ? colour : zero;
+                RTW_PROBE_CLK(3);
                 if (kHit64 && sph_hit) {
                     // Metal / Dielectric sphere: the f64 scatter of both in one pass
                     RTW_PROBE_LANES(7);
@@ -2383,6 +2490,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                         o64 = pnt64;
                         d = from64<R>(d64);
                     }
+                    RTW_PROBE_CLK(6);
                 } else if (sizeof(R) == 8 && (mtype == kMatMetal || mtype == kMatDielectric)) {
                     // f64: Metal::scatter and Dialectric::scatter (material.rs:407-421,
                     // 458-487) in one pass (specular_dir64 with the reference's
@@ -2404,6 +2512,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                         self_iso = next_iso;
                         d = from64<R>(dir);
                     }
+                    RTW_PROBE_CLK(6);
                 } else if (mtype == kMatMetal) {
                     RTW_PROBE_LANES(7);
                     // Metal::scatter, material.rs:407-421
@@ -2423,6 +2532,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                         }
                         d = dir;
                     }
+                    RTW_PROBE_CLK(7);
                 } else if (mtype == kMatDielectric) {
                     RTW_PROBE_LANES(8);
                     // Dialectric::scatter, material.rs:458-487
@@ -2443,13 +2553,16 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                     self_iso = next_iso;
                     if constexpr (kHit64) o64 = pnt64;
                     d = dir;
+                    RTW_PROBE_CLK(8);
                 } else if (mtype == kMatLambertian) {
                     RTW_PROBE_LANES(9);
                     // Lambertian + MixturePdf(HittablePdf(lights), CosinePdf):
                     // material.rs:357-376, pdf.rs:33-101, camera.rs:504-521
                     lamb = true;
                     const V3<R> att = colour;
-                    const Onb<R> uvw(nrm);
+                    // the normal's Onb (onb.rs:8-35) is built by mixture_direction
+                    // for the cosine lanes only; the pdf needs its w = normalize(n)
+                    const V3<R> wn = PR::normalize(nrm);
                     V3<R> dir;
                     const bool to_light = PR::u_std(g.next()) < (R)0.5;
                     bool sampled = false;
@@ -2480,11 +2593,12 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                         // or the cosine lobe, in one pass (mixture_direction)
                         R4<R> L = R4<R>{0, 0, 0, 0};
                         if (to_light) L = li[g.index(kargs()->sc.n_lights)];
-                        dir = mixture_direction(to_light, uvw, mk(L.x, L.y, L.z), L.w, pnt, g);
+                        dir = mixture_direction(to_light, nrm, mk(L.x, L.y, L.z), L.w, pnt, g);
                     }
                     RTW_PROBE_LAMBERT_DIR();
+                    RTW_PROBE_CLK(4);
                     const V3<R> ndir = PR::normalize(dir);
-                    const R cos_w = PR::over_pi(dot(ndir, uvw.w));
+                    const R cos_w = PR::over_pi(dot(ndir, wn));
                     R acc;                                                // hittable_list.rs:408-412
                     // the light grid's walk by the whole wave: deferred to the end of the trip
                     const bool coop = kCoopGrid && p.light_bvh == 2 && p.grid_piece != 0 && !(kPrims && kargs()->sc.lref);
@@ -2513,10 +2627,11 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                     else if constexpr (kWorld == kWorldBvhLds && sizeof(R) == 4)
                         acc = lights_pdf_sum_pk<kRobust>(li, l_lp, kargs()->sc.n_lights, pnt, dir);
                     else if constexpr (kWorld == kWorldBvhLds && sizeof(R) == 8)
-                        acc = lights_pdf_sum<kRobust>(li, kargs()->sc.n_lights, pnt, dir, l_li32);
+                        acc = lights_pdf_sum_pk64(li, l_li32, kargs()->sc.n_lights, pnt, dir);
                     else
                         acc = lights_pdf_sum<kRobust>(li, kargs()->sc.n_lights, pnt, dir);
                     RTW_PROBE_LIGHT_PDF();
+                    RTW_PROBE_CLK(5);
                     // / len; a BVH leaf list multiplies by len and divides again (bvh.rs:67-76, 191-194)
                     R lpdf = PR::div_(acc, (R)p.sc.n_list);
                     if (p.sc.light_flags & 1u) lpdf = PR::div_(lpdf * (R)p.sc.n_list, (R)p.sc.n_list);
@@ -2524,6 +2639,8 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                     const R spdf = PR::max_(PR::over_pi(dot(nrm, ndir)), (R)0);
                     const V3<R> w = PR::divs(att * spdf, pdf);
                     const V3<R> new_mult = mult * w;
+                    RTW_PROBE_NAN_LAMBERT(__builtin_isnan(mult.x + mult.y + mult.z),
+                                          __builtin_isnan(new_mult.x + new_mult.y + new_mult.z), best);
                     res.add(mult, emitted);
                     mult = new_mult;
                     o = pnt;
@@ -2535,6 +2652,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                     }
                     d = dir;
                     }
+                    RTW_PROBE_CLK(4);
                 } else {
                     // Invisible (material.rs:321-325): scatter() == None
                     col = mult * emitted + res.value();
@@ -2578,6 +2696,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                 }
             }
         }
+        RTW_PROBE_CLK(9);
         lambs += (uint32_t)__popcll(__ballot(lamb));
         if constexpr (kCoopGrid) {
             // the deferred Lambertian light pdfs of this trip, by the whole wave;
@@ -2629,10 +2748,14 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                     pend = false;
                 }
             }
+            RTW_PROBE_CLK(11);
         }
         acquire();
+        RTW_PROBE_CLK(0);
     }
 
+    RTW_PROBE_CLK(10);
+    RTW_PROBE_CLK_END();
     RTW_PROBE_WAVE_END();
     // wave-reduce the per-lane counters (segs, lambs are per wave), one atomic per wave
     for (int off = 32; off > 0; off >>= 1) {
@@ -2652,15 +2775,19 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
 // image: 0).  The fold accumulates in double whatever R is: with many chunks
 // (C4: 4096 spp) an f32 running sum would lose low bits; in f64 mode this is
 // the reference's sequential f64 fold (camera.rs:323-335).
-constexpr uint32_t kFoldWindow = 16;                  // chunks staged per pass
-constexpr uint32_t kFoldRow = kFoldWindow * 3 + 1;    // LDS row (odd: no bank conflicts)
+// chunks staged per pass: 12 KiB of LDS per wave in either precision (f64 at
+// 16 chunks took 25 KiB: six waves per CU, too few to keep the loads in flight)
+template <typename R>
+constexpr uint32_t kFoldWindow = sizeof(R) == 4 ? 16 : 8;
 
 template <typename R>
 __global__ void __launch_bounds__(64) reduce_chunks_kernel(const KParams<R> p, R* __restrict__ out) {
+    constexpr uint32_t kFoldWin = kFoldWindow<R>;
+    constexpr uint32_t kFoldRow = kFoldWin * 3 + 1;    // LDS row (odd: no bank conflicts)
     // one wave per tile; a pixel's chunk sums are contiguous (the sample-major
     // item pool hands the lanes consecutive chunks of one pixel, whose sums
     // then fill whole cache lines together), so the wave stages a window of
-    // kFoldWindow chunks x 64 pixels through LDS with row-contiguous loads and
+    // kFoldWin chunks x 64 pixels through LDS with row-contiguous loads and
     // each lane folds its pixel's row in chunk order
     __shared__ R win[64 * kFoldRow];
     const uint32_t lt = blockIdx.x, lane = threadIdx.x;
@@ -2670,11 +2797,11 @@ __global__ void __launch_bounds__(64) reduce_chunks_kernel(const KParams<R> p, R
     const size_t row_len = (size_t)p.n_chunks * 3;
     const R* tile = p.partial + (size_t)lt * 64 * row_len;
     double sx = 0, sy = 0, sz = 0;
-    constexpr uint32_t kNv = kFoldWindow * 3;
-    for (uint32_t c0 = 0; c0 < p.n_chunks; c0 += kFoldWindow) {
-        const uint32_t kw = min(kFoldWindow, p.n_chunks - c0), nv = kw * 3;
+    constexpr uint32_t kNv = kFoldWin * 3;
+    for (uint32_t c0 = 0; c0 < p.n_chunks; c0 += kFoldWin) {
+        const uint32_t kw = min(kFoldWin, p.n_chunks - c0), nv = kw * 3;
         const R* src = tile + (size_t)c0 * 3;
-        if (kw == kFoldWindow) {
+        if (kw == kFoldWin) {
             // full window: every lane's kNv loads issued back to back
             R v[kNv];
 #pragma unroll

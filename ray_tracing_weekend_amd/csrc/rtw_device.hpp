@@ -373,7 +373,7 @@ __device__ __forceinline__ V3<R> sphere_random(V3<R> c, R radius, V3<R> o, Rng& 
 // The Lambertian mixture's direction (MixturePdf::generate, pdf.rs:91-96)
 // for a light list of spheres: to_light -> Sphere::random of light L
 // (sphere.rs:113-127, as sphere_random), else CosinePdf::generate in the
-// normal's frame uvw (pdf.rs:45-48, as cosine_hemisphere).  Both draw r1, r2,
+// normal's frame (pdf.rs:45-48, as cosine_hemisphere).  Both draw r1, r2,
 // take an azimuth from one and a height from the other and rotate by a
 // frame, so one code path serves both: the lanes of a wave that took either
 // branch run it together (one pass instead of two).  Per lane the words and
@@ -381,17 +381,15 @@ __device__ __forceinline__ V3<R> sphere_random(V3<R> c, R radius, V3<R> o, Rng& 
 // same bit for bit (f64: the oracle's rtwo_sphere_random /
 // rtwo_cosine_hemisphere).
 template <typename R>
-__device__ __forceinline__ V3<R> mixture_direction(bool to_light, const Onb<R>& uvw, V3<R> c, R radius, V3<R> o,
-                                                   Rng& g) {
-    V3<R> fu = uvw.u, fv = uvw.v, fw = uvw.w;
+__device__ __forceinline__ V3<R> mixture_direction(bool to_light, V3<R> n, V3<R> c, R radius, V3<R> o, Rng& g) {
+    // one Onb per lane: the light direction's (Sphere::random) or the normal's
+    // (CosinePdf::generate), built by the same code for both
+    const V3<R> direction = c - o;
+    const Onb<R> f(to_light ? direction : n);
+    const V3<R> fu = f.u, fv = f.v, fw = f.w;
     R q = (R)0;   // light: r^2 / distance^2
     if (to_light) {
-        const V3<R> direction = c - o;
         const R distance = P<R>::sqrt_(dot(direction, direction));
-        const Onb<R> lf(direction);
-        fu = lf.u;
-        fv = lf.v;
-        fw = lf.w;
         if constexpr (sizeof(R) == 4) q = radius * radius * __builtin_amdgcn_rcpf(distance * distance);
         else q = P<R>::div_(radius * radius, distance * distance);
     }

@@ -174,7 +174,7 @@ constexpr uint32_t kCoopStash = 20;
 // key; f64: u64 t bits + u32 id) and 64 rendezvous bytes, in LDS right after
 // the traversal stacks of the workgroup's waves.
 template <typename R>
-constexpr uint32_t kStealSlotBytes = sizeof(R) == 4 ? 64 * 8 : 64 * 12;
+constexpr uint32_t kStealSlotBytes = sizeof(R) == 4 ? 64 * 8 : 64 * 20;   // f64: + a culling bound per ray
 template <typename R>
 constexpr uint32_t kStealLdsPerWave = kStealSlotBytes<R> + 64;
 // LDS of the traversal stacks + the stealing area of one workgroup

@@ -24,11 +24,29 @@
 // own-sphere f64 test, 6 = closest-hit query, 7 = Metal, 8 = Dielectric,
 // 9 = Lambertian, 10 = next sample), read back with rtw_probe_lanes_read.
 //
+// RTW_CLOCK (tools/clock_profile.py): the wave's shader-clock cycles by part
+// of the segment loop -- RTW_PROBE_CLK(id) charges the cycles since the last
+// probe to part `id` (a ds_add_u64 by the first active lane into the wave's
+// LDS slots; the parts a wave runs one after another under different exec
+// masks are charged separately), summed over waves into g_clk at the end.
+// 0 item pool + sample start, 1 planes, 2 closest hit, 3 hit record,
+// 4 Lambertian (direction + throughput), 5 light pdf, 6 f64 specular,
+// 7 Metal, 8 Dielectric, 9 sample end, 10 wave tail (no item left),
+// 11 cooperative light-grid walk, 12 loop head.
+//
+// RTW_NANORIGIN (tools/nan_origins.py): per world object, the samples whose
+// throughput turned NaN at a Lambertian bounce off that object (g_nan[1 +
+// object id]; g_nan[0]: NaN at any other point of the path, counted at the
+// sample's end).
+//
 // RTW_TRACE (tools/trace_paths.py): record every segment of the first
 // kTraceSamples samples of one pixel -- the ray (origin, direction) and the
 // closest hit (object id, t) -- into a device array the tool reads back with
 // rtw_probe_trace_read_f32 / _f64 (exported by the trace build only).
 #pragma once
+
+#define RTW_CAT2(a, b) a##b
+#define RTW_CAT(a, b) RTW_CAT2(a, b)
 
 #ifndef RTW_EXP
 #define RTW_EXP 0
@@ -143,7 +161,7 @@ extern "C" int rtw_probe_timeline_read(unsigned long long* out, size_t n, int re
                 const R4<R> L = li[g2.index(p.sc.n_lights)]; \
                 dir2 = sphere_random(mk(L.x, L.y, L.z), L.w, pnt, g2); \
             } else { \
-                dir2 = uvw.transform(cosine_hemisphere<R>(g2)); \
+                dir2 = Onb<R>(nrm).transform(cosine_hemisphere<R>(g2)); \
             } \
             ntest += dir2.x == (R)-7 ? 1u : 0u; \
         } \
@@ -226,8 +244,6 @@ extern "C" int rtw_probe_timeline_read(unsigned long long* out, size_t n, int re
 constexpr uint32_t kTraceSamples = 64, kTraceSegs = 64, kTraceRec = 8;
 static __device__ double g_trace[kTraceSamples * kTraceSegs * kTraceRec];
 static __device__ unsigned long long g_trace_pix = ~0ull;
-#define RTW_CAT2(a, b) a##b
-#define RTW_CAT(a, b) RTW_CAT2(a, b)
 // set the traced pixel (j * W + i) and clear the array / copy it out (n doubles)
 extern "C" int RTW_CAT(rtw_probe_trace_set_, RTW_TRACE)(unsigned long long pix) {
     static double zero[kTraceSamples * kTraceSegs * kTraceRec];
@@ -277,4 +293,62 @@ extern "C" int rtw_probe_lanes_read(unsigned long long* out, int reset) {
 }
 #else
 #define RTW_PROBE_LANES(id)
+#endif
+
+#ifdef RTW_CLOCK
+constexpr int kClkParts = 16;
+static __device__ unsigned long long g_clk[kClkParts];
+#define RTW_PROBE_CLK_INIT() \
+    __shared__ unsigned long long clk_lds_[kWavesPerBlock][kClkParts]; \
+    if (lane < (uint32_t)kClkParts) clk_lds_[wave][lane] = 0; \
+    uint64_t clk_t_ = __builtin_amdgcn_s_memtime()
+#define RTW_PROBE_CLK(id) \
+    do { \
+        const uint64_t n_ = __builtin_amdgcn_s_memtime(); \
+        const uint64_t m_ = __ballot(true); \
+        if ((uint32_t)__lane_id() == (uint32_t)__builtin_ctzll(m_)) \
+            atomicAdd(&clk_lds_[wave][(id)], (unsigned long long)(n_ - clk_t_)); \
+        clk_t_ = n_; \
+    } while (0)
+#define RTW_PROBE_CLK_END() \
+    do { \
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront"); \
+        __builtin_amdgcn_wave_barrier(); \
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront"); \
+        if (lane < (uint32_t)kClkParts) atomicAdd(&g_clk[lane], clk_lds_[wave][lane]); \
+    } while (0)
+extern "C" int RTW_CAT(rtw_probe_clock_read_, RTW_CLOCK)(unsigned long long* out, int reset) {
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_clk), sizeof g_clk) != hipSuccess) return -1;
+    if (reset) {
+        static unsigned long long zero[kClkParts];
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_clk), zero, sizeof zero) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#else
+#define RTW_PROBE_CLK_INIT()
+#define RTW_PROBE_CLK(id)
+#define RTW_PROBE_CLK_END()
+#endif
+
+#ifdef RTW_NANORIGIN
+constexpr int kNanSlots = 1 << 16;
+static __device__ unsigned long long g_nan[kNanSlots];
+#define RTW_PROBE_NAN_LAMBERT(was, now, obj) \
+    do { \
+        if (!(was) && (now) && (uint32_t)(obj) + 1u < (uint32_t)kNanSlots) atomicAdd(&g_nan[1 + (obj)], 1ull); \
+    } while (0)
+extern "C" int RTW_CAT(rtw_probe_nan_read_, RTW_NANORIGIN)(unsigned long long* out, size_t n, int reset) {
+    n = n < (size_t)kNanSlots ? n : (size_t)kNanSlots;
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_nan), n * sizeof(unsigned long long)) != hipSuccess) return -1;
+    if (reset) {
+        static unsigned long long zero[kNanSlots];
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_nan), zero, sizeof zero) != hipSuccess) return -1;
+    }
+    return (int)n;
+}
+#else
+#define RTW_PROBE_NAN_LAMBERT(was, now, obj)
 #endif

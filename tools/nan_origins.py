@@ -1,0 +1,101 @@
+#!/usr/bin/env python3
+"""Where NaN samples come from, f32 (hit64) vs f64 at the same seed
+(experiment tool; the RTW_NANORIGIN build, rtw_probes.hpp): per world object,
+the samples whose throughput turned NaN at a Lambertian bounce off it -- a
+point inside a light sphere (Sphere::pdf_value's sqrt of a negative,
+sphere.rs:101-111).  Object ids: planes first, then spheres.
+
+    python tools/nan_origins.py build
+    python tools/nan_origins.py run [--spp 100] [--seed 5] [--tuning k=v,...]
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+VAR = os.path.join(ROOT, "build", "variants", "nan")
+
+
+def build():
+    cs = os.path.join(ROOT, "ray_tracing_weekend_amd", "csrc")
+    b = os.path.join(ROOT, "ray_tracing_weekend_amd", "build")
+    os.makedirs(VAR, exist_ok=True)
+    common = ["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "-fno-slp-vectorize", "--offload-arch=gfx950",
+              f"-I{cs}", f"-I{ROOT}/include"]
+    subprocess.run(common + ["-ffp-contract=on", "-DRTW_NANORIGIN=f32", "-c", f"{cs}/render_f32.hip", "-o",
+                             f"{VAR}/render_f32.o"], check=True)
+    subprocess.run(common + ["-ffp-contract=off", "-DRTW_NANORIGIN=f64", "-c", f"{cs}/render_f64.hip", "-o",
+                             f"{VAR}/render_f64.o"], check=True)
+    subprocess.run(common + ["-ffp-contract=off", "-c", f"{cs}/capi.cpp", "-o", f"{VAR}/capi.o"], check=True)
+    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o", f"{VAR}/librtw.so",
+                    f"{VAR}/render_f32.o", f"{VAR}/render_f64.o", f"{VAR}/capi.o", f"{b}/rtw_host.o", f"{b}/bvh.o",
+                    "-ldl"], check=True)
+    for f in ("render_f32.o", "render_f64.o", "capi.o"):
+        os.remove(os.path.join(VAR, f))
+    print("built", f"{VAR}/librtw.so")
+
+
+def run(a):
+    os.environ["RTW_LIB_OVERRIDE"] = os.path.join(VAR, "librtw.so")
+    sys.path.insert(0, ROOT)
+    import numpy as np
+    import ray_tracing_weekend_amd as rtw
+    soa, b = rtw.scenes.simple_soa(0x5EED0001)
+    cam = b.with_image_width(1200).with_image_height(800).with_samples_per_pixel(a.spp).with_max_depth(50).build()
+    n_pl = len(soa.plane_mat)
+    sph = np.asarray(soa.spheres).reshape(-1, 4)
+    lights = np.asarray(soa.lights).reshape(-1, 4)
+    mtype = np.asarray(soa.mat_type)
+    smat = np.asarray(soa.sphere_mat)
+    out = {"spp": a.spp, "seed": a.seed, "tuning": a.tuning}
+    counts = {}
+    for name, prec in (("f32", rtw.RTW_F32), ("f64", rtw.RTW_F64)):
+        rd = getattr(rtw._lib, f"rtw_probe_nan_read_{name}")
+        rd.argtypes = [C.c_void_p, C.c_size_t, C.c_int]
+        n = 1 + n_pl + len(sph)
+        buf = (C.c_ulonglong * n)()
+        with rtw.Renderer(precision=prec) as r:
+            for kv in filter(None, a.tuning.split(",")):
+                k, v = kv.split("=")
+                r.set_tuning(k, int(v))
+            r.set_scene(soa)
+            rd(buf, n, 1)
+            img = r.render(cam, a.seed)
+            st = r.stats
+            assert rd(buf, n, 1) >= 0
+        c = np.array(buf[1:], dtype=np.int64)
+        counts[name] = c
+        out[name] = {"nan_origin_samples": int(c.sum()), "nan_pixels": int(np.isnan(img).any(-1).sum()),
+                     "segments_per_sample": round(st.segments / st.samples, 5)}
+    # per-sphere comparison: the spheres with the most NaN origins in either mode
+    f32, f64 = counts["f32"], counts["f64"]
+    top = np.argsort(-(f32 + f64))[:25]
+    rows = []
+    for k in top:
+        if f32[k] + f64[k] == 0:
+            break
+        rec = {"object": int(k), "f32": int(f32[k]), "f64": int(f64[k])}
+        if k >= n_pl:
+            s = sph[k - n_pl]
+            d = np.linalg.norm(lights[:, :3] - s[:3], axis=1)
+            inside = np.nonzero(d < np.abs(lights[:, 3]) + abs(s[3]))[0]
+            rec.update(center=[round(float(v), 4) for v in s[:3]], radius=float(s[3]),
+                       material=int(mtype[smat[k - n_pl]]), overlapping_lights=inside.tolist())
+        rows.append(rec)
+    out["top_objects"] = rows
+    z = (f32.sum() - f64.sum()) / max(np.sqrt(f32.sum() + f64.sum()), 1.0)
+    out["origin_diff_z"] = round(float(z), 2)
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("cmd", choices=["build", "run"])
+    ap.add_argument("--spp", type=int, default=100)
+    ap.add_argument("--seed", type=int, default=5)
+    ap.add_argument("--tuning", default="")
+    a = ap.parse_args()
+    build() if a.cmd == "build" else run(a)

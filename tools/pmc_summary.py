@@ -1,7 +1,10 @@
 #!/usr/bin/env python3
 """Summarise rocprofv3 PMC csvs for the render kernel: per-dispatch averages
-over the full renders (a launch under a quarter of the largest one of a
-counter -- a 2-spp tile-cost pilot render, tuning lpt_inline=0 -- is left out)."""
+over the steady-state renders.  Left out: the first render-kernel dispatch of
+each pass (the first render of a scene / camera runs in tile index order and
+counts the tile costs with atomics -- not the schedule the timed steps run)
+and any launch under a quarter of the largest one of a counter (a 2-spp pilot
+render, tuning lpt_inline=0)."""
 import collections, csv, glob, sys
 root = sys.argv[1]
 agg = collections.defaultdict(list)
@@ -10,12 +13,13 @@ for f in sorted(glob.glob(f"{root}/pmc*/pmc_counter_collection.csv")):
     for row in csv.DictReader(open(f)):
         if "render_kernel" not in row["Kernel_Name"]:
             continue
-        per[(row["Dispatch_Id"], row["Counter_Name"])] += float(row["Counter_Value"])
+        per[(int(row["Dispatch_Id"]), row["Counter_Name"])] += float(row["Counter_Value"])
+    first = min((d for d, _ in per), default=None)
     top = collections.defaultdict(float)
     for (d, name), v in per.items():
         top[name] = max(top[name], v)
     for (d, name), v in per.items():
-        if v >= 0.25 * top[name]:
+        if d != first and v >= 0.25 * top[name]:
             agg[name].append(v)
 for k in sorted(agg):
     v = agg[k]
@@ -29,7 +33,8 @@ for k in sorted(agg):
 # wave64 VALU instruction = 2 cycles; GRBM_GUI_ACTIVE sums the 8 XCDs):
 #   valu_issue_frac   = SQ_INSTS_VALU x 2 / (1024 SIMDs x GRBM_GUI_ACTIVE / 8)
 #   lanes_active_frac = SQ_THREAD_CYCLES_VALU / (64 x SQ_INSTS_VALU)
-#   wave_wait_frac    = SQ_WAIT_INST_ANY / SQ_WAVE_CYCLES
+#   wave_wait_frac    = SQ_WAIT_INST_ANY / SQ_WAVE_CYCLES (waiting for an instruction to issue)
+#   mem_wait_frac     = SQ_WAIT_ANY / SQ_WAVE_CYCLES (waiting on any s_waitcnt: memory, LDS)
 # bench.py reports them in `roofline` for the same kernel.
 if len(sys.argv) > 3 and sys.argv[2] == "--traffic":
     import json
@@ -46,6 +51,8 @@ if len(sys.argv) > 3 and sys.argv[2] == "--traffic":
         d["lanes_active_frac"] = round(avg("SQ_THREAD_CYCLES_VALU") / (64 * avg("SQ_INSTS_VALU")), 4)
     if agg.get("SQ_WAIT_INST_ANY") and agg.get("SQ_WAVE_CYCLES"):
         d["wave_wait_frac"] = round(avg("SQ_WAIT_INST_ANY") / avg("SQ_WAVE_CYCLES"), 4)
+    if agg.get("SQ_WAIT_ANY") and agg.get("SQ_WAVE_CYCLES"):
+        d["mem_wait_frac"] = round(avg("SQ_WAIT_ANY") / avg("SQ_WAVE_CYCLES"), 4)
     d["pmc_source"] = root
     names = set()
     for f in glob.glob(f"{root}/pmc*/pmc_counter_collection.csv"):

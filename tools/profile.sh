@@ -6,7 +6,7 @@ set -u
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 OUT="$ROOT/gpurun_out"; mkdir -p "$OUT"
 TAG="$1"; shift
-ARGS="${*:---steps 2 --warmup 1 --no-cpu-baseline}"
+ARGS="${*:---steps 2 --warmup 2 --no-cpu-baseline --no-modes --configs none}"
 PROG="$ROOT/${PROG:-bench.py}"
 export TMPDIR=/tmp
 cd /tmp
