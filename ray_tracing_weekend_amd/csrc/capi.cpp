@@ -1010,7 +1010,7 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
         // level `bvh_depth` has that many inner nodes above it (host/bvh.cpp)
         const uint32_t bin_stack = std::max(p.sc.bvh_depth, min_stack);
         // kWorldBvhLds layout: stacks + stealing area (traversal_lds) | f32 nodes (bvh32) | leaf spheres |
-        // ids (padded to 8) | lights | (f32) light pairs | (f64) the lights' f32 pairs + L
+        // ids (padded to 8) | lights | (f32) light pairs | (f64) the lights rounded to f32
         const size_t tree_lds = rtw::traversal_lds<R>(bin_stack) + (size_t)p.sc.n_nodes * sizeof(rtw::BvhNode<float>) +
                                 (size_t)p.sc.n_sph * sizeof(rtw::R4<float>) +
                                 (size_t)((p.sc.n_sph + 7u) & ~7u) * sizeof(uint32_t) +
@@ -1019,7 +1019,7 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
                                 // f32: the light pairs of the packed light test; f64: the
                                 // lights rounded to f32 for the pre-pass (16 B each)
                                 (sizeof(R) == 4 ? (size_t)((p.sc.n_lights + 1u) & ~1u) * sizeof(rtw::R4<R>)
-                                                : (size_t)((p.sc.n_lights + 1u) / 2u) * 3 * sizeof(rtw::R4<float>));
+                                                : (size_t)p.sc.n_lights * sizeof(rtw::R4<float>));
         if (c->bvh_kind == 2 && p.sc.bvh4_stack + 1 <= rtw::kBvhStack) {
             world = rtw::kWorldBvh4;       // 4-wide, when its stack bound fits
             p.stack = std::max(p.sc.bvh4_stack + 1, min_stack);

@@ -489,10 +489,17 @@ __device__ __forceinline__ float lights_pdf_sum(const R4<float>* __restrict__ li
 // staged in LDS; each packed lane does exactly light_hit_f32's operations, so
 // the mask -- and the sum -- are bit-identical to lights_pdf_sum.
 typedef float f2v __attribute__((ext_vector_type(2)));
+// `sampled` (>= 0): the light the direction was drawn toward (Sphere::random,
+// sphere.rs:113-127) counts whatever the f32 test says: the direction lies in
+// its cone, so the reference's f64 test hits it (but at an ulp of the cone's
+// edge), while the f32 discriminant can lose the grazing edge directions --
+// and a lost light there turns the bounce's pdf to 0 and its weight to 0 / 0
+// when the light is below the surface (r04: the f32 mode's surplus NaN
+// samples on spheres that overlap no light, tools/nan_origins.py).
 template <bool kRobust>
 __device__ __forceinline__ float lights_pdf_sum_pk(const R4<float>* __restrict__ li,
                                                    const R4<float>* __restrict__ lp, uint32_t n,
-                                                   V3<float> o, V3<float> d) {
+                                                   V3<float> o, V3<float> d, int32_t sampled = -1) {
     const float a = len2_f32(d);
     const float ia = __builtin_amdgcn_rcpf(a);
     const f2v ox = {o.x, o.x}, oy = {o.y, o.y}, oz = {o.z, o.z};
@@ -526,58 +533,12 @@ __device__ __forceinline__ float lights_pdf_sum_pk(const R4<float>* __restrict__
             }
             mask |= ((h0 ? 1u : 0u) | (h1 ? 2u : 0u)) << k;
         }
+        if ((uint32_t)(sampled - (int32_t)base) < 32u) mask |= 1u << (sampled - (int32_t)base);
         while (mask) {
             const uint32_t k = (uint32_t)__builtin_ctz(mask);
             mask &= mask - 1u;
             const R4<float> L = li[base + k];
             acc += light_pdf_f32(L, o);
-        }
-    }
-    return acc;
-}
-
-// lights_pdf_sum (f64) with the pre-pass on packed FP32, two lights per
-// instruction (the light_may_hit arithmetic per component).  lp = the lights as
-// pairs, three R4 per pair {x0, x1, y0, y1}, {z0, z1, |r0|, |r1|}, {L0, L1, -, -}
-// with L = |cx| + |cy| + |cz| + |r| (an odd list ends with a NaN light: never
-// a candidate), staged in LDS.  The slack e = 2^-18 (|o|_1 + L) differs from
-// the scalar pre-pass's only in the order of its additions (an ulp of e):
-// the same bound, far above the f32 error.
-__device__ __forceinline__ double lights_pdf_sum_pk64(const R4<double>* __restrict__ li,
-                                                      const R4<float>* __restrict__ lp, uint32_t n,
-                                                      V3<double> o, V3<double> d) {
-    const LightPre pre(o, d);
-    const f2v ox = {pre.ox, pre.ox}, oy = {pre.oy, pre.oy}, oz = {pre.oz, pre.oz};
-    const f2v dx = {pre.dx, pre.dx}, dy = {pre.dy, pre.dy}, dz = {pre.dz, pre.dz};
-    const f2v ia2 = {pre.ia, pre.ia}, on2 = {pre.on, pre.on}, dn2 = {2.0f * pre.dn, 2.0f * pre.dn};
-    const f2v k18 = {0x1p-18f, 0x1p-18f};
-    double acc = 0.0;
-    for (uint32_t base = 0; base < n; base += 32) {
-        const uint32_t m = min(32u, n - base);
-        uint32_t mask = 0;
-#pragma unroll 2
-        for (uint32_t k = 0; k < m; k += 2) {
-            const R4<float> A = lp[(base + k) / 2 * 3], B = lp[(base + k) / 2 * 3 + 1], C = lp[(base + k) / 2 * 3 + 2];
-            const f2v fx = ox - f2v{A.x, A.y}, fy = oy - f2v{A.z, A.w}, fz = oz - f2v{B.x, B.y};
-            const f2v r = {B.z, B.w};
-            const f2v hb = __builtin_elementwise_fma(dz, fz, __builtin_elementwise_fma(dy, fy, dx * fx));
-            const f2v tc = -hb * ia2;
-            const f2v lx = __builtin_elementwise_fma(tc, dx, fx), ly = __builtin_elementwise_fma(tc, dy, fy),
-                      lz = __builtin_elementwise_fma(tc, dz, fz);
-            const f2v l2 = __builtin_elementwise_fma(lx, lx, __builtin_elementwise_fma(ly, ly, lz * lz));
-            const f2v f2 = __builtin_elementwise_fma(fx, fx, __builtin_elementwise_fma(fy, fy, fz * fz));
-            const f2v e = k18 * (on2 + f2v{C.x, C.y});
-            const f2v re = r + e, rr = re * re, ed = e * dn2;
-            const bool h0 = (l2.x <= rr.x) & ((hb.x <= ed.x) | (f2.x <= rr.x));
-            const bool h1 = (l2.y <= rr.y) & ((hb.y <= ed.y) | (f2.y <= rr.y));
-            mask |= ((h0 ? 1u : 0u) | (h1 ? 2u : 0u)) << k;
-        }
-        mask &= m == 32 ? 0xffffffffu : ((1u << m) - 1u);
-        while (mask) {
-            const uint32_t k = (uint32_t)__builtin_ctz(mask);
-            mask &= mask - 1u;
-            const R4<double> L = li[base + k];
-            acc = acc + sphere_pdf_value(mk(L.x, L.y, L.z), L.w, o, d);
         }
     }
     return acc;
@@ -2004,28 +1965,12 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                 l_lp[2 * q + 1] = R4<R>{A.z, B.z, A.w * A.w, odd ? B.w * B.w : (R)-INFINITY};
             }
         } else {
-            // the lights rounded to f32 as pairs (the packed pre-pass of lights_pdf_sum_pk64)
+            // the lights rounded to f32 with |radius| (the f32 pre-pass of lights_pdf_sum;
+            // a packed-FP32 pre-pass over light pairs measured 1.4 ms slower: r04)
             l_li32 = reinterpret_cast<R4<float>*>(l_li + p.sc.n_lights);
-            const uint32_t n = p.sc.n_lights;
-            for (uint32_t q = threadIdx.x; 2 * q < n; q += kBlock) {
-                auto f32 = [&](uint32_t k, float& x, float& y, float& z, float& r) {
-                    if (k < n) {
-                        const R4<R> L = p.sc.lights[k];
-                        x = (float)L.x;
-                        y = (float)L.y;
-                        z = (float)L.z;
-                        r = fabsf((float)L.w);
-                    } else {
-                        x = y = z = r = __builtin_nanf("");
-                    }
-                };
-                float ax, ay, az, ar, bx, by, bz, br;
-                f32(2 * q, ax, ay, az, ar);
-                f32(2 * q + 1, bx, by, bz, br);
-                l_li32[3 * q] = R4<float>{ax, bx, ay, by};
-                l_li32[3 * q + 1] = R4<float>{az, bz, ar, br};
-                l_li32[3 * q + 2] = R4<float>{fabsf(ax) + fabsf(ay) + fabsf(az) + ar,
-                                              fabsf(bx) + fabsf(by) + fabsf(bz) + br, 0.0f, 0.0f};
+            for (uint32_t k = threadIdx.x; k < p.sc.n_lights; k += kBlock) {
+                const R4<R> L = p.sc.lights[k];
+                l_li32[k] = R4<float>{(float)L.x, (float)L.y, (float)L.z, fabsf((float)L.w)};
             }
         }
         __syncthreads();
@@ -2588,11 +2533,15 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                             }
                         }
                     }
+                    int32_t lsel = -1;   // the sampled light (f32: always counted in the pdf)
                     if (!sampled) {
                         // a sphere light (one gen_index draw, then Sphere::random)
                         // or the cosine lobe, in one pass (mixture_direction)
                         R4<R> L = R4<R>{0, 0, 0, 0};
-                        if (to_light) L = li[g.index(kargs()->sc.n_lights)];
+                        if (to_light) {
+                            lsel = (int32_t)g.index(kargs()->sc.n_lights);
+                            L = li[lsel];
+                        }
                         dir = mixture_direction(to_light, nrm, mk(L.x, L.y, L.z), L.w, pnt, g);
                     }
                     RTW_PROBE_LAMBERT_DIR();
@@ -2625,9 +2574,9 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                                   : lights_pdf_bvh<kRobust>(p.sc, pnt, dir,
                                                             reinterpret_cast<int32_t*>(smem) + wave * p.stack * 64 + lane);
                     else if constexpr (kWorld == kWorldBvhLds && sizeof(R) == 4)
-                        acc = lights_pdf_sum_pk<kRobust>(li, l_lp, kargs()->sc.n_lights, pnt, dir);
+                        acc = lights_pdf_sum_pk<kRobust>(li, l_lp, kargs()->sc.n_lights, pnt, dir, lsel);
                     else if constexpr (kWorld == kWorldBvhLds && sizeof(R) == 8)
-                        acc = lights_pdf_sum_pk64(li, l_li32, kargs()->sc.n_lights, pnt, dir);
+                        acc = lights_pdf_sum<kRobust>(li, kargs()->sc.n_lights, pnt, dir, l_li32);
                     else
                         acc = lights_pdf_sum<kRobust>(li, kargs()->sc.n_lights, pnt, dir);
                     RTW_PROBE_LIGHT_PDF();

@@ -37,19 +37,23 @@ def main():
     ap.add_argument("--size", default="1200x800", help="WxH (C4: 3840x2160)")
     ap.add_argument("--spp", type=int, default=500)
     ap.add_argument("--ranks", default="", help="only these ranks of each N (e.g. 0 for one C4 share)")
+    ap.add_argument("--precision", default="f64", choices=["f32", "f64"],
+                    help="f64: the headline parity mode (default); f32: the hit64 speed mode")
     a = ap.parse_args()
     W, H = (int(x) for x in a.size.split("x"))
     SPP = a.spp
     scene, b = rtw.scenes.simple_soa()
     cam = b.with_image_width(W).with_image_height(H).with_samples_per_pixel(SPP).with_max_depth(50).build()
-    r = rtw.Renderer(precision=rtw.RTW_F32)
+    prec = rtw.RTW_F64 if a.precision == "f64" else rtw.RTW_F32
+    tdt = torch.float64 if prec == rtw.RTW_F64 else torch.float32
+    r = rtw.Renderer(precision=prec)
     for kv in filter(None, a.tuning.split(",")):
         k, v = kv.split("=")
         r.set_tuning(k, int(v))
     r.set_scene(scene)
-    buf = torch.empty((rtw.tiles_for_rank(W, H, 0, 1) * 64 * 3,), dtype=torch.float32, device="cuda:0")
+    buf = torch.empty((rtw.tiles_for_rank(W, H, 0, 1) * 64 * 3,), dtype=tdt, device="cuda:0")
     if W * H * SPP <= 2_000_000_000:
-        r.render_device(cam, 1, buf.data_ptr(), buf.numel() * 4)     # warm-up
+        r.render_device(cam, 1, buf.data_ptr(), buf.numel() * buf.element_size())     # warm-up
     torch.cuda.synchronize()
     base = base_cold = base_frame = None
     for n in (int(x) for x in a.ns.split(",")):
@@ -59,7 +63,7 @@ def main():
             r.set_scene(scene)   # drops the cached task order: the next render counts the tile costs
             torch.cuda.synchronize()
             t0 = time.perf_counter()
-            r.render_device(cam, 7, buf.data_ptr(), buf.numel() * 4, rank=rank, nranks=n)   # cold render
+            r.render_device(cam, 7, buf.data_ptr(), buf.numel() * buf.element_size(), rank=rank, nranks=n)   # cold render
             torch.cuda.synchronize()
             cold.append((time.perf_counter() - t0) * 1e3)
             cold_rend.append(r.get_timings(1)[0][0])   # the cold render's own kernel
@@ -67,7 +71,7 @@ def main():
             for _ in range(a.reps):
                 torch.cuda.synchronize()
                 t0 = time.perf_counter()
-                r.render_device(cam, 7, buf.data_ptr(), buf.numel() * 4, rank=rank, nranks=n)
+                r.render_device(cam, 7, buf.data_ptr(), buf.numel() * buf.element_size(), rank=rank, nranks=n)
                 torch.cuda.synchronize()
                 best = min(best, time.perf_counter() - t0)
             tm = r.get_timings(a.reps)
@@ -78,15 +82,15 @@ def main():
         base = base or slowest
         st = r.get_stats()
         # the gather + device assemble of the N packed buffers (rank 0)
-        nbytes = rtw.tiles_for_rank(W, H, 0, n) * 64 * 3 * 4
+        nbytes = rtw.tiles_for_rank(W, H, 0, n) * 64 * 3 * buf.element_size()
         gather_ms = 0.0 if n == 1 else (25e-6 + nbytes / 50e9) * 1e3
-        ranks_buf = torch.zeros((n, rtw.tiles_for_rank(W, H, 0, n) * 64 * 3), dtype=torch.float32, device="cuda:0")
-        img = torch.empty((H, W, 3), dtype=torch.float32, device="cuda:0")
-        r.assemble_tiles(ranks_buf.data_ptr(), ranks_buf.stride(0) * 4, n, W, H, img.data_ptr())
+        ranks_buf = torch.zeros((n, rtw.tiles_for_rank(W, H, 0, n) * 64 * 3), dtype=tdt, device="cuda:0")
+        img = torch.empty((H, W, 3), dtype=tdt, device="cuda:0")
+        r.assemble_tiles(ranks_buf.data_ptr(), ranks_buf.stride(0) * ranks_buf.element_size(), n, W, H, img.data_ptr())
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(5):
-            r.assemble_tiles(ranks_buf.data_ptr(), ranks_buf.stride(0) * 4, n, W, H, img.data_ptr())
+            r.assemble_tiles(ranks_buf.data_ptr(), ranks_buf.stride(0) * ranks_buf.element_size(), n, W, H, img.data_ptr())
         torch.cuda.synchronize()
         assemble_ms = (time.perf_counter() - t0) / 5 * 1e3
         frame = slowest + gather_ms + assemble_ms
