@@ -71,7 +71,7 @@ struct rtw_ctx {
                                       // run one after another, so the pilot lasts as long as its
                                       // longest path
     static constexpr uint32_t kGridPieceAuto = 0xFFFFFFFFu;
-    uint32_t grid_piece = kGridPieceAuto;   // f32 light grid walks: cells per piece of the wave's
+    uint32_t grid_piece = kGridPieceAuto;   // light grid walks: cells per piece of the wave's
                                       // cooperative walk (0: one lane walks its own ray)
     uint32_t light_bvh_min = 64;      // light lists at least this long use the light BVH
                                       // (C2, 19 lights: the linear masked loop is faster)
@@ -1003,9 +1003,12 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
             if (p.sc.lg_on) p.light_bvh = 2;                          // light grid
             else if (light_stack <= rtw::kBvhStack) p.light_bvh = 1;  // light BVH
         }
-        // the light grid's cooperative walk (f32) parks path state in the stack area
+        // the light grid's cooperative walk parks path state in the stack area
+        // (f64: 5 words per piece of the walk -- [count, 4 list indices] -- after
+        // the 20-word stash: >= 64 pieces per round)
         const uint32_t min_stack = p.light_bvh == 1 ? light_stack
-                                   : (sizeof(R) == 4 && p.light_bvh == 2 ? rtw::kCoopStash + 1u : 1u);
+                                   : (p.light_bvh == 2 ? (sizeof(R) == 8 ? rtw::kCoopStash + 6u : rtw::kCoopStash + 1u)
+                                                       : 1u);
         // binary traversal pushes at most one entry per inner level: a leaf at
         // level `bvh_depth` has that many inner nodes above it (host/bvh.cpp)
         const uint32_t bin_stack = std::max(p.sc.bvh_depth, min_stack);

@@ -1747,6 +1747,127 @@ __device__ __forceinline__ double lights_pdf_grid(const DevScene<double>& sc, V3
     });
 }
 
+// lights_pdf_grid (f64) by the whole wave: the pieces of
+// lights_pdf_grid_coop (the same cut of each pending ray's grid interval into
+// k = ceil(cells / P) pieces, dealt to the 64 lanes), each piece walking its
+// cells in f64 exactly as lights_pdf_grid does -- pre-pass, f64 sphere test,
+// the closest-approach cell rule, so every hit light is found by exactly one
+// piece -- and emitting the list indices it finds (at most kPieceIds, into
+// the LDS `slots`, [count, ids] per piece).  Each owner merges the indices of
+// its pieces and of the big list into its kMax smallest and sums their pdfs
+// in LIST order (lights_sum_in_list_order's sum: bit-identical to
+// lights_pdf_grid).  A ray whose pieces found more than that (or a piece more
+// than kPieceIds) walks again alone (lights_pdf_grid).  Every lane of the wave
+// calls this (converged), with wave-uniform P; `cap_words` (a multiple of 64)
+// of LDS at `slots`.
+__device__ __forceinline__ double lights_pdf_grid_coop64(const DevScene<double>& sc, bool pend, V3<double> o,
+                                                         V3<double> d, uint32_t P, uint32_t* __restrict__ slots,
+                                                         uint32_t cap_words, uint32_t lane) {
+    constexpr uint32_t kPieceIds = 4, kSlot = kPieceIds + 1, kMax = 8;
+    const uint32_t cap = cap_words / (kSlot * 64) * 64;   // pieces per round
+    // (the host sizes the stack area for at least one round of 64 pieces; a
+    // smaller area takes the per-lane walk -- never a loop that cannot advance)
+    if (cap == 0) return pend ? lights_pdf_grid<false>(sc, o, d) : 0.0;
+    uint32_t ids[kMax];
+    uint32_t n = 0;
+    bool dropped = false;
+    auto add = [&](uint32_t id) {   // the kMax smallest list indices (lights_sum_in_list_order)
+        if (n == kMax) {
+            dropped = true;
+            if (id > ids[kMax - 1]) return;
+            --n;
+        }
+        uint32_t q = n;
+        while (q > 0 && ids[q - 1] > id) {
+            ids[q] = ids[q - 1];
+            --q;
+        }
+        ids[q] = id;
+        ++n;
+    };
+    double tn = 0.0, tf = 0.0;
+    uint32_t k = 0;
+    if (pend) {
+        const LightPre pre(o, d);
+        for (uint32_t q = 0; q < sc.lg_big; ++q) {
+            const R4<double> L = sc.lg_sph[q];
+            double t;
+            if (pre.may_hit(L) && sphere_t(mk(L.x, L.y, L.z), L.w * L.w, o, d, 0.0, t)) add(sc.lg_id[q]);
+        }
+        uint32_t cells = 0;
+        if (light_grid_span(sc, o, d, grid_inv(d.x), grid_inv(d.y), grid_inv(d.z), tn, tf, cells))
+            k = (cells + P - 1u) / P;
+    }
+    uint32_t incl = k;
+#pragma unroll
+    for (uint32_t off = 1; off < 64; off <<= 1) {
+        const uint32_t v = (uint32_t)__shfl_up((int)incl, off);
+        if (lane >= off) incl += v;
+    }
+    const uint32_t first = incl - k, total = (uint32_t)__shfl((int)incl, 63);
+    for (uint32_t b = 0; b < total; b += cap) {
+        const uint32_t e = min(b + cap, total);
+        for (uint32_t r = b; r < e; r += 64) {
+            const uint32_t g = r + lane;
+            uint32_t own = 0;
+#pragma unroll
+            for (uint32_t step = 32; step; step >>= 1) {
+                const uint32_t f = (uint32_t)__shfl((int)first, (int)(own + step));
+                own = f <= g ? own + step : own;
+            }
+            const V3<double> ro = mk(bperm_d(o.x, own), bperm_d(o.y, own), bperm_d(o.z, own));
+            const V3<double> rd = mk(bperm_d(d.x, own), bperm_d(d.y, own), bperm_d(d.z, own));
+            const double rtn = bperm_d(tn, own), rtf = bperm_d(tf, own);
+            const uint32_t rk = (uint32_t)bperm_i((int32_t)k, own), rfirst = (uint32_t)bperm_i((int32_t)first, own);
+            if (g < e) {
+                const uint32_t j = g - rfirst;
+                const double step = (rtf - rtn) / (double)rk;
+                auto t_at = [&](uint32_t q) { return q == 0 ? rtn : (double)q * step + rtn; };
+                const LightPre rpre(ro, rd);
+                const double ria = 1.0 / (rd.x * rd.x + rd.y * rd.y + rd.z * rd.z);
+                uint32_t* slot = slots + (g - b) * kSlot;
+                uint32_t cnt = 0;
+                light_grid_walk_piece(sc, ro, rd, grid_inv(rd.x), grid_inv(rd.y), grid_inv(rd.z), t_at(j),
+                                      t_at(j + 1), j == 0, j + 1 == rk, [&](uint32_t q, double te, double tx) {
+                    const R4<double> L = sc.lg_sph[q];
+                    double t;
+                    if (rpre.may_hit(L) && sphere_t(mk(L.x, L.y, L.z), L.w * L.w, ro, rd, 0.0, t)) {
+                        const double tc = -((ro.x - L.x) * rd.x + (ro.y - L.y) * rd.y + (ro.z - L.z) * rd.z) * ria;
+                        if (tc >= te && tc < tx) {
+                            if (cnt < kPieceIds) slot[1 + cnt] = sc.lg_id[q];
+                            ++cnt;
+                        }
+                    }
+                });
+                slot[0] = cnt;
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (k) {
+            const uint32_t g0 = max(first, b), g1 = min(first + k, e);
+            for (uint32_t g = g0; g < g1; ++g) {
+                const uint32_t* slot = slots + (g - b) * kSlot;
+                const uint32_t cnt = slot[0];
+                if (cnt > kPieceIds) dropped = true;
+                for (uint32_t q = 0; q < min(cnt, kPieceIds); ++q) add(slot[1 + q]);
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    if (!pend) return 0.0;
+    if (dropped) return lights_pdf_grid<false>(sc, o, d);   // many hits: the lane's own multi-pass walk
+    double acc = 0.0;
+    for (uint32_t q = 0; q < n; ++q) {
+        const R4<double> L = sc.lights[ids[q]];
+        acc = acc + sphere_pdf_value(mk(L.x, L.y, L.z), L.w, o, d);
+    }
+    return acc;
+}
+
 // Light list with quads (DevScene::lref set): HittableList::pdf_value over
 // the mixed list in list order (hittable_list.rs:408-412), reference
 // arithmetic per entry; `li` = the sphere lights (LDS-staged or global).
@@ -1896,8 +2017,16 @@ template <typename R, int kWorld, int kOpt>
 #ifndef RTW_WAVES_F64
 #define RTW_WAVES_F64 4
 #endif
+// f64 kernels with the light grid / BVH (C3, C5): 3 waves per SIMD -- the
+// cooperative grid walk on top of the f64 path state needs ~170 VGPRs (at 128
+// the compiler spilled the loop-carried state at every trip)
+#ifndef RTW_WAVES_F64_LBVH
+#define RTW_WAVES_F64_LBVH 3
+#endif
 __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ? RTW_WAVES_H64 : RTW_WAVES)
-                                                         : ((kOpt & (kOptPrims | kOptTex)) ? 1 : RTW_WAVES_F64))
+                                                         : ((kOpt & (kOptPrims | kOptTex)) ? 1
+                                                            : ((kOpt & kOptLightBvh) ? RTW_WAVES_F64_LBVH
+                                                                                     : RTW_WAVES_F64)))
     render_kernel(const KParams<R> p) {
     using PR = P<R>;
     constexpr bool kRobust = (kOpt & kOptRobust) != 0;
@@ -2094,7 +2223,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
     // Lambertian bounce's light pdf is left pending (`pend`) for the wave's
     // cooperative grid walk at the end of the trip (lights_pdf_grid_coop); the
     // bounce's att * scattering pdf and half its cosine pdf wait with it
-    constexpr bool kCoopGrid = kLightBvh && sizeof(R) == 4 && !kPrims;
+    constexpr bool kCoopGrid = kLightBvh && !kPrims;
     bool pend = false;
     V3<R> pend_aw = zero;
     R pend_ch = (R)0;
@@ -2655,7 +2784,8 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                 // state and (hit64) the f64 ray wait in the wave's LDS stack area
                 // ([word][lane]; the host sizes p.stack >= kCoopStash + 1) instead of
                 // being spilled to scratch by the compiler; the pieces' slots follow.
-                constexpr uint32_t kStash = kHit64 ? 20u : 8u;
+                // (f64: the RNG state and the pending ray (o, d) itself)
+                constexpr uint32_t kStash = (kHit64 || sizeof(R) == 8) ? 20u : 8u;
                 static_assert(kStash < kCoopStash + 1, "the host's stack minimum covers the stash");
                 uint32_t* area = reinterpret_cast<uint32_t*>(smem) + wave * p.stack * 64;
                 // hit64: the pending ray is (o64, d64) rounded (o = pnt, d = dir), so o and d
@@ -2677,10 +2807,19 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                 if constexpr (kHit64) {
                     put(4, dbits(o64.x)); put(5, dbits(o64.y)); put(6, dbits(o64.z));
                     put(7, dbits(d64.x)); put(8, dbits(d64.y)); put(9, dbits(d64.z));
+                } else if constexpr (sizeof(R) == 8) {
+                    put(4, dbits(o.x)); put(5, dbits(o.y)); put(6, dbits(o.z));
+                    put(7, dbits(d.x)); put(8, dbits(d.y)); put(9, dbits(d.z));
                 }
-                float* slots = reinterpret_cast<float*>(area + kStash * 64);
-                const R acc = lights_pdf_grid_coop<kRobust>(p.sc, pend, po, pd, kargs()->grid_piece, slots,
-                                                            (p.stack - kStash) * 64, lane);
+                R acc;
+                if constexpr (sizeof(R) == 8) {
+                    acc = lights_pdf_grid_coop64(p.sc, pend, po, pd, kargs()->grid_piece, area + kStash * 64,
+                                                 (p.stack - kStash) * 64, lane);
+                } else {
+                    float* slots = reinterpret_cast<float*>(area + kStash * 64);
+                    acc = lights_pdf_grid_coop<kRobust>(p.sc, pend, po, pd, kargs()->grid_piece, slots,
+                                                        (p.stack - kStash) * 64, lane);
+                }
                 g.s0 = get(0);
                 g.s1 = get(1);
                 g.s2 = get(2);
@@ -2688,6 +2827,9 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                 if constexpr (kHit64) {
                     o64 = V3<double>{bitsd(get(4)), bitsd(get(5)), bitsd(get(6))};
                     d64 = V3<double>{bitsd(get(7)), bitsd(get(8)), bitsd(get(9))};
+                } else if constexpr (sizeof(R) == 8) {
+                    o = V3<R>{(R)bitsd(get(4)), (R)bitsd(get(5)), (R)bitsd(get(6))};
+                    d = V3<R>{(R)bitsd(get(7)), (R)bitsd(get(8)), (R)bitsd(get(9))};
                 }
                 if (pend) {
                     R lpdf = PR::div_(acc, (R)p.sc.n_list);

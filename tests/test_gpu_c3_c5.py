@@ -103,3 +103,24 @@ def test_cooperative_grid_walk_matches_lane_walk(config, n, spp):
     assert same.all() and np.array_equal(np.nan_to_num(imgs["coop_pixel_major"], nan=-7.0), np.nan_to_num(c, nan=-7.0))
     p3 = imgs["coop_p3"]
     assert np.array_equal(np.isnan(p3).any(-1), np.isnan(ln).any(-1))
+
+
+@pytest.mark.parametrize("config,n,spp", [("C3", 50, 4), ("C5", 500, 2)])
+def test_f64_cooperative_grid_walk_is_bit_identical(config, n, spp):
+    """f64 (parity mode): the wave-cooperative walk (lights_pdf_grid_coop64:
+    the pieces find the hit lights' list indices, each owner sums their pdfs in
+    list order) against one lane per ray (grid_piece = 0, lights_pdf_grid) and
+    another piece size: the same hit lights, summed in the same order, so the
+    frames are equal bit for bit (NaN masks included)."""
+    soa, b = rtw.scenes.simple_soa(SEED_SCENE, n)
+    cam = b.with_image_width(W).with_image_height(H).with_samples_per_pixel(spp).with_max_depth(DEPTH).build()
+    imgs = {}
+    for key, tuning in (("coop", {}), ("lane", {"grid_piece": 0}), ("coop_p3", {"grid_piece": 3})):
+        with rtw.Renderer(precision=rtw.RTW_F64) as r:
+            for k, v in tuning.items():
+                r.set_tuning(k, v)
+            r.set_scene(soa)
+            imgs[key] = r.render(cam, 19)
+    ref = np.nan_to_num(imgs["lane"], nan=-7.0)
+    for key in ("coop", "coop_p3"):
+        assert np.array_equal(np.nan_to_num(imgs[key], nan=-7.0), ref), (config, key)

@@ -1,7 +1,8 @@
 #!/bin/bash
 # One GPU session: parity tests, smoke, bench, then rocprofv3 kernel-trace +
-# PMC passes of the headline (f32 hit64) and the f64 parity kernels, each
-# summarised on the box against the library that ran (ISA-hash stamped).
+# PMC passes of the headline (f64 parity, round 4 on) and the f32 hit64
+# kernels, each summarised on the box against the library that ran
+# (ISA-hash stamped).
 # Stops at the first fault-type exit (abort/segfault/timeout); a plain test
 # failure (pytest rc 1) still lets the measurement steps run.
 #   tools/gpu_round.sh TAG          (PROFILE=0: no rocprofv3 steps)
@@ -28,7 +29,8 @@ rc=$?; echo "bench rc=$rc"; cut -c1-1500 "$OUT/bench_$TAG.json"; tail -3 "$OUT/b
 if [ $rc -ne 0 ]; then exit $rc; fi
 
 if [ "${PROFILE:-1}" = "1" ]; then
-  bash "$ROOT/tools/profile.sh" "$TAG" --steps 2 --warmup 1 --no-cpu-baseline --no-modes || exit $?
-  bash "$ROOT/tools/profile.sh" "${TAG}_f64" --precision f64 --steps 2 --warmup 1 --no-cpu-baseline --no-modes || exit $?
+  bash "$ROOT/tools/profile.sh" "$TAG" --steps 2 --warmup 2 --no-cpu-baseline --no-modes --configs none || exit $?
+  bash "$ROOT/tools/profile.sh" "${TAG}_f32" --precision f32 --steps 2 --warmup 2 --no-cpu-baseline --no-modes \
+    --configs none || exit $?
 fi
 exit 0

@@ -23,7 +23,7 @@ def cp(src, dst):
 
 cp(f"{G}/pytest_gpu_{tag}.log", f"{tag}_pytest_gpu.log")
 cp(f"{G}/bench_{tag}.json", f"{tag}_bench.json")
-for sub in ("", "_f64"):
+for sub in ("", "_f32", "_f64"):
     t = f"{tag}{sub}"
     stats = glob.glob(f"{G}/prof_{t}/*kernel_stats.csv")
     if stats:
