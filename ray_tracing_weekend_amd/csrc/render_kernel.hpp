@@ -1752,118 +1752,147 @@ __device__ __forceinline__ double lights_pdf_grid(const DevScene<double>& sc, V3
 // k = ceil(cells / P) pieces, dealt to the 64 lanes), each piece walking its
 // cells in f64 exactly as lights_pdf_grid does -- pre-pass, f64 sphere test,
 // the closest-approach cell rule, so every hit light is found by exactly one
-// piece -- and emitting the list indices it finds (at most kPieceIds, into
-// the LDS `slots`, [count, ids] per piece).  Each owner merges the indices of
-// its pieces and of the big list into its kMax smallest and sums their pdfs
-// in LIST order (lights_sum_in_list_order's sum: bit-identical to
-// lights_pdf_grid).  A ray whose pieces found more than that (or a piece more
-// than kPieceIds) walks again alone (lights_pdf_grid).  Every lane of the wave
-// calls this (converged), with wave-uniform P; `cap_words` (a multiple of 64)
-// of LDS at `slots`.
+// piece.  The sum must run in LIST order (lights_sum_in_list_order), so it
+// goes in passes over list indices >= lo: a piece keeps the kPieceIds
+// smallest indices >= lo it finds, sorted, in its LDS slot ([count, ids]);
+// each owner merges its pieces' indices and the big list's into its kMax
+// smallest.  Every index up to `bound` is then known -- bound = the largest
+// kept index of a piece or an owner list that had to drop some, else
+// unbounded -- so the owner sums those pdfs in order and, when something was
+// dropped, the wave walks again for its rays with lo = bound + 1 (each pass
+// sums at least one index: the walk always ends).  A ray skimming C5's light
+// layer (~10 hits) takes two passes; the walk never falls back to one lane.
+// Bit-identical to lights_pdf_grid.  Every lane of the wave calls this
+// (converged), with wave-uniform P; `cap_words` (a multiple of 64) of LDS at
+// `slots`.
 __device__ __forceinline__ double lights_pdf_grid_coop64(const DevScene<double>& sc, bool pend, V3<double> o,
                                                          V3<double> d, uint32_t P, uint32_t* __restrict__ slots,
                                                          uint32_t cap_words, uint32_t lane) {
-    constexpr uint32_t kPieceIds = 4, kSlot = kPieceIds + 1, kMax = 8;
+    constexpr uint32_t kPieceIds = kCoop64PieceIds, kSlot = kPieceIds + 1, kMax = RTW_COOP64_MAX;
     const uint32_t cap = cap_words / (kSlot * 64) * 64;   // pieces per round
     // (the host sizes the stack area for at least one round of 64 pieces; a
     // smaller area takes the per-lane walk -- never a loop that cannot advance)
     if (cap == 0) return pend ? lights_pdf_grid<false>(sc, o, d) : 0.0;
-    uint32_t ids[kMax];
-    uint32_t n = 0;
-    bool dropped = false;
-    auto add = [&](uint32_t id) {   // the kMax smallest list indices (lights_sum_in_list_order)
-        if (n == kMax) {
-            dropped = true;
-            if (id > ids[kMax - 1]) return;
-            --n;
-        }
-        uint32_t q = n;
-        while (q > 0 && ids[q - 1] > id) {
-            ids[q] = ids[q - 1];
-            --q;
-        }
-        ids[q] = id;
-        ++n;
-    };
     double tn = 0.0, tf = 0.0;
     uint32_t k = 0;
     if (pend) {
-        const LightPre pre(o, d);
-        for (uint32_t q = 0; q < sc.lg_big; ++q) {
-            const R4<double> L = sc.lg_sph[q];
-            double t;
-            if (pre.may_hit(L) && sphere_t(mk(L.x, L.y, L.z), L.w * L.w, o, d, 0.0, t)) add(sc.lg_id[q]);
-        }
         uint32_t cells = 0;
         if (light_grid_span(sc, o, d, grid_inv(d.x), grid_inv(d.y), grid_inv(d.z), tn, tf, cells))
             k = (cells + P - 1u) / P;
     }
-    uint32_t incl = k;
-#pragma unroll
-    for (uint32_t off = 1; off < 64; off <<= 1) {
-        const uint32_t v = (uint32_t)__shfl_up((int)incl, off);
-        if (lane >= off) incl += v;
-    }
-    const uint32_t first = incl - k, total = (uint32_t)__shfl((int)incl, 63);
-    for (uint32_t b = 0; b < total; b += cap) {
-        const uint32_t e = min(b + cap, total);
-        for (uint32_t r = b; r < e; r += 64) {
-            const uint32_t g = r + lane;
-            uint32_t own = 0;
-#pragma unroll
-            for (uint32_t step = 32; step; step >>= 1) {
-                const uint32_t f = (uint32_t)__shfl((int)first, (int)(own + step));
-                own = f <= g ? own + step : own;
-            }
-            const V3<double> ro = mk(bperm_d(o.x, own), bperm_d(o.y, own), bperm_d(o.z, own));
-            const V3<double> rd = mk(bperm_d(d.x, own), bperm_d(d.y, own), bperm_d(d.z, own));
-            const double rtn = bperm_d(tn, own), rtf = bperm_d(tf, own);
-            const uint32_t rk = (uint32_t)bperm_i((int32_t)k, own), rfirst = (uint32_t)bperm_i((int32_t)first, own);
-            if (g < e) {
-                const uint32_t j = g - rfirst;
-                const double step = (rtf - rtn) / (double)rk;
-                auto t_at = [&](uint32_t q) { return q == 0 ? rtn : (double)q * step + rtn; };
-                const LightPre rpre(ro, rd);
-                const double ria = 1.0 / (rd.x * rd.x + rd.y * rd.y + rd.z * rd.z);
-                uint32_t* slot = slots + (g - b) * kSlot;
-                uint32_t cnt = 0;
-                light_grid_walk_piece(sc, ro, rd, grid_inv(rd.x), grid_inv(rd.y), grid_inv(rd.z), t_at(j),
-                                      t_at(j + 1), j == 0, j + 1 == rk, [&](uint32_t q, double te, double tx) {
-                    const R4<double> L = sc.lg_sph[q];
-                    double t;
-                    if (rpre.may_hit(L) && sphere_t(mk(L.x, L.y, L.z), L.w * L.w, ro, rd, 0.0, t)) {
-                        const double tc = -((ro.x - L.x) * rd.x + (ro.y - L.y) * rd.y + (ro.z - L.z) * rd.z) * ria;
-                        if (tc >= te && tc < tx) {
-                            if (cnt < kPieceIds) slot[1 + cnt] = sc.lg_id[q];
-                            ++cnt;
-                        }
-                    }
-                });
-                slot[0] = cnt;
-            }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        if (k) {
-            const uint32_t g0 = max(first, b), g1 = min(first + k, e);
-            for (uint32_t g = g0; g < g1; ++g) {
-                const uint32_t* slot = slots + (g - b) * kSlot;
-                const uint32_t cnt = slot[0];
-                if (cnt > kPieceIds) dropped = true;
-                for (uint32_t q = 0; q < min(cnt, kPieceIds); ++q) add(slot[1 + q]);
-            }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    }
-    if (!pend) return 0.0;
-    if (dropped) return lights_pdf_grid<false>(sc, o, d);   // many hits: the lane's own multi-pass walk
     double acc = 0.0;
-    for (uint32_t q = 0; q < n; ++q) {
-        const R4<double> L = sc.lights[ids[q]];
-        acc = acc + sphere_pdf_value(mk(L.x, L.y, L.z), L.w, o, d);
+    uint32_t lo = 0;
+    bool more = pend;
+    while (__any(more)) {
+        uint32_t ids[kMax];
+        uint32_t n = 0, bound = 0xffffffffu;
+        bool dropped = false;
+        auto add = [&](uint32_t id) {   // the kMax smallest list indices (lights_sum_in_list_order)
+            if (n == kMax) {
+                dropped = true;
+                if (id > ids[kMax - 1]) return;
+                --n;
+            }
+            uint32_t q = n;
+            while (q > 0 && ids[q - 1] > id) {
+                ids[q] = ids[q - 1];
+                --q;
+            }
+            ids[q] = id;
+            ++n;
+        };
+        if (more) {
+            const LightPre pre(o, d);
+            for (uint32_t q = 0; q < sc.lg_big; ++q) {
+                const R4<double> L = sc.lg_sph[q];
+                double t;
+                const uint32_t id = sc.lg_id[q];
+                if (id >= lo && pre.may_hit(L) && sphere_t(mk(L.x, L.y, L.z), L.w * L.w, o, d, 0.0, t)) add(id);
+            }
+        }
+        const uint32_t kp = more ? k : 0u;   // this pass's pieces
+        uint32_t incl = kp;
+#pragma unroll
+        for (uint32_t off = 1; off < 64; off <<= 1) {
+            const uint32_t v = (uint32_t)__shfl_up((int)incl, off);
+            if (lane >= off) incl += v;
+        }
+        const uint32_t first = incl - kp, total = (uint32_t)__shfl((int)incl, 63);
+        for (uint32_t b = 0; b < total; b += cap) {
+            const uint32_t e = min(b + cap, total);
+            for (uint32_t r = b; r < e; r += 64) {
+                const uint32_t g = r + lane;
+                uint32_t own = 0;
+#pragma unroll
+                for (uint32_t step = 32; step; step >>= 1) {
+                    const uint32_t f = (uint32_t)__shfl((int)first, (int)(own + step));
+                    own = f <= g ? own + step : own;
+                }
+                const V3<double> ro = mk(bperm_d(o.x, own), bperm_d(o.y, own), bperm_d(o.z, own));
+                const V3<double> rd = mk(bperm_d(d.x, own), bperm_d(d.y, own), bperm_d(d.z, own));
+                const double rtn = bperm_d(tn, own), rtf = bperm_d(tf, own);
+                const uint32_t rk = (uint32_t)bperm_i((int32_t)kp, own), rfirst = (uint32_t)bperm_i((int32_t)first, own);
+                const uint32_t rlo = (uint32_t)bperm_i((int32_t)lo, own);
+                if (g < e) {
+                    const uint32_t j = g - rfirst;
+                    const double step = (rtf - rtn) / (double)rk;
+                    auto t_at = [&](uint32_t q) { return q == 0 ? rtn : (double)q * step + rtn; };
+                    const LightPre rpre(ro, rd);
+                    const double ria = 1.0 / (rd.x * rd.x + rd.y * rd.y + rd.z * rd.z);
+                    uint32_t* ent = slots + (g - b) * kSlot + 1;
+                    uint32_t cnt = 0;
+                    light_grid_walk_piece(sc, ro, rd, grid_inv(rd.x), grid_inv(rd.y), grid_inv(rd.z), t_at(j),
+                                          t_at(j + 1), j == 0, j + 1 == rk, [&](uint32_t q, double te, double tx) {
+                        const R4<double> L = sc.lg_sph[q];
+                        double t;
+                        if (rpre.may_hit(L) && sphere_t(mk(L.x, L.y, L.z), L.w * L.w, ro, rd, 0.0, t)) {
+                            const double tc = -((ro.x - L.x) * rd.x + (ro.y - L.y) * rd.y + (ro.z - L.z) * rd.z) * ria;
+                            const uint32_t id = sc.lg_id[q];
+                            if (tc >= te && tc < tx && id >= rlo) {
+                                // the piece's kPieceIds smallest, sorted (rare: a hit)
+                                uint32_t m = min(cnt, kPieceIds);
+                                ++cnt;
+                                if (m == kPieceIds) {
+                                    if (id > ent[kPieceIds - 1]) return;
+                                    --m;                               // the largest gives way
+                                }
+                                while (m > 0 && ent[m - 1] > id) {
+                                    ent[m] = ent[m - 1];
+                                    --m;
+                                }
+                                ent[m] = id;
+                            }
+                        }
+                    });
+                    ent[-1] = cnt;
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (kp) {
+                const uint32_t g0 = max(first, b), g1 = min(first + kp, e);
+                for (uint32_t g = g0; g < g1; ++g) {
+                    const uint32_t* ent = slots + (g - b) * kSlot + 1;
+                    const uint32_t cnt = ent[-1];
+                    for (uint32_t q = 0; q < min(cnt, kPieceIds); ++q) add(ent[q]);
+                    if (cnt > kPieceIds) bound = min(bound, ent[kPieceIds - 1]);
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+        if (more) {
+            if (dropped) bound = min(bound, ids[kMax - 1]);
+            for (uint32_t q = 0; q < n; ++q) {
+                if (ids[q] > bound) break;
+                const R4<double> L = sc.lights[ids[q]];
+                acc = acc + sphere_pdf_value(mk(L.x, L.y, L.z), L.w, o, d);
+            }
+            more = bound != 0xffffffffu;
+            lo = bound + 1u;
+        }
     }
     return acc;
 }

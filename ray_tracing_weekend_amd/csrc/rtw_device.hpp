@@ -76,6 +76,18 @@ struct P<double> {
     __device__ static __forceinline__ double u_std(uint64_t v) {
         return (1.0 / 9007199254740992.0) * (double)(v >> 11);
     }
+    // 2 * u_std(v) - 1 (UnitSphere's / UnitDisk's coordinate, utils.rs:99-144)
+    // without the integer conversion: with b = bit 63 of v and D = 1 + m 2^-52
+    // built from bits 11..62 (m), (v >> 11) 2^-52 - 1 = D - (2 - b), and both
+    // roundings are exact (Sterbenz), so the two forms agree bit for bit
+    // (tests/test_rng_forms.py checks the identity over 2^20 words and the edges)
+    __device__ static __forceinline__ double u_pm1(uint64_t v) {
+        const uint32_t hi = (uint32_t)(v >> 32), lo = (uint32_t)v;
+        const uint32_t dlo = __builtin_amdgcn_alignbit(hi, lo, 11);
+        const uint32_t dhi = 0x3FF00000u | ((hi >> 11) & 0xFFFFFu);
+        const uint32_t chi = 0x40000000u - ((hi >> 31) << 20);
+        return __hiloint2double((int)dhi, (int)dlo) - __hiloint2double((int)chi, 0);
+    }
     __device__ static __forceinline__ double unit12(uint64_t v) {
         return __longlong_as_double((long long)((v >> 12) | 0x3FF0000000000000ULL));
     }
@@ -275,9 +287,9 @@ __device__ __forceinline__ V3<R> unit_sphere(Rng& g) {
         return mk(rxy * c, rxy * s, r * z);
     } else {
         for (;;) {
-            R in0 = (R)2 * P<R>::u_std(g.next()) - (R)1;
-            R in1 = (R)2 * P<R>::u_std(g.next()) - (R)1;
-            R in2 = (R)2 * P<R>::u_std(g.next()) - (R)1;
+            R in0 = P<R>::u_pm1(g.next());
+            R in1 = P<R>::u_pm1(g.next());
+            R in2 = P<R>::u_pm1(g.next());
             V3<R> out = mk(in0, in1, in2);
             if (dot(out, out) < (R)1) return out;
         }

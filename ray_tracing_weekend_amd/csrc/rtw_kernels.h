@@ -169,6 +169,16 @@ constexpr uint32_t kBvhStack = 32;    // per-lane traversal stack entries (LDS)
 // path state per lane in the wave's stack area (render_kernel.hpp), so the
 // host gives them at least kCoopStash + 1 entries
 constexpr uint32_t kCoopStash = 20;
+// the f64 cooperative grid walk (lights_pdf_grid_coop64): list indices one
+// piece keeps per pass (its LDS slot: count + ids), and that a ray's owner
+// sums per pass
+#ifndef RTW_COOP64_PIECE_IDS
+#define RTW_COOP64_PIECE_IDS 6
+#endif
+#ifndef RTW_COOP64_MAX
+#define RTW_COOP64_MAX 8
+#endif
+constexpr uint32_t kCoop64PieceIds = RTW_COOP64_PIECE_IDS;
 // Subtree stealing in the while-while traversal (render_kernel.hpp
 // bvh_traverse_steal): per wave the result slots of its 64 rays (f32: a u64
 // key; f64: u64 t bits + u32 id) and 64 rendezvous bytes, in LDS right after
