@@ -2463,6 +2463,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
             }
             RTW_PROBE_CLK(2);
             RTW_PROBE_SEGMENT();
+            RTW_PROBE_HIT(best);
 
             bool done = false;
             V3<R> col = zero;

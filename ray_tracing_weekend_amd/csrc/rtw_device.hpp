@@ -192,7 +192,17 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
     return z ^ (z >> 31);
 }
-__device__ __forceinline__ uint64_t rotl(uint64_t x, int k) { return (x << k) | (x >> (64 - k)); }
+// (x << k) | (x >> (64 - k)) as two v_alignbit_b32 (the compiler's shift / or
+// form takes three instructions); k >= 32 rotates the swapped halves by k - 32
+template <int k>
+__device__ __forceinline__ uint64_t rotl(uint64_t x) {
+    static_assert(k > 0 && k < 64 && k != 32, "rotation count");
+    const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+    if constexpr (k < 32)
+        return ((uint64_t)__builtin_amdgcn_alignbit(hi, lo, 32 - k) << 32) | __builtin_amdgcn_alignbit(lo, hi, 32 - k);
+    else
+        return ((uint64_t)__builtin_amdgcn_alignbit(lo, hi, 64 - k) << 32) | __builtin_amdgcn_alignbit(hi, lo, 64 - k);
+}
 
 struct Rng {
     uint64_t s0, s1, s2, s3;
@@ -205,14 +215,14 @@ struct Rng {
         k += 0x9E3779B97F4A7C15ULL; s3 = mix64(k);
     }
     __device__ __forceinline__ uint64_t next() {
-        uint64_t result = rotl(s0 + s3, 23) + s0;
+        uint64_t result = rotl<23>(s0 + s3) + s0;
         uint64_t t = s1 << 17;
         s2 ^= s0;
         s3 ^= s1;
         s1 ^= s2;
         s0 ^= s3;
         s2 ^= t;
-        s3 = rotl(s3, 45);
+        s3 = rotl<45>(s3);
         return result;
     }
     // gen_range(0..n) for u32 (rand 0.8.6 sample_single_inclusive), next_u32 = next >> 32

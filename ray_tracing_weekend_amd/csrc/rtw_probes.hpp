@@ -339,6 +339,22 @@ static __device__ unsigned long long g_nan[kNanSlots];
     do { \
         if (!(was) && (now) && (uint32_t)(obj) + 1u < (uint32_t)kNanSlots) atomicAdd(&g_nan[1 + (obj)], 1ull); \
     } while (0)
+// and the segments' closest hits per object (slot 1 + id; slot 0: misses)
+static __device__ unsigned long long g_hit[kNanSlots];
+#define RTW_PROBE_HIT(obj) \
+    do { \
+        if ((uint32_t)((obj) + 1) < (uint32_t)kNanSlots) atomicAdd(&g_hit[1 + (obj)], 1ull); \
+    } while (0)
+extern "C" int RTW_CAT(rtw_probe_hit_read_, RTW_NANORIGIN)(unsigned long long* out, size_t n, int reset) {
+    n = n < (size_t)kNanSlots ? n : (size_t)kNanSlots;
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_hit), n * sizeof(unsigned long long)) != hipSuccess) return -1;
+    if (reset) {
+        static unsigned long long zero[kNanSlots];
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_hit), zero, sizeof zero) != hipSuccess) return -1;
+    }
+    return (int)n;
+}
 extern "C" int RTW_CAT(rtw_probe_nan_read_, RTW_NANORIGIN)(unsigned long long* out, size_t n, int reset) {
     n = n < (size_t)kNanSlots ? n : (size_t)kNanSlots;
     if (hipDeviceSynchronize() != hipSuccess) return -1;
@@ -351,4 +367,5 @@ extern "C" int RTW_CAT(rtw_probe_nan_read_, RTW_NANORIGIN)(unsigned long long* o
 }
 #else
 #define RTW_PROBE_NAN_LAMBERT(was, now, obj)
+#define RTW_PROBE_HIT(obj)
 #endif

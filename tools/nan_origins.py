@@ -3,7 +3,9 @@
 (experiment tool; the RTW_NANORIGIN build, rtw_probes.hpp): per world object,
 the samples whose throughput turned NaN at a Lambertian bounce off it -- a
 point inside a light sphere (Sphere::pdf_value's sqrt of a negative,
-sphere.rs:101-111).  Object ids: planes first, then spheres.
+sphere.rs:101-111) -- and the segments' closest hits per object (where the
+f32 paths' extra segments go), f64 at a second seed as the noise floor.
+Object ids: planes first, then spheres; -1: miss.
 
     python tools/nan_origins.py build
     python tools/nan_origins.py run [--spp 100] [--seed 5] [--tuning k=v,...]
@@ -51,25 +53,50 @@ def run(a):
     mtype = np.asarray(soa.mat_type)
     smat = np.asarray(soa.sphere_mat)
     out = {"spp": a.spp, "seed": a.seed, "tuning": a.tuning}
-    counts = {}
-    for name, prec in (("f32", rtw.RTW_F32), ("f64", rtw.RTW_F64)):
-        rd = getattr(rtw._lib, f"rtw_probe_nan_read_{name}")
+    counts, hits = {}, {}
+    for name, prec, seed in (("f32", rtw.RTW_F32, a.seed), ("f64", rtw.RTW_F64, a.seed),
+                             ("f64_other_seed", rtw.RTW_F64, a.seed + 1)):
+        lib = name[:3]
+        rd = getattr(rtw._lib, f"rtw_probe_nan_read_{lib}")
         rd.argtypes = [C.c_void_p, C.c_size_t, C.c_int]
+        rh = getattr(rtw._lib, f"rtw_probe_hit_read_{lib}")
+        rh.argtypes = [C.c_void_p, C.c_size_t, C.c_int]
         n = 1 + n_pl + len(sph)
         buf = (C.c_ulonglong * n)()
+        hbuf = (C.c_ulonglong * n)()
         with rtw.Renderer(precision=prec) as r:
             for kv in filter(None, a.tuning.split(",")):
                 k, v = kv.split("=")
                 r.set_tuning(k, int(v))
             r.set_scene(soa)
             rd(buf, n, 1)
-            img = r.render(cam, a.seed)
+            rh(hbuf, n, 1)
+            img = r.render(cam, seed)
             st = r.stats
-            assert rd(buf, n, 1) >= 0
+            assert rd(buf, n, 1) >= 0 and rh(hbuf, n, 1) >= 0
         c = np.array(buf[1:], dtype=np.int64)
         counts[name] = c
+        hits[name] = np.array(hbuf[:], dtype=np.int64)   # [0]: misses, [1 + id]: closest hits
         out[name] = {"nan_origin_samples": int(c.sum()), "nan_pixels": int(np.isnan(img).any(-1).sum()),
-                     "segments_per_sample": round(st.segments / st.samples, 5)}
+                     "segments_per_sample": round(st.segments / st.samples, 5),
+                     "segments_hist": int(hits[name].sum()), "misses": int(hits[name][0])}
+    # closest hits per object: where the f32 paths' extra segments land, with
+    # the f64 two-seed difference as the noise floor
+    def hit_rows(x, y):
+        z = (x - y) / np.sqrt(np.maximum(x + y, 1))
+        order = np.argsort(-np.abs(z))[:20]
+        rows = []
+        for k in order:
+            obj = int(k) - 1
+            rec = {"object": obj, "a": int(x[k]), "b": int(y[k]), "z": round(float(z[k]), 1)}
+            if obj >= n_pl:
+                s = sph[obj - n_pl]
+                rec.update(center=[round(float(v), 3) for v in s[:3]], radius=float(s[3]),
+                           material=int(mtype[smat[obj - n_pl]]))
+            rows.append(rec)
+        return rows, float(np.sqrt(np.mean(z * z)))
+    out["hits_f32_vs_f64"], out["hits_z_rms_f32_vs_f64"] = hit_rows(hits["f32"], hits["f64"])
+    out["hits_f64_vs_f64_other_seed"], out["hits_z_rms_f64_seeds"] = hit_rows(hits["f64_other_seed"], hits["f64"])
     # per-sphere comparison: the spheres with the most NaN origins in either mode
     f32, f64 = counts["f32"], counts["f64"]
     top = np.argsort(-(f32 + f64))[:25]
