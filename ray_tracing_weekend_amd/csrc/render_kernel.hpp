@@ -2258,6 +2258,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
     R pend_ch = (R)0;
     RTW_PROBE_WAVE_BEGIN();
     RTW_PROBE_CLK_INIT();
+    RTW_PROBE_HIT_INIT();
 
     auto start_sample = [&]() {
         const KArgs* k = kargs();
@@ -2289,6 +2290,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
         }
         mult = mk<R>(1, 1, 1);
         res.reset();
+        RTW_PROBE_HIT_RESET();
         depth = k->max_depth;
         self_s = -1;
         self_iso = false;

@@ -339,11 +339,19 @@ static __device__ unsigned long long g_nan[kNanSlots];
     do { \
         if (!(was) && (now) && (uint32_t)(obj) + 1u < (uint32_t)kNanSlots) atomicAdd(&g_nan[1 + (obj)], 1ull); \
     } while (0)
-// and the segments' closest hits per object (slot 1 + id; slot 0: misses)
+// and the segments' closest hits per object (slot 1 + id; slot 0: misses),
+// and in the second half those that hit the object the previous segment hit
+// (a re-hit of the surface the ray starts on: "acne")
 static __device__ unsigned long long g_hit[kNanSlots];
+#define RTW_PROBE_HIT_INIT() int32_t hit_prev_ = -2
+#define RTW_PROBE_HIT_RESET() hit_prev_ = -2
 #define RTW_PROBE_HIT(obj) \
     do { \
-        if ((uint32_t)((obj) + 1) < (uint32_t)kNanSlots) atomicAdd(&g_hit[1 + (obj)], 1ull); \
+        if ((uint32_t)((obj) + 1) < (uint32_t)kNanSlots / 2u) { \
+            atomicAdd(&g_hit[1 + (obj)], 1ull); \
+            if ((obj) >= 0 && (obj) == hit_prev_) atomicAdd(&g_hit[kNanSlots / 2 + 1 + (obj)], 1ull); \
+        } \
+        hit_prev_ = (obj); \
     } while (0)
 extern "C" int RTW_CAT(rtw_probe_hit_read_, RTW_NANORIGIN)(unsigned long long* out, size_t n, int reset) {
     n = n < (size_t)kNanSlots ? n : (size_t)kNanSlots;
@@ -368,4 +376,6 @@ extern "C" int RTW_CAT(rtw_probe_nan_read_, RTW_NANORIGIN)(unsigned long long* o
 #else
 #define RTW_PROBE_NAN_LAMBERT(was, now, obj)
 #define RTW_PROBE_HIT(obj)
+#define RTW_PROBE_HIT_INIT()
+#define RTW_PROBE_HIT_RESET()
 #endif

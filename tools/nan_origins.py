@@ -53,7 +53,7 @@ def run(a):
     mtype = np.asarray(soa.mat_type)
     smat = np.asarray(soa.sphere_mat)
     out = {"spp": a.spp, "seed": a.seed, "tuning": a.tuning}
-    counts, hits = {}, {}
+    counts, hits, rehits = {}, {}, {}
     for name, prec, seed in (("f32", rtw.RTW_F32, a.seed), ("f64", rtw.RTW_F64, a.seed),
                              ("f64_other_seed", rtw.RTW_F64, a.seed + 1)):
         lib = name[:3]
@@ -64,22 +64,28 @@ def run(a):
         n = 1 + n_pl + len(sph)
         buf = (C.c_ulonglong * n)()
         hbuf = (C.c_ulonglong * n)()
+        half = 1 << 15                                    # rtw_probes.hpp: kNanSlots / 2
+        full = (C.c_ulonglong * (half + n))()
         with rtw.Renderer(precision=prec) as r:
             for kv in filter(None, a.tuning.split(",")):
                 k, v = kv.split("=")
                 r.set_tuning(k, int(v))
             r.set_scene(soa)
             rd(buf, n, 1)
-            rh(hbuf, n, 1)
+            rh(full, half + n, 1)
             img = r.render(cam, seed)
             st = r.stats
-            assert rd(buf, n, 1) >= 0 and rh(hbuf, n, 1) >= 0
+            assert rd(buf, n, 1) >= 0 and rh(full, half + n, 1) >= 0
+        hbuf = full[:n]
+        h2buf = full[half:half + n]
         c = np.array(buf[1:], dtype=np.int64)
         counts[name] = c
         hits[name] = np.array(hbuf[:], dtype=np.int64)   # [0]: misses, [1 + id]: closest hits
+        rehits[name] = np.array(h2buf[:], dtype=np.int64)[1:]   # [id]: hits of the object hit just before
         out[name] = {"nan_origin_samples": int(c.sum()), "nan_pixels": int(np.isnan(img).any(-1).sum()),
                      "segments_per_sample": round(st.segments / st.samples, 5),
-                     "segments_hist": int(hits[name].sum()), "misses": int(hits[name][0])}
+                     "segments_hist": int(hits[name].sum()), "misses": int(hits[name][0]),
+                     "rehits": int(rehits[name].sum())}
     # closest hits per object: where the f32 paths' extra segments land, with
     # the f64 two-seed difference as the noise floor
     def hit_rows(x, y):
@@ -97,6 +103,14 @@ def run(a):
         return rows, float(np.sqrt(np.mean(z * z)))
     out["hits_f32_vs_f64"], out["hits_z_rms_f32_vs_f64"] = hit_rows(hits["f32"], hits["f64"])
     out["hits_f64_vs_f64_other_seed"], out["hits_z_rms_f64_seeds"] = hit_rows(hits["f64_other_seed"], hits["f64"])
+    # re-hits of the object the ray starts on, per object
+    def rehit_rows(x, y):
+        z = (x - y) / np.sqrt(np.maximum(x + y, 1))
+        order = np.argsort(-np.abs(z))[:15]
+        return [{"object": int(k), "a": int(x[k]), "b": int(y[k]), "z": round(float(z[k]), 1),
+                 "material": int(mtype[smat[int(k) - n_pl]]) if k >= n_pl else -1} for k in order]
+    out["rehits_f32_vs_f64"] = rehit_rows(rehits["f32"], rehits["f64"])
+    out["rehits_f64_vs_f64_other_seed"] = rehit_rows(rehits["f64_other_seed"], rehits["f64"])
     # per-sphere comparison: the spheres with the most NaN origins in either mode
     f32, f64 = counts["f32"], counts["f64"]
     top = np.argsort(-(f32 + f64))[:25]
