@@ -1401,6 +1401,9 @@ __device__ __forceinline__ V3<double> dielectric_dir64(V3<double> u, V3<double> 
 // `kRefSphere`: Metal's UnitSphere by the reference's rejection loop in f64
 // (the f64 parity kernels), else the f32 kernels' direct sampler carried into
 // f64 (dither64).
+#ifndef RTW_HIT64_REF_SPHERE
+#define RTW_HIT64_REF_SPHERE 0   // hit64 Metal: 1 = the reference's f64 rejection loop (experiment)
+#endif
 template <bool kRefSphere = false>
 __device__ __forceinline__ V3<double> specular_dir64(bool metal, V3<double> d, V3<double> n, bool front,
                                                      const R4<double>& M, Rng& g, bool& keep) {
@@ -2584,7 +2587,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                     const bool metal = mtype == kMatMetal;
                     bool keep;
                     RTW_PROBE_SCATTER64(specular_dir64(metal, d64, n64, front, kargs()->sc.mat64[m], g2, keep2).y);
-                    d64 = specular_dir64(metal, d64, n64, front, kargs()->sc.mat64[m], g, keep);
+                    d64 = specular_dir64<RTW_HIT64_REF_SPHERE != 0>(metal, d64, n64, front, kargs()->sc.mat64[m], g, keep);
                     if (!keep) {
                         col = mult * emitted + res.value();
                         done = true;
