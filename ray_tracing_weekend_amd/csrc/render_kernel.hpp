@@ -41,6 +41,9 @@ namespace dev {
 #include "rtw_probes.hpp"
 #else
 #define RTW_PROBE_NAN_LAMBERT(was, now, obj)
+#define RTW_PROBE_HIT_INIT()
+#define RTW_PROBE_HIT_RESET()
+#define RTW_PROBE_HIT(obj)
 #define RTW_PROBE_CLK_INIT()
 #define RTW_PROBE_CLK(id)
 #define RTW_PROBE_CLK_END()

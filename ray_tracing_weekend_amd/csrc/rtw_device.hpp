@@ -309,8 +309,14 @@ __device__ __forceinline__ V3<R> unit_sphere(Rng& g) {
 template <typename R>
 __device__ __forceinline__ V3<R> unit_disk(Rng& g) {
     for (;;) {
-        R x = (R)2 * P<R>::u_std(g.next()) - (R)1;
-        R z = (R)2 * P<R>::u_std(g.next()) - (R)1;
+        R x, z;
+        if constexpr (sizeof(R) == 8) {      // 2 u - 1 from the word's bits (u_pm1, exact)
+            x = P<R>::u_pm1(g.next());
+            z = P<R>::u_pm1(g.next());
+        } else {
+            x = (R)2 * P<R>::u_std(g.next()) - (R)1;
+            z = (R)2 * P<R>::u_std(g.next()) - (R)1;
+        }
         V3<R> out = mk<R>(x, 0, z);
         if (dot(out, out) < (R)1) return out;
     }
