@@ -67,7 +67,7 @@ def main():
         render_ms, _ = r.get_timings(a.steps)
         samples = cfg["w"] * cfg["h"] * spp
         print(json.dumps({
-            "config": name, "precision": a.precision, "lib": os.environ.get("RTW_LIB_OVERRIDE", "tree"), "spheres": len(scene.sphere_mat), "lights": len(scene.lights),
+            "config": name, "precision": a.precision, "tuning": a.tuning, "lib": os.environ.get("RTW_LIB_OVERRIDE", "tree"), "spheres": len(scene.sphere_mat), "lights": len(scene.lights),
             "width": cfg["w"], "height": cfg["h"], "spp": spp, "max_depth": 50,
             "msamples_s": round(samples / dt / 1e6, 1), "ms_per_render": round(dt * 1e3, 2),
             "kernel_ms": round(sum(render_ms) / len(render_ms), 2),
