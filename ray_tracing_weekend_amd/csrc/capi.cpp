@@ -1052,12 +1052,16 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
     // routes textured / quad / cuboid scenes to kernels without them)
     p.hit64 = c->hit64 ? 1u : 0u;
     // auto: walks that cross the whole grid in few pieces give the wave little to
-    // share, short ones pay each piece's setup: a fourteenth of the grid's widest
-    // side, 4..16 cells (at the default 1/2 cell per light: C3, ~16 cells wide:
-    // 4; C5, 158 wide: 11)
+    // share, short ones pay each piece's setup: f32, a fourteenth of the grid's
+    // widest side, 4..16 cells (at the default 1/2 cell per light: C3, ~16 cells
+    // wide: 4; C5, 158 wide: 11); f64, whose pieces also carry the list-order
+    // merge, a seventh, 4..24 (C3 4, C5 22: C5 3249 -> 3133 ms, C3 unchanged;
+    // profiles/r04_w_grid_piece_sweep.jsonl)
+    const uint32_t grid_w = std::max(p.sc.lg_n[0], std::max(p.sc.lg_n[1], p.sc.lg_n[2]));
     p.grid_piece = c->grid_piece != rtw_ctx::kGridPieceAuto
                        ? c->grid_piece
-                       : std::max(4u, std::min(16u, std::max(p.sc.lg_n[0], std::max(p.sc.lg_n[1], p.sc.lg_n[2])) / 14u));
+                       : (sizeof(R) == 8 ? std::max(4u, std::min(24u, grid_w / 7u))
+                                         : std::max(4u, std::min(16u, grid_w / 14u)));
     p.task_table = nullptr;
     p.tile_cost = nullptr;
     p.cost_spp = 0;
