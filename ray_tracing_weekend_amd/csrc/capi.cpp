@@ -1005,9 +1005,9 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
         }
         // the light grid's cooperative walk parks path state in the stack area
         // (f64: kCoop64PieceIds + 1 words per piece of the walk -- [count, list
-        // indices] -- after the 20-word stash: >= 64 pieces per round)
+        // indices] -- after the kCoopStash64-word stash: >= 64 pieces per round)
         const uint32_t min_stack = p.light_bvh == 1 ? light_stack
-                                   : (p.light_bvh == 2 ? (sizeof(R) == 8 ? rtw::kCoopStash + rtw::kCoop64PieceIds + 2u : rtw::kCoopStash + 1u)
+                                   : (p.light_bvh == 2 ? (sizeof(R) == 8 ? rtw::kCoopStash64 + rtw::kCoop64PieceIds + 2u : rtw::kCoopStash + 1u)
                                                        : 1u);
         // binary traversal pushes at most one entry per inner level: a leaf at
         // level `bvh_depth` has that many inner nodes above it (host/bvh.cpp)

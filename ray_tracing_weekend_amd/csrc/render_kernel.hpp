@@ -2823,8 +2823,12 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                 // ([word][lane]; the host sizes p.stack >= kCoopStash + 1) instead of
                 // being spilled to scratch by the compiler; the pieces' slots follow.
                 // (f64: the RNG state and the pending ray (o, d) itself)
-                constexpr uint32_t kStash = (kHit64 || sizeof(R) == 8) ? 20u : 8u;
-                static_assert(kStash < kCoopStash + 1, "the host's stack minimum covers the stash");
+                // (f64, RTW_STASH64_EXTRA: also the throughput and the pending
+                // bounce's weights -- without them the compiler spilled ~28
+                // dwords per lane around every walk)
+                constexpr uint32_t kStash = sizeof(R) == 8 ? kCoopStash64 : (kHit64 ? 20u : 8u);
+                static_assert(kStash < (sizeof(R) == 8 ? kCoopStash64 : kCoopStash) + 1,
+                              "the host's stack minimum covers the stash");
                 uint32_t* area = reinterpret_cast<uint32_t*>(smem) + wave * p.stack * 64;
                 // hit64: the pending ray is (o64, d64) rounded (o = pnt, d = dir), so o and d
                 // need not stay live to here
@@ -2848,6 +2852,11 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                 } else if constexpr (sizeof(R) == 8) {
                     put(4, dbits(o.x)); put(5, dbits(o.y)); put(6, dbits(o.z));
                     put(7, dbits(d.x)); put(8, dbits(d.y)); put(9, dbits(d.z));
+                    if constexpr (RTW_STASH64_EXTRA != 0) {
+                        put(10, dbits(mult.x)); put(11, dbits(mult.y)); put(12, dbits(mult.z));
+                        put(13, dbits(pend_aw.x)); put(14, dbits(pend_aw.y)); put(15, dbits(pend_aw.z));
+                        put(16, dbits(pend_ch));
+                    }
                 }
                 R acc;
                 if constexpr (sizeof(R) == 8) {
@@ -2868,6 +2877,11 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                 } else if constexpr (sizeof(R) == 8) {
                     o = V3<R>{(R)bitsd(get(4)), (R)bitsd(get(5)), (R)bitsd(get(6))};
                     d = V3<R>{(R)bitsd(get(7)), (R)bitsd(get(8)), (R)bitsd(get(9))};
+                    if constexpr (RTW_STASH64_EXTRA != 0) {
+                        mult = V3<R>{(R)bitsd(get(10)), (R)bitsd(get(11)), (R)bitsd(get(12))};
+                        pend_aw = V3<R>{(R)bitsd(get(13)), (R)bitsd(get(14)), (R)bitsd(get(15))};
+                        pend_ch = (R)bitsd(get(16));
+                    }
                 }
                 if (pend) {
                     R lpdf = PR::div_(acc, (R)p.sc.n_list);

@@ -169,6 +169,12 @@ constexpr uint32_t kBvhStack = 32;    // per-lane traversal stack entries (LDS)
 // path state per lane in the wave's stack area (render_kernel.hpp), so the
 // host gives them at least kCoopStash + 1 entries
 constexpr uint32_t kCoopStash = 20;
+// f64 light-grid kernels: the walk parks the RNG state, the ray and (when
+// RTW_STASH64_EXTRA) the path throughput and the pending bounce's weights
+#ifndef RTW_STASH64_EXTRA
+#define RTW_STASH64_EXTRA 1
+#endif
+constexpr uint32_t kCoopStash64 = RTW_STASH64_EXTRA ? 34u : 20u;
 // the f64 cooperative grid walk (lights_pdf_grid_coop64): list indices one
 // piece keeps per pass (its LDS slot: count + ids), and that a ray's owner
 // sums per pass
