@@ -1027,7 +1027,9 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
             world = rtw::kWorldBvh4;       // 4-wide, when its stack bound fits
             p.stack = std::max(p.sc.bvh4_stack + 1, min_stack);
             bvh_width = 4;
-        } else if (bin_stack <= rtw::kBvhStack) {
+        } else if (p.sc.bvh_depth <= rtw::kBvhStack && min_stack <= rtw::kWalkStashMax) {
+            // the tree bounds the traversal stack; the light grid's walk may ask
+            // for a larger per-lane area (its LDS stash + piece slots)
             p.stack = bin_stack;
             bvh_width = 2;
             const size_t lds_max = c->bvh_lds_max ? c->bvh_lds_max : (sizeof(R) == 4 ? 36 * 1024 : 52 * 1024);

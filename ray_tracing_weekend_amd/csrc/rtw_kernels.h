@@ -165,6 +165,7 @@ constexpr uint32_t kBoxRot = 144, kBoxInv = 153, kBoxT = 162, kBoxTi = 165, kBox
                    kBoxOk = 174;
 
 constexpr uint32_t kBvhStack = 32;    // per-lane traversal stack entries (LDS)
+constexpr uint32_t kWalkStashMax = 48; // per-lane LDS words the light grid's walk may ask for
 // f32 light-grid kernels: the cooperative walk parks up to this many words of
 // path state per lane in the wave's stack area (render_kernel.hpp), so the
 // host gives them at least kCoopStash + 1 entries
