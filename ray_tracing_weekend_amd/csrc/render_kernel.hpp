@@ -2920,8 +2920,11 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
 // the reference's sequential f64 fold (camera.rs:323-335).
 // chunks staged per pass: 12 KiB of LDS per wave in either precision (f64 at
 // 16 chunks took 25 KiB: six waves per CU, too few to keep the loads in flight)
+#ifndef RTW_FOLD_WIN64
+#define RTW_FOLD_WIN64 8
+#endif
 template <typename R>
-constexpr uint32_t kFoldWindow = sizeof(R) == 4 ? 16 : 8;
+constexpr uint32_t kFoldWindow = sizeof(R) == 4 ? 16 : RTW_FOLD_WIN64;
 
 template <typename R>
 __global__ void __launch_bounds__(64) reduce_chunks_kernel(const KParams<R> p, R* __restrict__ out) {
