@@ -2918,10 +2918,11 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
 // image: 0).  The fold accumulates in double whatever R is: with many chunks
 // (C4: 4096 spp) an f32 running sum would lose low bits; in f64 mode this is
 // the reference's sequential f64 fold (camera.rs:323-335).
-// chunks staged per pass: 12 KiB of LDS per wave in either precision (f64 at
-// 16 chunks took 25 KiB: six waves per CU, too few to keep the loads in flight)
+// chunks staged per pass: 12 KiB of LDS per wave in f32; f64 12 chunks (19
+// KiB: the step 0.24 ms shorter than at 8, profiles/r04_h_fold_window_ab.txt;
+// 16 took 25 KiB: six waves per CU, too few to keep the loads in flight)
 #ifndef RTW_FOLD_WIN64
-#define RTW_FOLD_WIN64 8
+#define RTW_FOLD_WIN64 12
 #endif
 template <typename R>
 constexpr uint32_t kFoldWindow = sizeof(R) == 4 ? 16 : RTW_FOLD_WIN64;

@@ -17,7 +17,8 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-VAR = os.path.join(ROOT, "build", "variants", "trace")
+VAR = os.environ.get("TRACE_VAR", os.path.join(ROOT, "build", "variants", "trace"))
+EXTRA = os.environ.get("TRACE_FLAGS", "").split()   # extra -D flags of an experiment build
 
 
 def build():
@@ -25,7 +26,7 @@ def build():
     b = os.path.join(ROOT, "ray_tracing_weekend_amd", "build")
     os.makedirs(VAR, exist_ok=True)
     common = ["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "-fno-slp-vectorize", "--offload-arch=gfx950",
-              f"-I{cs}", f"-I{ROOT}/include"]
+              f"-I{cs}", f"-I{ROOT}/include"] + EXTRA
     subprocess.run(common + ["-ffp-contract=on", "-DRTW_TRACE=f32", "-c", f"{cs}/render_f32.hip", "-o",
                              f"{VAR}/render_f32.o"], check=True)
     subprocess.run(common + ["-ffp-contract=off", "-DRTW_TRACE=f64", "-c", f"{cs}/render_f64.hip", "-o",
