@@ -2,8 +2,8 @@
 """Where f32 (hit64) paths part from f64 (experiment tool, CPU): reads a
 tools/trace_paths.py npz (per traced pixel, 64 samples x 64 segments of
 {object id, t, origin xyz, direction xyz}) and, for every sample, finds the
-first segment whose closest hit differs (object id, or t beyond 1e-9
-relative).  Each divergence is classified by the object the ray starts on
+first segment whose closest hit is another object (t differs at the f32
+level from the first segment on: hit64's camera ray is f32).  Each divergence is classified by the object the ray starts on
 (the previous segment's hit) and its material, and by whether one precision
 re-hits that object (an acne re-hit: the entry of a Metal trap, DESIGN.md
 §2b) where the other does not.  Build the trace library with the reference
@@ -55,8 +55,7 @@ def main(path):
                 ida, idb = int(a[k, 0]), int(b[k, 0])
                 if ida == -2 and idb == -2:
                     break
-                same_t = ida < 0 or abs(a[k, 1] - b[k, 1]) <= 1e-9 * max(abs(a[k, 1]), 1e-300)
-                if ida == idb and same_t:
+                if ida == idb:     # the discrete path (object sequence); t differs at f32 level
                     continue
                 prev = int(a[k - 1, 0]) if k > 0 else -1
                 kind = "camera" if k == 0 else material(prev)
