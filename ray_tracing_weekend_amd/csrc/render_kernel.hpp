@@ -1404,6 +1404,9 @@ __device__ __forceinline__ V3<double> dielectric_dir64(V3<double> u, V3<double> 
 // `kRefSphere`: Metal's UnitSphere by the reference's rejection loop in f64
 // (the f64 parity kernels), else the f32 kernels' direct sampler carried into
 // f64 (dither64).
+#ifndef RTW_HIT64_LAMB64
+#define RTW_HIT64_LAMB64 0   // hit64 Lambertian: 1 = the direction in f64 (experiment)
+#endif
 #ifndef RTW_HIT64_REF_SPHERE
 #define RTW_HIT64_REF_SPHERE 0   // hit64 Metal: 1 = the reference's f64 rejection loop (experiment)
 #endif
@@ -2701,6 +2704,8 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                         }
                     }
                     int32_t lsel = -1;   // the sampled light (f32: always counted in the pdf)
+                    V3<double> dir64l = {0.0, 0.0, 0.0};   // RTW_HIT64_LAMB64: the f64 direction
+                    bool have64 = false;
                     if (!sampled) {
                         // a sphere light (one gen_index draw, then Sphere::random)
                         // or the cosine lobe, in one pass (mixture_direction)
@@ -2709,7 +2714,21 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                             lsel = (int32_t)g.index(kargs()->sc.n_lights);
                             L = li[lsel];
                         }
-                        dir = mixture_direction(to_light, nrm, mk(L.x, L.y, L.z), L.w, pnt, g);
+                        if constexpr (kHit64 && RTW_HIT64_LAMB64 != 0) {
+                            // experiment: the Lambertian direction in f64 from the f64
+                            // normal (same words, the f64 kernels' arithmetic)
+                            V3<double> nl = to64(nrm);
+                            if (best >= sbase) {
+                                nl = sphere_normal64(pnt64, kargs()->sc.sph64[best - sbase]);
+                                if (!front64(d64, nl)) nl = -nl;
+                            }
+                            dir64l = mixture_direction<double>(to_light, nl, V3<double>{(double)L.x, (double)L.y, (double)L.z},
+                                                               (double)L.w, pnt64, g);
+                            dir = from64<R>(dir64l);
+                            have64 = true;
+                        } else {
+                            dir = mixture_direction(to_light, nrm, mk(L.x, L.y, L.z), L.w, pnt, g);
+                        }
                     }
                     RTW_PROBE_LAMBERT_DIR();
                     RTW_PROBE_CLK(4);
@@ -2729,7 +2748,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                         self_iso = next_iso;
                         if constexpr (kHit64) {
                             o64 = pnt64;
-                            d64 = dither64(dir);
+                            d64 = have64 ? dir64l : dither64(dir);
                         }
                         d = dir;
                     } else {
@@ -2764,7 +2783,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                     self_iso = next_iso;
                     if constexpr (kHit64) {
                         o64 = pnt64;
-                        d64 = dither64(dir);
+                        d64 = have64 ? dir64l : dither64(dir);
                     }
                     d = dir;
                     }
