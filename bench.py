@@ -62,6 +62,7 @@ FLOP_BOX = 20                # one child slab test: 6 x (lo*inv - o*inv) + 6 min
 FLOP_PLANE = 6               # d.n (5) + compare
 FLOP_LAMBERT_BASE = 40       # mixture sample + ONB + cosine pdf, per Lambertian bounce
 FLOP_LIGHT = 17              # one light's Sphere::hit discriminant in HittablePdf::value
+FLOP_CELL = 8                # one light-grid DDA step: 2 compares + exit_t (sub, fma, mul, max) + select
 ACCEL_NAMES = {1: "brute_lds", 2: "bvh"}
 
 
@@ -73,9 +74,9 @@ def parse():
     ap.add_argument("--precision", choices=["f32", "f64"], default="f64",
                     help="f64: the parity mode, the reference's arithmetic, bit-identical to the oracle "
                          "(the headline; FP64 roofline); f32: the speed mode (hit64)")
-    ap.add_argument("--cpu-seconds", type=float, default=8.0,
-                    help="target CPU time of the cpu_baseline sample (reference-BVH leg; the cached-BVH "
-                         "leg gets a third of it)")
+    ap.add_argument("--cpu-row-step", type=int, default=100,
+                    help="cpu_baseline sample: the fixed image rows step/2, 3 step/2, ... (every step-th row, "
+                         "stratified; no pilot, so every run times the same samples)")
     ap.add_argument("--configs", default="C3,C5",
                     help="other BASELINE configs timed on one GPU after the headline (comma list of C3, "
                          "C5; 'none' to skip)")
@@ -121,15 +122,23 @@ def kernel_identity(r, precision):
     return isa.render_kernel_name(precision, *v), isa.kernel_isa_sha(isa.render_kernel_symbol(precision, *v))
 
 
-def attach_pmc(roof, workload, kname, sha):
+def attach_pmc(roof, workload, kname, sha, chunk_sum_bytes=None):
     """traffic + PMC fractions into a roofline dict, only from a profile of
-    the same machine code (else null)."""
+    the same machine code (else null).  scratch_write_frac = (WRITE_SIZE -
+    the chunk sums the kernel must write) / WRITE_SIZE: the share of the
+    kernel's writes that is register spill (scratch write-back) or other
+    waste; `chunk_sum_bytes` = n_chunks x pixels x 3 x element bytes."""
     t = pmc_traffic(workload, kname, sha)
     roof["isa_sha"] = sha
     roof["traffic"] = t["bytes_per_launch"] if t else None
     roof["traffic_source"] = t["file"] if t else None
-    for k in ("valu_issue_frac", "lanes_active_frac", "wave_wait_frac", "mem_wait_frac", "scratch_write_frac"):
+    for k in ("valu_issue_frac", "lanes_active_frac", "wave_wait_frac", "mem_wait_frac"):
         roof[k] = t.get(k) if t else None
+    wb = t.get("write_bytes") if t else None
+    roof["write_bytes"] = wb
+    roof["chunk_sum_bytes"] = chunk_sum_bytes
+    roof["scratch_write_frac"] = (round(max(0.0, wb - chunk_sum_bytes) / wb, 4)
+                                  if wb and chunk_sum_bytes is not None else None)
     return roof
 
 
@@ -161,46 +170,37 @@ def host_cpus():
     return threads, info
 
 
-def cpu_baseline(scene, target_s):
+def cpu_baseline(scene, row_step):
     """The oracle (C restatement of the reference path, oracle/) timed on this
-    host on a bounded sample of the same workload: every k-th image row of the
-    1200x800x500spp render, faithful reference-BVH traversal (bvh.rs incl. its
-    per-visit node-AABB recomputation), one task per pixel over every CPU this
-    process may use.  Test infrastructure used as the CPU baseline only --
-    never on the GPU path."""
+    host on a bounded, FIXED sample of the same workload: the stratified image
+    rows step/2, 3 step/2, ... (every `row_step`-th row, the full width, all
+    500 spp) of the 1200x800x500spp render, faithful reference-BVH traversal
+    (bvh.rs incl. its per-visit node-AABB recomputation), one task per pixel
+    over every CPU this process may use.  No pilot: every run times the same
+    samples (sky and sphere rows differ several-fold in cost).  Test
+    infrastructure used as the CPU baseline only -- never on the GPU path."""
     from oracle import oracle as O
     threads, info = host_cpus()
     cam = O.camera_build(**dict(O.simple_camera_kw(), image_width=W, image_height=H,
                                 samples_per_pixel=SPP, max_depth=DEPTH))
     sc = O.Scene(**scene.__dict__)
+    rows = (row_step // 2, H, row_step)
     res = {}
     for name, accel in (("bvh_ref", O.ACCEL_BVH_REF), ("bvh_cached", O.ACCEL_BVH_CACHED)):
-        # pilot: one row, 1/10 of the width, to size the sample (the cached-BVH
-        # leg is informational: a third of the time)
-        tgt = target_s if name == "bvh_ref" else target_s / 3
         t0 = time.perf_counter()
-        _, st = O.render(cam, sc, 99, accel=accel, threads=1, rows=(H // 2, H // 2 + 1, 1),
-                         cols=(0, W // 10))
-        per_sample = (time.perf_counter() - t0) / max(st.samples, 1)
-        rows = int(max(1, min(H, tgt * threads / (per_sample * W * SPP))))
-        step = max(1, H // rows)
-        t0 = time.perf_counter()
-        img, st = O.render(cam, sc, 99, accel=accel, threads=threads, rows=(0, H, step))
+        img, st = O.render(cam, sc, 99, accel=accel, threads=threads, rows=rows)
         dt = time.perf_counter() - t0
-        res[name] = (st.samples / dt / 1e6, st.samples, step, dt)
+        res[name] = (st.samples / dt / 1e6, st.samples, dt)
         if name == "bvh_ref":
             ref_img = img
-        if target_s < 5:
-            break
-    v, n, step, dt = res["bvh_ref"]
+    v, n, dt = res["bvh_ref"]
     out = {"value": round(v, 4), "unit": "Msamples/s", "cores": threads, "kind": "port",
-           "sample": f"every {step}th row of the {W}x{H}x{SPP}spp depth-{DEPTH} render "
-                     f"({n} samples, {dt:.1f} s), oracle f64, reference BVH restated incl. "
-                     f"per-visit node-AABB recomputation (bvh.rs:147-152), {threads} threads",
+           "sample": f"the fixed rows {rows[0]}, {rows[0] + row_step}, ... (every {row_step}th, stratified) of the "
+                     f"{W}x{H}x{SPP}spp depth-{DEPTH} render ({n} samples, {dt:.1f} s), oracle f64, reference BVH "
+                     f"restated incl. per-visit node-AABB recomputation (bvh.rs:147-152), {threads} threads",
            "host": info}
-    if "bvh_cached" in res:
-        out["value_bvh_cached"] = round(res["bvh_cached"][0], 4)
-    out["parity"] = parity_on_sample(scene, (0, H, step), 99, ref_img)
+    out["value_bvh_cached"] = round(res["bvh_cached"][0], 4)
+    out["parity"] = parity_on_sample(scene, rows, 99, ref_img)
     return out
 
 
@@ -238,10 +238,23 @@ def parity_on_sample(scene, oracle_rows, seed, ref_full):
     return out
 
 
-def exe_flops_of(st, n_pl, n_li):
+FLOPS_BASIS = ("executed, from the kernel's counters (rtw_stats, DESIGN.md §5): node_visits x bvh_width x 20 + "
+               "sphere_tests x 17 + segments x planes x 6 + light_tests x 17 + grid_cells x 8 + lambertian x 40 "
+               "(light_tests = Lambertian bounces x lights for the linear light loop; the light grid / BVH "
+               "kernels count the lights they test)")
+
+
+def exe_flops_of(st, n_pl):
     """Executed flops of one launch from the kernel's counters."""
     return st.node_visits * int(st.bvh_width) * FLOP_BOX + st.sphere_tests * FLOP_SPHERE + \
-        st.segments * FLOP_PLANE * n_pl + st.lambertian * (FLOP_LIGHT * n_li + FLOP_LAMBERT_BASE)
+        st.segments * FLOP_PLANE * n_pl + st.light_tests * FLOP_LIGHT + st.grid_cells * FLOP_CELL + \
+        st.lambertian * FLOP_LAMBERT_BASE
+
+
+def counters_of(st):
+    """The rtw_stats counters the flops / bytes formulas read (per launch)."""
+    return {k: int(getattr(st, k)) for k in ("samples", "segments", "lambertian", "node_visits", "sphere_tests",
+                                            "light_tests", "grid_cells", "bvh_width")}
 
 
 def mode_line(scene, cam, precision, tuning, steps, warmup, dev):
@@ -253,7 +266,7 @@ def mode_line(scene, cam, precision, tuning, steps, warmup, dev):
     the plain-f32 speed mode, outside the stated f32 tolerance)."""
     prec = rtw.RTW_F32 if precision == "f32" else rtw.RTW_F64
     tdtype = torch.float32 if prec == rtw.RTW_F32 else torch.float64
-    n_pl, n_li = len(scene.plane_mat), len(scene.lights)
+    n_pl = len(scene.plane_mat)
     with rtw.Renderer(device=dev.index, precision=prec) as r:
         for k, v in tuning.items():
             r.set_tuning(k, v)
@@ -268,7 +281,7 @@ def mode_line(scene, cam, precision, tuning, steps, warmup, dev):
         st = r.get_stats()
         kname, sha = kernel_identity(r, precision)
     avg_ms = float(np.mean(render_ms))
-    flops = exe_flops_of(st, n_pl, n_li)
+    flops = exe_flops_of(st, n_pl)
     peak = PEAK_FP32_TFLOPS if prec == rtw.RTW_F32 else PEAK_FP64_TFLOPS
     rate = flops / (avg_ms * 1e-3) / 1e12
     line = {"value": round(W * H * SPP * steps / elapsed / 1e6, 3), "unit": "Msamples/s",
@@ -276,9 +289,12 @@ def mode_line(scene, cam, precision, tuning, steps, warmup, dev):
             "tuning": tuning, "kernel": kname, "chunk": int(st.chunk),
             "kernel_ms_avg": round(avg_ms, 3),
             "roofline": {"bound": "valu", "achieved": round(rate, 3), "peak": peak, "unit": "TFLOP/s",
-                         "frac": round(rate / peak, 4), "flops_per_launch": int(flops)},
+                         "frac": round(rate / peak, 4), "flops_per_launch": int(flops),
+                         "counters": counters_of(st)},
             "segments_per_sample": round(st.segments / max(st.samples, 1), 4)}
-    attach_pmc(line["roofline"], f"book1_simple_{W}x{H}_{SPP}spp_depth{DEPTH}", kname, sha)
+    esz = 4 if prec == rtw.RTW_F32 else 8
+    attach_pmc(line["roofline"], f"book1_simple_{W}x{H}_{SPP}spp_depth{DEPTH}", kname, sha,
+               chunk_sum_bytes=W * H * -(-SPP // int(st.chunk)) * 3 * esz)
     return line
 
 
@@ -394,24 +410,33 @@ def config_line(name, precision, dev):
             "segments_per_sample": round(st.segments / max(st.samples, 1), 4),
             "node_visits_per_segment": round(st.node_visits / max(st.segments, 1), 3),
             "sphere_tests_per_segment": round(st.sphere_tests / max(st.segments, 1), 3)}
+    esz = 4 if prec == rtw.RTW_F32 else 8
+    csum = cfg["w"] * cfg["h"] * -(-cfg["spp"] // int(st.chunk)) * 3 * esz
+    line["light_tests_per_lambertian"] = round(st.light_tests / max(st.lambertian, 1), 3)
+    line["grid_cells_per_lambertian"] = round(st.grid_cells / max(st.lambertian, 1), 3)
     if name == "C5":
         # f32 nodes (both child boxes + links) in both precisions: the f64 kernels cull on the f32 tree;
-        # leaf spheres {c, r^2} f32 (+ the f64 sphere of a candidate in the parity mode)
+        # leaf spheres {c, r^2} f32 (+ the f64 sphere of a candidate in the parity mode); the light
+        # grid's walks: a cell's offset pair (8 B) and each tested light {c, r} (16 B f32, 32 B f64)
         node_b, sph_b = 64, (16 if prec == rtw.RTW_F32 else 16 + 32)
-        req = st.node_visits * node_b + st.sphere_tests * sph_b
+        cell_b, light_b = 8, (16 if prec == rtw.RTW_F32 else 32)
+        req = st.node_visits * node_b + st.sphere_tests * sph_b + st.grid_cells * cell_b + st.light_tests * light_b
         rate = req / (avg_ms * 1e-3) / 1e9
         line["roofline"] = {"bound": "hbm", "achieved": round(rate, 2), "peak": 8000.0, "unit": "GB/s",
                             "frac": round(rate / 8000.0, 4), "bytes_per_launch": int(req),
-                            "basis": f"traversal requests: node visits x {node_b} B + sphere tests x {sph_b} B "
-                                     "(served by L2 / MALL: the 36 MB working set fits the 256 MB MALL)"}
-        attach_pmc(line["roofline"], workload, kname, sha)
+                            "basis": f"requests from the counters: node_visits x {node_b} B + sphere_tests x {sph_b} B "
+                                     f"+ grid_cells x {cell_b} B + light_tests x {light_b} B (served by L2 / MALL: "
+                                     "the working set fits the 256 MB MALL)",
+                            "counters": counters_of(st)}
+        attach_pmc(line["roofline"], workload, kname, sha, chunk_sum_bytes=csum)
     else:
-        flops = exe_flops_of(st, n_pl, n_li)
+        flops = exe_flops_of(st, n_pl)
         peak = PEAK_FP32_TFLOPS if prec == rtw.RTW_F32 else PEAK_FP64_TFLOPS
         rate = flops / (avg_ms * 1e-3) / 1e12
         line["roofline"] = {"bound": "valu", "achieved": round(rate, 3), "peak": peak, "unit": "TFLOP/s",
-                            "frac": round(rate / peak, 4), "flops_per_launch": int(flops)}
-        attach_pmc(line["roofline"], workload, kname, sha)
+                            "frac": round(rate / peak, 4), "flops_per_launch": int(flops),
+                            "flops_basis": FLOPS_BASIS, "counters": counters_of(st)}
+        attach_pmc(line["roofline"], workload, kname, sha, chunk_sum_bytes=csum)
     return line
 
 
@@ -517,7 +542,7 @@ def main():
     n_sph, n_pl, n_li = len(scene.sphere_mat), len(scene.plane_mat), len(scene.lights)
     alg_flops = st.segments * (ALG_SPHERE * n_sph + ALG_PLANE * n_pl) + \
         st.lambertian * (ALG_SPHERE * n_li + ALG_LAMBERT_BASE)
-    exe_flops = exe_flops_of(st, n_pl, n_li)
+    exe_flops = exe_flops_of(st, n_pl)
     accel = ACCEL_NAMES.get(int(st.accel), str(st.accel))
     avg_ms = float(np.mean(render_ms)) if render_ms else float("nan")
     alg_rate = alg_flops / (avg_ms * 1e-3) / 1e12
@@ -555,8 +580,8 @@ def main():
                      "kernel": kname,
                      "kernel_ms_avg": round(avg_ms, 3),
                      "flops_per_launch": int(exe_flops),
-                     "flops_basis": "executed: node visits x width x 20 + sphere tests x 17 + segments x planes x 6 "
-                                    "+ Lambertian bounces x (17 x lights + 40), from the kernel's counters (DESIGN.md §5)",
+                     "flops_basis": FLOPS_BASIS,
+                     "counters": counters_of(st),
                      "algorithmic_equiv_tflops": round(alg_rate, 3),
                      "algorithmic_equiv_flops_per_launch": int(alg_flops),
                      "algorithmic_equiv_basis": "SURVEY.md 8d brute-force world query (23 flops x every sphere per "
@@ -569,7 +594,8 @@ def main():
     }
     if per_rank_ms is not None:
         out["roofline"]["kernel_ms_per_rank"] = per_rank_ms
-    attach_pmc(out["roofline"], out["config"]["workload"], kname, sha)
+    attach_pmc(out["roofline"], out["config"]["workload"], kname, sha,
+               chunk_sum_bytes=W * H * -(-SPP // int(st.chunk)) * 3 * (4 if prec == rtw.RTW_F32 else 8) // world_size)
     if world_size == 1 and not a.no_modes:
         # the same workload in the other arithmetic modes (single GPU, after the timed region)
         out["modes"] = {}
@@ -585,7 +611,7 @@ def main():
             for p in (a.precision, "f32" if a.precision == "f64" else "f64"):
                 out["configs"][f"{name}_{p}"] = config_line(name, p, dev)
     if world_size == 1 and not a.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(scene, a.cpu_seconds)
+        out["cpu_baseline"] = cpu_baseline(scene, a.cpu_row_step)
     print(json.dumps(out), flush=True)
     r.close()
     if dist is not None:

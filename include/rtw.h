@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define RTW_ABI_VERSION 8
+#define RTW_ABI_VERSION 9
 
 /* error codes */
 #define RTW_OK 0
@@ -182,6 +182,12 @@ typedef struct rtw_stats {
      * HittableList::random on an empty light list (hittable_list.rs:417)
      * -> RTW_E_NO_LIGHTS */
     uint64_t panic_plane_uv, panic_no_lights;
+    /* light-pdf work (ABI 9): light tests = (bounce, light) pairs tested by the
+     * light pdf -- every Lambertian bounce x every light for the linear list
+     * loop (hittable_list.rs:408-412), the lights of the big list, the visited
+     * grid cells or light-BVH leaves for the light grid / BVH (counted by the
+     * kernel); grid_cells = light-grid cells those walks visited */
+    uint64_t light_tests, grid_cells;
 } rtw_stats;
 
 typedef struct rtw_ctx rtw_ctx;
@@ -209,6 +215,20 @@ int rtw_create_devices(const int *devices, uint32_t n_devices, int precision, rt
 /* The same over the devices whose bits are set (bit k = HIP device k, in
  * increasing order); NULL on error (an empty mask included). */
 rtw_ctx *rtw_create_mask(uint64_t device_mask, int precision);
+/* rtw_create_mask with its error code (ABI 9): RTW_E_INVALID for an empty mask
+ * or a device that is not visible (compare rtw_visible_devices), RTW_E_DEVICE
+ * for a HIP / RCCL failure -- which a caller must not answer by dropping GPUs. */
+int rtw_create_mask_ex(uint64_t device_mask, int precision, rtw_ctx **out);
+/* HIP devices visible to this process (RTW_E_DEVICE if HIP fails). */
+int rtw_visible_devices(void);
+/* TEST MODE (ABI 9): a multi-device context of n_ranks ranks that all live on
+ * one device, with every product code path of rtw_create_devices -- per-rank
+ * contexts, streams, work buffers and scene copies, rank 0 rendering into its
+ * gather slot, the equal-size slots, the assembly, the summed stats -- except
+ * the transport: the gather is n_ranks - 1 device copies on rank 0's stream,
+ * each after its rank's render, instead of ncclGather.  It lets a one-GPU box
+ * execute and check the n-rank path; RCCL stays the only product transport. */
+int rtw_create_virtual(int device, uint32_t n_ranks, int precision, rtw_ctx **out);
 /* Ranks of a context (1 for rtw_create), and rank k's per-device context
  * (k = 0: ctx itself) for rtw_get_stats / rtw_get_timings / rtw_last_kernel
  * of that rank; owned by ctx (do not destroy).  rtw_device_of: its HIP device. */
@@ -313,7 +333,9 @@ int rtw_assemble_tiles(rtw_ctx *ctx, const void *d_ranks, size_t rank_stride_byt
                        uint32_t image_width, uint32_t image_height, void *d_image, void *stream);
 /* Counters of the last render (waits for it to finish).  Returns
  * RTW_E_NO_LIGHTS / RTW_E_PANIC (stats still filled) when a sample reached a
- * reference panic. */
+ * reference panic, RTW_E_INVALID before the first render.  A multi-device
+ * context sums the ranks that took part in its last render (all of them after
+ * rtw_render / rtw_render_image_device; rank 0 after rtw_render_device). */
 int rtw_get_stats(rtw_ctx *ctx, rtw_stats *stats);
 /* Device times (HIP events) of the last min(max, 64) renders, oldest first:
  * render_ms = the render kernel alone, total_ms = render + chunk reduction.

@@ -490,9 +490,17 @@ class Renderer:
     """An rtw_ctx: a device (or, with `devices`, one rank per listed GPU:
     rtw_create_devices), a precision, a resident scene and work buffers."""
 
-    def __init__(self, device: int = 0, precision: int = RTW_F32, *, devices=None):
+    def __init__(self, device: int = 0, precision: int = RTW_F32, *, devices=None, virtual_ranks=None):
         self.ctx = None
-        if devices is not None:
+        if virtual_ranks is not None:
+            # test mode (rtw_create_virtual): `virtual_ranks` ranks on `device`,
+            # the gather by device copies -- the n-rank path on one GPU
+            out = C.c_void_p()
+            rc = _lib.rtw_create_virtual(device, int(virtual_ranks), precision, C.byref(out))
+            if rc != 0:
+                raise RenderError(rc, f"rtw_create_virtual({device}, {virtual_ranks}) failed (code {rc})")
+            self.ctx = out.value
+        elif devices is not None:
             devs = [int(d) for d in devices]
             arr = (C.c_int * max(len(devs), 1))(*devs)
             out = C.c_void_p()
@@ -520,7 +528,7 @@ class Renderer:
         sub = _lib.rtw_device_ctx(self.ctx, k)
         if not sub:
             raise RenderError(_capi.RTW_E_INVALID, f"no rank {k}")
-        return _RankView(sub, int(_lib.rtw_device_of(sub)), self.precision)
+        return _RankView(self, sub, int(_lib.rtw_device_of(sub)), self.precision)
 
     def close(self):
         if self.ctx:
@@ -620,16 +628,25 @@ class Renderer:
 
 
 class _RankView(Renderer):
-    """One rank of a multi-device Renderer (not owned: close() is a no-op)."""
+    """One rank of a multi-device Renderer (not owned: close() is a no-op).
+    It keeps its parent alive and refuses to run once the parent is closed
+    (the rank's context is freed with it)."""
 
-    def __init__(self, ctx, device, precision):   # noqa: D107  (no rtw_create)
-        self.ctx = ctx
+    def __init__(self, parent, ctx, device, precision):   # noqa: D107  (no rtw_create)
+        self._parent = parent
+        self._sub = ctx
         self.device = device
         self.precision = precision
         self.stats = _capi.rtw_stats()
 
+    @property
+    def ctx(self):
+        if self._parent is None or not self._parent.ctx:
+            raise RenderError(_capi.RTW_E_INVALID, "rank view of a closed Renderer")
+        return self._sub
+
     def close(self):
-        self.ctx = None
+        self._parent = None
 
     __del__ = close
 

@@ -67,7 +67,7 @@ class rtw_scene(C.Structure):
     ]
 
 
-ABI_VERSION = 8     # RTW_ABI_VERSION of include/rtw.h
+ABI_VERSION = 9     # RTW_ABI_VERSION of include/rtw.h
 
 
 class rtw_stats(C.Structure):
@@ -77,6 +77,7 @@ class rtw_stats(C.Structure):
         ("node_visits", C.c_uint64), ("sphere_tests", C.c_uint64),
         ("bvh_width", C.c_uint32), ("kernel", C.c_uint32),
         ("panic_plane_uv", C.c_uint64), ("panic_no_lights", C.c_uint64),
+        ("light_tests", C.c_uint64), ("grid_cells", C.c_uint64),
     ]
 
 
@@ -86,6 +87,9 @@ PROTOTYPES = [
     ("rtw_create", C.c_void_p, [C.c_int, C.c_int]),
     ("rtw_create_devices", C.c_int, [C.POINTER(C.c_int), C.c_uint32, C.c_int, C.POINTER(C.c_void_p)]),
     ("rtw_create_mask", C.c_void_p, [C.c_uint64, C.c_int]),
+    ("rtw_create_mask_ex", C.c_int, [C.c_uint64, C.c_int, C.POINTER(C.c_void_p)]),
+    ("rtw_visible_devices", C.c_int, []),
+    ("rtw_create_virtual", C.c_int, [C.c_int, C.c_uint32, C.c_int, C.POINTER(C.c_void_p)]),
     ("rtw_device_count", C.c_uint32, [C.c_void_p]),
     ("rtw_device_ctx", C.c_void_p, [C.c_void_p, C.c_uint32]),
     ("rtw_device_of", C.c_int, [C.c_void_p]),

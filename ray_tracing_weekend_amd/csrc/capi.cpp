@@ -96,7 +96,7 @@ struct rtw_ctx {
     size_t out_cap = 0;
     void* d_img = nullptr;
     size_t img_cap = 0;
-    static constexpr int kCounters = 7;   // rtw_kernels.h KParams::counters
+    static constexpr int kCounters = 9;   // rtw_kernels.h KParams::counters
     unsigned long long* d_counters = nullptr;
     std::vector<unsigned char> h_out;
     // longest-tiles-first task list (pilot render, see lpt_pilot / lpt_tasks)
@@ -121,6 +121,8 @@ struct rtw_ctx {
     rtw_stats last{};
     int last_variant = 0;             // render kernel of the last render: launch_render_impl's code
     uint32_t last_n_sph = 0;
+    uint32_t last_light_bvh = 0;      // KParams::light_bvh of the last render (0: the linear light loop)
+    uint32_t last_n_list = 0;         // ... and its light-list length
     std::string err;
     // multi-device context (rtw_create_devices): this context is rank 0 on the
     // first device; peers[k - 1] is the context of rank k on device k of the
@@ -131,6 +133,18 @@ struct rtw_ctx {
     std::vector<ncclComm_t> comms;
     void* d_gather = nullptr;         // rank 0's device: the n ranks' packed tiles (gather target)
     size_t gather_cap = 0;
+    // virtual ranks (rtw_create_virtual, a test mode): every rank on one device,
+    // the gather done by device copies on rank 0's stream after peer_ev[k - 1]
+    bool virt = false;
+    std::vector<hipEvent_t> peer_ev;
+    // the last multi-device gather + assembly, on rank 0's stream of that call:
+    // the next call's renders (every rank) wait for it before they overwrite
+    // d_gather or a peer's packed tiles
+    hipEvent_t gather_ev = nullptr;
+    bool gather_pending = false;
+    // ranks whose counters the last render filled (rtw_get_stats): n after
+    // rtw_render / rtw_render_image_device, 1 after rtw_render_device
+    uint32_t stats_ranks = 1;
 };
 
 namespace {
@@ -1012,9 +1026,10 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
         // binary traversal pushes at most one entry per inner level: a leaf at
         // level `bvh_depth` has that many inner nodes above it (host/bvh.cpp)
         const uint32_t bin_stack = std::max(p.sc.bvh_depth, min_stack);
-        // kWorldBvhLds layout: stacks + stealing area (traversal_lds) | f32 nodes (bvh32) | leaf spheres |
-        // ids (padded to 8) | lights | (f32) light pairs | (f64) the lights rounded to f32
-        const size_t tree_lds = rtw::traversal_lds<R>(bin_stack) + (size_t)p.sc.n_nodes * sizeof(rtw::BvhNode<float>) +
+        // kWorldBvhLds layout: stacks + stealing area (+ light-work counters) (traversal_lds) | f32 nodes
+        // (bvh32) | leaf spheres | ids (padded to 8) | lights | (f32) light pairs | (f64) the lights rounded to f32
+        const size_t tree_lds = rtw::traversal_lds<R>(bin_stack, p.light_bvh != 0) +
+                                (size_t)p.sc.n_nodes * sizeof(rtw::BvhNode<float>) +
                                 (size_t)p.sc.n_sph * sizeof(rtw::R4<float>) +
                                 (size_t)((p.sc.n_sph + 7u) & ~7u) * sizeof(uint32_t) +
                                 (sizeof(R) == 8 ? 32 : 0) +   // (f64: the light list 32-B aligned)
@@ -1183,6 +1198,8 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
     c->last.bvh_width = bvh_width;
     c->last.kernel = (uint32_t)world;
     c->last_n_sph = p.sc.n_sph;
+    c->last_light_bvh = p.light_bvh;
+    c->last_n_list = p.sc.n_list;
     c->last.chunk = chunk;
     return RTW_OK;
 }
@@ -1201,7 +1218,8 @@ rtw_ctx* rtw_create(int device, int precision) {
     c->precision = precision;
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
-        hipMalloc(reinterpret_cast<void**>(&c->d_counters), rtw_ctx::kCounters * sizeof(unsigned long long)) != hipSuccess) {
+        hipMalloc(reinterpret_cast<void**>(&c->d_counters), rtw_ctx::kCounters * sizeof(unsigned long long)) != hipSuccess ||
+        hipMemset(c->d_counters, 0, rtw_ctx::kCounters * sizeof(unsigned long long)) != hipSuccess) {
         rtw_destroy(c);
         return nullptr;
     }
@@ -1211,11 +1229,41 @@ rtw_ctx* rtw_create(int device, int precision) {
                 rtw_destroy(c);
                 return nullptr;
             }
-    if (false) {
-        rtw_destroy(c);
-        return nullptr;
-    }
     return c;
+}
+
+int rtw_visible_devices(void) {
+    int visible = 0;
+    return hipGetDeviceCount(&visible) == hipSuccess ? visible : RTW_E_DEVICE;
+}
+
+// the rank contexts of a multi-device context (devices[0] = rank 0 = the
+// returned context) plus the events that order consecutive gathers
+static int create_ranks(const int* devices, uint32_t n, int precision, rtw_ctx** out) {
+    rtw_ctx* c = rtw_create(devices[0], precision);
+    if (!c) return RTW_E_DEVICE;
+    c->multi = true;
+    for (uint32_t k = 1; k < n; ++k) {
+        rtw_ctx* pk = rtw_create(devices[k], precision);
+        if (!pk) {
+            rtw_destroy(c);
+            return RTW_E_DEVICE;
+        }
+        c->peers.push_back(pk);
+        hipEvent_t e = nullptr;
+        if (hipSetDevice(devices[k]) != hipSuccess || hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+            rtw_destroy(c);
+            return RTW_E_DEVICE;
+        }
+        c->peer_ev.push_back(e);
+    }
+    if (hipSetDevice(devices[0]) != hipSuccess ||
+        hipEventCreateWithFlags(&c->gather_ev, hipEventDisableTiming) != hipSuccess) {
+        rtw_destroy(c);
+        return RTW_E_DEVICE;
+    }
+    *out = c;
+    return RTW_OK;
 }
 
 int rtw_create_devices(const int* devices, uint32_t n_devices, int precision, rtw_ctx** out) {
@@ -1230,23 +1278,15 @@ int rtw_create_devices(const int* devices, uint32_t n_devices, int precision, rt
         for (uint32_t b = 0; b < a; ++b)
             if (devices[a] == devices[b]) return RTW_E_INVALID;
     }
-    int visible = 0;
-    if (hipGetDeviceCount(&visible) != hipSuccess) return RTW_E_DEVICE;
+    const int visible = rtw_visible_devices();
+    if (visible < 0) return RTW_E_DEVICE;
     for (uint32_t a = 0; a < n_devices; ++a)
         if (devices[a] >= visible) return RTW_E_INVALID;
     const RcclApi& api = rccl_api();
     if (!api.ok) return RTW_E_DEVICE;
-    rtw_ctx* c = rtw_create(devices[0], precision);
-    if (!c) return RTW_E_DEVICE;
-    c->multi = true;
-    for (uint32_t k = 1; k < n_devices; ++k) {
-        rtw_ctx* pk = rtw_create(devices[k], precision);
-        if (!pk) {
-            rtw_destroy(c);
-            return RTW_E_DEVICE;
-        }
-        c->peers.push_back(pk);
-    }
+    rtw_ctx* c = nullptr;
+    const int rc = create_ranks(devices, n_devices, precision, &c);
+    if (rc) return rc;
     c->comms.assign(n_devices, nullptr);
     const std::vector<int> list(devices, devices + n_devices);
     if (api.comm_init_all(c->comms.data(), (int)n_devices, list.data()) != ncclSuccess) {
@@ -1259,13 +1299,36 @@ int rtw_create_devices(const int* devices, uint32_t n_devices, int precision, rt
     return RTW_OK;
 }
 
-rtw_ctx* rtw_create_mask(uint64_t device_mask, int precision) {
+int rtw_create_virtual(int device, uint32_t n_ranks, int precision, rtw_ctx** out) {
+    if (!out) return RTW_E_INVALID;
+    *out = nullptr;
+    if (device < 0 || n_ranks == 0 || n_ranks > 64 || (precision != RTW_F32 && precision != RTW_F64))
+        return RTW_E_INVALID;
+    const int visible = rtw_visible_devices();
+    if (visible < 0) return RTW_E_DEVICE;
+    if (device >= visible) return RTW_E_INVALID;
+    const std::vector<int> list(n_ranks, device);
+    rtw_ctx* c = nullptr;
+    const int rc = create_ranks(list.data(), n_ranks, precision, &c);
+    if (rc) return rc;
+    c->virt = true;
+    *out = c;
+    return RTW_OK;
+}
+
+int rtw_create_mask_ex(uint64_t device_mask, int precision, rtw_ctx** out) {
+    if (!out) return RTW_E_INVALID;
+    *out = nullptr;
     std::vector<int> list;
     for (int k = 0; k < 64; ++k)
         if ((device_mask >> k) & 1u) list.push_back(k);
+    if (list.empty()) return RTW_E_INVALID;
+    return rtw_create_devices(list.data(), (uint32_t)list.size(), precision, out);
+}
+
+rtw_ctx* rtw_create_mask(uint64_t device_mask, int precision) {
     rtw_ctx* c = nullptr;
-    if (list.empty()) return nullptr;
-    return rtw_create_devices(list.data(), (uint32_t)list.size(), precision, &c) == RTW_OK ? c : nullptr;
+    return rtw_create_mask_ex(device_mask, precision, &c) == RTW_OK ? c : nullptr;
 }
 
 uint32_t rtw_device_count(const rtw_ctx* c) { return c ? 1u + (uint32_t)c->peers.size() : 0u; }
@@ -1291,9 +1354,20 @@ void rtw_destroy(rtw_ctx* c) {
             if (m && api.comm_destroy) (void)api.comm_destroy(m);
         c->comms.clear();
     }
+    if (c->virt)   // the device copies of the last gather read the peers' buffers on rank 0's device
+        for (uint32_t k = 0; k < rtw_device_count(c); ++k) {
+            (void)hipSetDevice(rtw_device_ctx(c, k)->device);
+            (void)hipDeviceSynchronize();
+        }
+    for (size_t k = 0; k < c->peer_ev.size(); ++k) {
+        (void)hipSetDevice(c->peers[k]->device);
+        if (c->peer_ev[k]) (void)hipEventDestroy(c->peer_ev[k]);
+    }
+    c->peer_ev.clear();
     for (rtw_ctx* pk : c->peers) rtw_destroy(pk);
     c->peers.clear();
     (void)hipSetDevice(c->device);
+    if (c->gather_ev) (void)hipEventDestroy(c->gather_ev);
     if (c->d_gather) (void)hipFree(c->d_gather);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->d_scene) (void)hipFree(c->d_scene);
@@ -1534,7 +1608,13 @@ int rtw_set_scene(rtw_ctx* c, const rtw_scene* s) {
     for (uint32_t k = 0; k < rtw_device_count(c); ++k) {   // multi-device: the same scene on every rank
         rtw_ctx* ck = rtw_device_ctx(c, k);
         rc = upload_scene(ck, s, blob, tmp32, tmp64);
-        if (rc) return k ? fail(c, rc, ck->err) : rc;
+        if (rc) {
+            // no rank keeps a scene: a partial update must not render one image
+            // from tiles of two scenes
+            for (uint32_t q = 0; q < rtw_device_count(c); ++q) rtw_device_ctx(c, q)->has_scene = false;
+            if (!c->peers.empty()) (void)hipSetDevice(c->device);
+            return k ? fail(c, rc, ck->err) : rc;
+        }
     }
     if (!c->peers.empty()) HIP_TRY(c, hipSetDevice(c->device));
     return RTW_OK;
@@ -1575,6 +1655,13 @@ int rtw_render_device(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t
     if (!c->has_scene) return fail(c, RTW_E_NO_SCENE, "rtw_set_scene was not called");
     HIP_TRY(c, hipSetDevice(c->device));
     hipStream_t s = resolve_stream(c, stream);
+    // a multi-device context renders on rank 0 only here: its stats are rank 0's
+    c->stats_ranks = 1;
+    if (c->gather_pending) {
+        // the last gather / assembly may still read d_gather (rank 0 renders into it
+        // again only through rtw_render_image_device, but d_out may alias it)
+        HIP_TRY(c, hipStreamWaitEvent(s, c->gather_ev, 0));
+    }
     return c->precision == RTW_F32 ? render_device_t<float>(c, cam, seed, rank, nranks, d_out, out_bytes, s)
                                    : render_device_t<double>(c, cam, seed, rank, nranks, d_out, out_bytes, s);
 }
@@ -1601,6 +1688,10 @@ int rtw_render_image_device(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, vo
         return img ? rtw_assemble_tiles(c, c->d_out, c->out_cap, 1, W, H, d_image, stream) : RTW_OK;
     }
     HIP_TRY(c, hipSetDevice(c->device));
+    // (the previous call's gather + assembly, possibly on another stream: rank
+    // 0's render below waits for gather_ev (rtw_render_device), the peers'
+    // streams were made to wait for it when it was recorded; a reallocation of
+    // d_gather in `ensure` synchronises the device)
     int rc = ensure(c, &c->d_gather, &c->gather_cap, (size_t)n * per * esz);
     if (rc) return rc;
     // launch every rank's share (asynchronous, each device on its own stream);
@@ -1617,26 +1708,52 @@ int rtw_render_image_device(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, vo
         rc = rtw_render_device(ck, cam, seed, k, n, dst, per * esz, k ? (void*)ck->stream : stream);
         if (rc) return k ? fail(c, rc, ck->err) : rc;
     }
-    // ONE gather of the packed tiles to rank 0 (RCCL over xGMI), ordered after
-    // each rank's render on that rank's stream
-    const RcclApi& api = rccl_api();
-    const ncclDataType_t dt = c->precision == RTW_F32 ? ncclFloat32 : ncclFloat64;
-    ncclResult_t r = api.group_start();
-    if (r != ncclSuccess) return rccl_fail(c, r, "ncclGroupStart");
-    for (uint32_t k = 0; k < n; ++k) {
-        rtw_ctx* ck = rtw_device_ctx(c, k);
-        r = api.gather(k ? ck->d_out : c->d_gather, k ? nullptr : c->d_gather, per, dt, 0, c->comms[k],
-                       k ? ck->stream : s0);
-        if (r != ncclSuccess) {
-            (void)api.group_end();
-            return rccl_fail(c, r, "ncclGather");
+    if (c->virt) {
+        // test mode (rtw_create_virtual): the gather as device copies on rank 0's
+        // stream, each after its rank's render -- the same slots an RCCL gather
+        // to root 0 fills
+        for (uint32_t k = 1; k < n; ++k) {
+            rtw_ctx* ck = rtw_device_ctx(c, k);
+            HIP_TRY(c, hipEventRecord(c->peer_ev[k - 1], ck->stream));
+            HIP_TRY(c, hipStreamWaitEvent(s0, c->peer_ev[k - 1], 0));
+            HIP_TRY(c, hipMemcpyAsync(static_cast<unsigned char*>(c->d_gather) + (size_t)k * per * esz, ck->d_out,
+                                      per * esz, hipMemcpyDeviceToDevice, s0));
         }
+    } else {
+        // ONE gather of the packed tiles to rank 0 (RCCL over xGMI), ordered after
+        // each rank's render on that rank's stream
+        const RcclApi& api = rccl_api();
+        const ncclDataType_t dt = c->precision == RTW_F32 ? ncclFloat32 : ncclFloat64;
+        ncclResult_t r = api.group_start();
+        if (r != ncclSuccess) return rccl_fail(c, r, "ncclGroupStart");
+        for (uint32_t k = 0; k < n; ++k) {
+            rtw_ctx* ck = rtw_device_ctx(c, k);
+            r = api.gather(k ? ck->d_out : c->d_gather, k ? nullptr : c->d_gather, per, dt, 0, c->comms[k],
+                           k ? ck->stream : s0);
+            if (r != ncclSuccess) {
+                (void)api.group_end();
+                return rccl_fail(c, r, "ncclGather");
+            }
+        }
+        r = api.group_end();
+        if (r != ncclSuccess) return rccl_fail(c, r, "ncclGroupEnd");
     }
-    r = api.group_end();
-    if (r != ncclSuccess) return rccl_fail(c, r, "ncclGroupEnd");
     HIP_TRY(c, hipSetDevice(c->device));
     // rank 0 un-interleaves the n buffers into the image
-    return img ? rtw_assemble_tiles(c, c->d_gather, per * esz, n, W, H, d_image, stream) : RTW_OK;
+    rc = img ? rtw_assemble_tiles(c, c->d_gather, per * esz, n, W, H, d_image, stream) : RTW_OK;
+    if (rc) return rc;
+    // every rank's next render waits for this gather + assembly (a peer's
+    // packed tiles are read on s0 in the virtual mode; d_gather always)
+    HIP_TRY(c, hipEventRecord(c->gather_ev, s0));
+    for (uint32_t k = 1; k < n; ++k) {
+        rtw_ctx* ck = rtw_device_ctx(c, k);
+        HIP_TRY(c, hipSetDevice(ck->device));
+        HIP_TRY(c, hipStreamWaitEvent(ck->stream, c->gather_ev, 0));
+    }
+    HIP_TRY(c, hipSetDevice(c->device));
+    c->gather_pending = true;
+    c->stats_ranks = n;
+    return RTW_OK;
 }
 
 int rtw_last_kernel(const rtw_ctx* c) {
@@ -1648,12 +1765,13 @@ static int rtw_get_stats_one(rtw_ctx* c, rtw_stats* out);
 
 int rtw_get_stats(rtw_ctx* c, rtw_stats* out) {
     if (!c || !out) return RTW_E_INVALID;
-    if (!c->peers.empty()) {
+    if (!c->peers.empty() && c->stats_ranks > 1) {
         // multi-device: the counters summed over the ranks of the last render,
-        // kernel_ms the slowest rank's; the rest as rank 0 reports it
+        // kernel_ms the slowest rank's; the rest as rank 0 reports it (after a
+        // rank-0-only rtw_render_device: rank 0's alone)
         rtw_stats sum{};
         int worst = RTW_OK;
-        for (uint32_t k = 0; k < rtw_device_count(c); ++k) {
+        for (uint32_t k = 0; k < std::min(c->stats_ranks, rtw_device_count(c)); ++k) {
             rtw_ctx* ck = rtw_device_ctx(c, k);
             rtw_stats st{};
             const int rc = rtw_get_stats_one(ck, &st);
@@ -1671,6 +1789,8 @@ int rtw_get_stats(rtw_ctx* c, rtw_stats* out) {
                 sum.sphere_tests += st.sphere_tests;
                 sum.panic_plane_uv += st.panic_plane_uv;
                 sum.panic_no_lights += st.panic_no_lights;
+                sum.light_tests += st.light_tests;
+                sum.grid_cells += st.grid_cells;
                 sum.kernel_ms = std::max(sum.kernel_ms, st.kernel_ms);
             }
         }
@@ -1682,6 +1802,7 @@ int rtw_get_stats(rtw_ctx* c, rtw_stats* out) {
 }
 
 static int rtw_get_stats_one(rtw_ctx* c, rtw_stats* out) {
+    if (c->n_renders == 0) return fail(c, RTW_E_INVALID, "no render yet");
     HIP_TRY(c, hipSetDevice(c->device));
     HIP_TRY(c, hipEventSynchronize(c->ev1));
     unsigned long long h[rtw_ctx::kCounters] = {};
@@ -1696,6 +1817,10 @@ static int rtw_get_stats_one(rtw_ctx* c, rtw_stats* out) {
     c->last.kernel_ms = ms;
     c->last.panic_plane_uv = h[4];
     c->last.panic_no_lights = h[5];
+    // the linear light loop tests every light of the list on every Lambertian
+    // bounce (hittable_list.rs:408-412); the light grid / BVH walks count theirs
+    c->last.light_tests = c->last_light_bvh ? h[7] : h[1] * (uint64_t)c->last_n_list;
+    c->last.grid_cells = h[8];
     *out = c->last;
     if (h[5])
         return fail(c, RTW_E_NO_LIGHTS, std::to_string(h[5]) + " samples drew a light from an empty light list "

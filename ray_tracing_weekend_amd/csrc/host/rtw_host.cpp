@@ -322,9 +322,19 @@ std::vector<std::vector<SampledColour>> Camera::render(const HittableList& world
                                                        const RenderOptions& opt) const {
     FlatScene flat = flatten(world, lights);
     rtw_scene view = flat.view();
-    rtw_ctx* ctx = opt.device_mask ? rtw_create_mask(opt.device_mask, opt.precision)
-                                   : rtw_create(opt.device, opt.precision);
-    if (!ctx) throw Error(RTW_E_DEVICE, "rtw_create failed (no gfx950 device, or a bad device mask?)");
+    rtw_ctx* ctx = nullptr;
+    if (opt.device_mask) {
+        // the mask's error code: RTW_E_INVALID (empty, or a device that is not
+        // visible) vs RTW_E_DEVICE (HIP / RCCL) -- both surface, neither narrows the mask
+        const int mrc = rtw_create_mask_ex(opt.device_mask, opt.precision, &ctx);
+        if (mrc != RTW_OK)
+            throw Error(mrc, mrc == RTW_E_INVALID ? "rtw_create_mask_ex: empty mask or a device that is not visible ("
+                                                    + std::to_string(rtw_visible_devices()) + " visible)"
+                                                  : "rtw_create_mask_ex: HIP / RCCL failure");
+    } else {
+        ctx = rtw_create(opt.device, opt.precision);
+        if (!ctx) throw Error(RTW_E_DEVICE, "rtw_create failed (no gfx950 device?)");
+    }
     rtw_set_accel(ctx, opt.accel);
     const uint32_t W = c_.image_width, H = c_.image_height;
     std::vector<double> sums((size_t)W * H * 3);

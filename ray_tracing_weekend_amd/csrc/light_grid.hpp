@@ -28,8 +28,10 @@ __device__ inline float grid_inv(float x) { return __builtin_amdgcn_rcpf(x); }
 // the walk rounds; the host pads every light's cell range by more than that
 // rounding, so a hit light is counted exactly once.  (Fetching the next
 // cells' ranges ahead of the tests measured slower: C5 +3 % to +15 % time.)
+// `ncell` (may be null): += the cells visited (KParams::counters[8]).
 template <typename R, typename Item>
-__host__ __device__ inline void light_grid_walk(const DevScene<R>& sc, V3<R> o, V3<R> d, Item&& item) {
+__host__ __device__ inline void light_grid_walk(const DevScene<R>& sc, V3<R> o, V3<R> d, Item&& item,
+                                                uint32_t* ncell = nullptr) {
     const R kInf = (R)INFINITY;
     const R ix = grid_inv(d.x), iy = grid_inv(d.y), iz = grid_inv(d.z);
     R tn, tf;
@@ -74,6 +76,7 @@ __host__ __device__ inline void light_grid_walk(const DevScene<R>& sc, V3<R> o, 
         const bool last = !(tx < kInf) || ni < 0 || ni >= nn;
         if (last) tx = kInf;
         const uint32_t b = sc.lg_start[c], e = sc.lg_start[c + 1];
+        if (ncell) ++*ncell;
         for (uint32_t k = b; k < e; ++k) item(k, te, tx);
         if (last) break;
         te = tx;
@@ -128,7 +131,7 @@ __host__ __device__ inline bool light_grid_span(const DevScene<R>& sc, V3<R> o, 
 // light is counted exactly once.  head && tail with t0 = tn is light_grid_walk.
 template <typename R, typename Item>
 __host__ __device__ inline void light_grid_walk_piece(const DevScene<R>& sc, V3<R> o, V3<R> d, R ix, R iy, R iz, R t0, R t1,
-                                             bool head, bool tail, Item&& item) {
+                                             bool head, bool tail, Item&& item, uint32_t* ncell = nullptr) {
     const R kInf = (R)INFINITY;
     const int nx = (int)sc.lg_n[0], ny = (int)sc.lg_n[1], nz = (int)sc.lg_n[2];
     auto cell_of = [&](R oc, R dc, R lo, R inv, int n) {
@@ -169,6 +172,7 @@ __host__ __device__ inline void light_grid_walk_piece(const DevScene<R>& sc, V3<
             tx = kInf;
         }
         const uint32_t b = sc.lg_start[c], e = sc.lg_start[c + 1];
+        if (ncell) ++*ncell;
         for (uint32_t k = b; k < e; ++k) item(k, te, tx);
         if (stop) break;
         te = tx;

@@ -1554,6 +1554,30 @@ __device__ __forceinline__ void bvh_closest_excl_steal(const DevScene<float>& sc
 //
 // Both children of a node are slab-tested against [0, inf); the visit order
 // does not matter for an all-hits query.
+// Light-pdf work of one lane, counted into KParams::counters[7] / [8]: light
+// tests (every light of the big list, a visited grid cell or a light-BVH leaf
+// that the ray is tested against) and light-grid cells visited.
+struct LightWork {
+    uint32_t tests = 0, cells = 0;
+};
+// ... added to the wave's u64 counters in LDS (w[0] tests, w[1] cells): from
+// any subset of lanes (LDS atomics), or from the whole converged wave (one sum)
+__device__ __forceinline__ void light_work_lane(unsigned long long* w, const LightWork& lw) {
+    if (lw.tests) atomicAdd(w, (unsigned long long)lw.tests);
+    if (lw.cells) atomicAdd(w + 1, (unsigned long long)lw.cells);
+}
+__device__ __forceinline__ void light_work_wave(unsigned long long* w, LightWork lw, uint32_t lane) {
+    uint32_t t = lw.tests, c = lw.cells;
+    for (int off = 32; off > 0; off >>= 1) {
+        t += (uint32_t)__shfl_xor((int)t, off);
+        c += (uint32_t)__shfl_xor((int)c, off);
+    }
+    if (lane == 0) {
+        w[0] += t;
+        w[1] += c;
+    }
+}
+
 template <typename R, typename Leaf>
 __device__ __forceinline__ void light_bvh_walk(const DevScene<R>& sc, V3<R> o, V3<R> d,
                                                int32_t* __restrict__ stk, Leaf&& leaf) {
@@ -1599,11 +1623,12 @@ __device__ __forceinline__ void light_bvh_walk(const DevScene<R>& sc, V3<R> o, V
 // f32: light_hit_f32 / light_pdf_f32 as in lights_pdf_sum; pdfs summed in walk order.
 template <bool kRobust>
 __device__ __forceinline__ float lights_pdf_bvh(const DevScene<float>& sc, V3<float> o, V3<float> d,
-                                                int32_t* __restrict__ stk) {
+                                                int32_t* __restrict__ stk, LightWork& lw) {
     const float a = len2_f32(d);
     const float ia = __builtin_amdgcn_rcpf(a);
     float acc = 0.f;
     light_bvh_walk(sc, o, d, stk, [&](uint32_t k) {
+        ++lw.tests;
         const R4<float> L = sc.lsph[k];
         const bool hit = light_hit_f32<kRobust>(L, o, d, a, ia);
         if (hit) acc += light_pdf_f32(L, o);
@@ -1616,10 +1641,11 @@ __device__ __forceinline__ float lights_pdf_bvh(const DevScene<float>& sc, V3<fl
 // falls back to the linear loop.
 template <bool kRobust>
 __device__ __forceinline__ double lights_pdf_bvh(const DevScene<double>& sc, V3<double> o, V3<double> d,
-                                                 int32_t* __restrict__ stk) {
+                                                 int32_t* __restrict__ stk, LightWork& lw) {
     const LightPre pre(o, d);
     return lights_sum_in_list_order(sc.lights, o, d, [&](auto&& add) {
         light_bvh_walk(sc, o, d, stk, [&](uint32_t k) {
+            ++lw.tests;
             const R4<double> L = sc.lsph[k];
             double t;
             if (pre.may_hit(L) && sphere_t(mk(L.x, L.y, L.z), L.w * L.w, o, d, 0.0, t)) add(sc.lid[k]);
@@ -1630,20 +1656,23 @@ __device__ __forceinline__ double lights_pdf_bvh(const DevScene<double>& sc, V3<
 // f32: the big list, then the walk; a light counts in the cell whose interval
 // holds its closest-approach parameter tc = -(d . (o - c)) / (d . d)
 template <bool kRobust>
-__device__ __forceinline__ float lights_pdf_grid(const DevScene<float>& sc, V3<float> o, V3<float> d) {
+__device__ __forceinline__ float lights_pdf_grid(const DevScene<float>& sc, V3<float> o, V3<float> d,
+                                                 LightWork& lw) {
     const float a = len2_f32(d);
     const float ia = __builtin_amdgcn_rcpf(a);
     float acc = 0.f;
+    lw.tests += sc.lg_big;
     for (uint32_t k = 0; k < sc.lg_big; ++k) {
         const R4<float> L = sc.lg_sph[k];
         if (light_hit_f32<kRobust>(L, o, d, a, ia)) acc += light_pdf_f32(L, o);
     }
     light_grid_walk(sc, o, d, [&](uint32_t k, float te, float tx) {
+        ++lw.tests;
         const R4<float> L = sc.lg_sph[k];
         const float fx = o.x - L.x, fy = o.y - L.y, fz = o.z - L.z;
         const float tc = -__builtin_fmaf(d.z, fz, __builtin_fmaf(d.y, fy, d.x * fx)) * ia;
         if (light_hit_f32<kRobust>(L, o, d, a, ia) & (tc >= te) & (tc < tx)) acc += light_pdf_f32(L, o);
-    });
+    }, &lw.cells);
     return acc;
 }
 // lights_pdf_grid by the whole wave (f32, KParams::grid_piece = P > 0).  A ray
@@ -1664,12 +1693,13 @@ __device__ __forceinline__ float lights_pdf_grid(const DevScene<float>& sc, V3<f
 template <bool kRobust>
 __device__ __forceinline__ float lights_pdf_grid_coop(const DevScene<float>& sc, bool pend, V3<float> o, V3<float> d,
                                                    uint32_t P, float* __restrict__ slots, uint32_t cap,
-                                                   uint32_t lane) {
+                                                   uint32_t lane, LightWork& lw) {
     float acc = 0.f, tn = 0.f, tf = 0.f;
     uint32_t k = 0;
     if (pend) {
         const float a = len2_f32(d);
         const float ia = __builtin_amdgcn_rcpf(a);
+        lw.tests += sc.lg_big;
         for (uint32_t q = 0; q < sc.lg_big; ++q) {
             const R4<float> L = sc.lg_sph[q];
             if (light_hit_f32<kRobust>(L, o, d, a, ia)) acc += light_pdf_f32(L, o);
@@ -1710,12 +1740,13 @@ __device__ __forceinline__ float lights_pdf_grid_coop(const DevScene<float>& sc,
                 float part = j == 0 ? racc : 0.f;
                 light_grid_walk_piece(sc, ro, rd, grid_inv(rd.x), grid_inv(rd.y), grid_inv(rd.z), t_at(j),
                                       t_at(j + 1), j == 0, j + 1 == rk, [&](uint32_t q, float te, float tx) {
+                    ++lw.tests;
                     const R4<float> L = sc.lg_sph[q];
                     const float fx = ro.x - L.x, fy = ro.y - L.y, fz = ro.z - L.z;
                     const float tc = -__builtin_fmaf(rd.z, fz, __builtin_fmaf(rd.y, fy, rd.x * fx)) * ria;
                     if (light_hit_f32<kRobust>(L, ro, rd, ra, ria) & (tc >= te) & (tc < tx))
                         part += light_pdf_f32(L, ro);
-                });
+                }, &lw.cells);
                 slots[g - b] = part;
             }
         }
@@ -1736,23 +1767,26 @@ __device__ __forceinline__ float lights_pdf_grid_coop(const DevScene<float>& sc,
 // f64 (parity mode): the hit lights' list indices, summed in LIST order
 // (lights_sum_in_list_order) as in lights_pdf_bvh.
 template <bool kRobust>
-__device__ __forceinline__ double lights_pdf_grid(const DevScene<double>& sc, V3<double> o, V3<double> d) {
+__device__ __forceinline__ double lights_pdf_grid(const DevScene<double>& sc, V3<double> o, V3<double> d,
+                                                  LightWork& lw) {
     const LightPre pre(o, d);   // the f32 pre-pass rules out the lights the ray misses
     const double ia = 1.0 / (d.x * d.x + d.y * d.y + d.z * d.z);
     return lights_sum_in_list_order(sc.lights, o, d, [&](auto&& add) {
+        lw.tests += sc.lg_big;
         for (uint32_t k = 0; k < sc.lg_big; ++k) {
             const R4<double> L = sc.lg_sph[k];
             double t;
             if (pre.may_hit(L) && sphere_t(mk(L.x, L.y, L.z), L.w * L.w, o, d, 0.0, t)) add(sc.lg_id[k]);
         }
         light_grid_walk(sc, o, d, [&](uint32_t k, double te, double tx) {
+            ++lw.tests;
             const R4<double> L = sc.lg_sph[k];
             double t;
             if (pre.may_hit(L) && sphere_t(mk(L.x, L.y, L.z), L.w * L.w, o, d, 0.0, t)) {
                 const double tc = -((o.x - L.x) * d.x + (o.y - L.y) * d.y + (o.z - L.z) * d.z) * ia;
                 if (tc >= te && tc < tx) add(sc.lg_id[k]);
             }
-        });
+        }, &lw.cells);
     });
 }
 
@@ -1776,12 +1810,12 @@ __device__ __forceinline__ double lights_pdf_grid(const DevScene<double>& sc, V3
 // `slots`.
 __device__ __forceinline__ double lights_pdf_grid_coop64(const DevScene<double>& sc, bool pend, V3<double> o,
                                                          V3<double> d, uint32_t P, uint32_t* __restrict__ slots,
-                                                         uint32_t cap_words, uint32_t lane) {
+                                                         uint32_t cap_words, uint32_t lane, LightWork& lw) {
     constexpr uint32_t kPieceIds = kCoop64PieceIds, kSlot = kPieceIds + 1, kMax = RTW_COOP64_MAX;
     const uint32_t cap = cap_words / (kSlot * 64) * 64;   // pieces per round
     // (the host sizes the stack area for at least one round of 64 pieces; a
     // smaller area takes the per-lane walk -- never a loop that cannot advance)
-    if (cap == 0) return pend ? lights_pdf_grid<false>(sc, o, d) : 0.0;
+    if (cap == 0) return pend ? lights_pdf_grid<false>(sc, o, d, lw) : 0.0;
     double tn = 0.0, tf = 0.0;
     uint32_t k = 0;
     if (pend) {
@@ -1812,6 +1846,7 @@ __device__ __forceinline__ double lights_pdf_grid_coop64(const DevScene<double>&
         };
         if (more) {
             const LightPre pre(o, d);
+            lw.tests += sc.lg_big;
             for (uint32_t q = 0; q < sc.lg_big; ++q) {
                 const R4<double> L = sc.lg_sph[q];
                 double t;
@@ -1852,6 +1887,7 @@ __device__ __forceinline__ double lights_pdf_grid_coop64(const DevScene<double>&
                     uint32_t cnt = 0;
                     light_grid_walk_piece(sc, ro, rd, grid_inv(rd.x), grid_inv(rd.y), grid_inv(rd.z), t_at(j),
                                           t_at(j + 1), j == 0, j + 1 == rk, [&](uint32_t q, double te, double tx) {
+                        ++lw.tests;
                         const R4<double> L = sc.lg_sph[q];
                         double t;
                         if (rpre.may_hit(L) && sphere_t(mk(L.x, L.y, L.z), L.w * L.w, ro, rd, 0.0, t)) {
@@ -1872,7 +1908,7 @@ __device__ __forceinline__ double lights_pdf_grid_coop64(const DevScene<double>&
                                 ent[m] = id;
                             }
                         }
-                    });
+                    }, &lw.cells);
                     ent[-1] = cnt;
                 }
             }
@@ -2097,7 +2133,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
     // instead of the vector-memory (TA/L1) path the shading loads use.
     DevScene<R> scw = p.sc;
     if constexpr (kWorld == kWorldBvhLds) {
-        unsigned char* base = smem + traversal_lds<R>(p.stack);
+        unsigned char* base = smem + traversal_lds<R>(p.stack, kLightBvh);
         // the f32 tree (bvh32) in both precisions: the while-while traversal culls on it
         BvhNode<float>* l_nodes = reinterpret_cast<BvhNode<float>*>(base);
         // the leaf spheres {c, r^2} in f32 (f64: the pre-pass copy bsph32; the
@@ -2162,6 +2198,13 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
     constexpr bool kSteal = RTW_STEAL && kWorld == kWorldBvhLds;
     unsigned char* const steal_area =
         smem + (size_t)kWavesPerBlock * p.stack * 64 * sizeof(int32_t) + wave * kStealLdsPerWave<R>;
+    // the light BVH / grid kernels: the wave's light-work counters (u64 light
+    // tests, grid cells), right after the traversal area
+    unsigned long long* const wcnt =
+        reinterpret_cast<unsigned long long*>(smem + traversal_lds<R>(p.stack) + wave * kLightWorkBytes);
+    if constexpr (kLightBvh) {
+        if (lane < 2) wcnt[lane] = 0ull;
+    }
     // the wave's current task (wave-uniform): local tile lt = global 8x8 tile
     // T = lt * nranks + rank at (tx, ty) -- the ranks take the image's tiles
     // round-robin (rtw_tiles_for_rank) -- and chunks [c_begin, c_begin +
@@ -2754,12 +2797,15 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                     } else {
                     if (kPrims && kargs()->sc.lref)
                         acc = lights_pdf_mixed(p.sc, li, pnt, dir);
-                    else if constexpr (kLightBvh)
+                    else if constexpr (kLightBvh) {
+                        LightWork lw;
                         acc = p.light_bvh == 2
-                                  ? lights_pdf_grid<kRobust>(p.sc, pnt, dir)
+                                  ? lights_pdf_grid<kRobust>(p.sc, pnt, dir, lw)
                                   : lights_pdf_bvh<kRobust>(p.sc, pnt, dir,
-                                                            reinterpret_cast<int32_t*>(smem) + wave * p.stack * 64 + lane);
-                    else if constexpr (kWorld == kWorldBvhLds && sizeof(R) == 4)
+                                                            reinterpret_cast<int32_t*>(smem) + wave * p.stack * 64 + lane,
+                                                            lw);
+                        light_work_lane(wcnt, lw);
+                    } else if constexpr (kWorld == kWorldBvhLds && sizeof(R) == 4)
                         acc = lights_pdf_sum_pk<kRobust>(li, l_lp, kargs()->sc.n_lights, pnt, dir, lsel);
                     else if constexpr (kWorld == kWorldBvhLds && sizeof(R) == 8)
                         acc = lights_pdf_sum<kRobust>(li, kargs()->sc.n_lights, pnt, dir, l_li32);
@@ -2878,14 +2924,16 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                     }
                 }
                 R acc;
+                LightWork lw;
                 if constexpr (sizeof(R) == 8) {
                     acc = lights_pdf_grid_coop64(p.sc, pend, po, pd, kargs()->grid_piece, area + kStash * 64,
-                                                 (p.stack - kStash) * 64, lane);
+                                                 (p.stack - kStash) * 64, lane, lw);
                 } else {
                     float* slots = reinterpret_cast<float*>(area + kStash * 64);
                     acc = lights_pdf_grid_coop<kRobust>(p.sc, pend, po, pd, kargs()->grid_piece, slots,
-                                                        (p.stack - kStash) * 64, lane);
+                                                        (p.stack - kStash) * 64, lane, lw);
                 }
+                light_work_wave(wcnt, lw, lane);
                 g.s0 = get(0);
                 g.s1 = get(1);
                 g.s2 = get(2);
@@ -2929,6 +2977,10 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
         atomicAdd(p.counters + 1, (unsigned long long)lambs);
         if (nvis) atomicAdd(p.counters + 2, (unsigned long long)nvis);
         if (ntest) atomicAdd(p.counters + 3, (unsigned long long)ntest);
+        if constexpr (kLightBvh) {
+            if (wcnt[0]) atomicAdd(p.counters + 7, wcnt[0]);
+            if (wcnt[1]) atomicAdd(p.counters + 8, wcnt[1]);
+        }
     }
 }
 
@@ -3060,7 +3112,7 @@ constexpr int kVariantRan = 1 << 16;
 template <typename R, int kOpt>
 inline int launch_world(const KParams<R>& p, int world, size_t lds_bytes, uint32_t blocks,
                         hipStream_t stream) {
-    const size_t stacks = traversal_lds<R>(p.stack);
+    const size_t stacks = traversal_lds<R>(p.stack, (kOpt & dev::kOptLightBvh) != 0);
     const bool resident = p.persist == kPersistResident;
     constexpr int kBrute = kOpt & ~dev::kOptLightBvh;   // the light BVH needs the BVH kernels' stack
     // textured scenes are small: their kernels exist for the brute-force and

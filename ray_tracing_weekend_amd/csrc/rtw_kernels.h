@@ -194,10 +194,16 @@ template <typename R>
 constexpr uint32_t kStealSlotBytes = sizeof(R) == 4 ? 64 * 8 : 64 * 20;   // f64: + a culling bound per ray
 template <typename R>
 constexpr uint32_t kStealLdsPerWave = kStealSlotBytes<R> + 64;
-// LDS of the traversal stacks + the stealing area of one workgroup
+// light-pdf work counters of a wave (u64 light tests, u64 light-grid cells:
+// KParams::counters[7], [8]); the kernels with the light BVH / grid
+// (light_bvh != 0) keep them right after the traversal area
+constexpr uint32_t kLightWorkBytes = 16;
+// LDS of the traversal stacks + the stealing area of one workgroup (+ the
+// light-work counters when `light_work`)
 template <typename R>
-__host__ __device__ inline size_t traversal_lds(uint32_t stack) {
-    return (size_t)kWavesPerBlock * ((size_t)stack * 64 * sizeof(int32_t) + kStealLdsPerWave<R>);
+__host__ __device__ inline size_t traversal_lds(uint32_t stack, bool light_work = false) {
+    return (size_t)kWavesPerBlock * ((size_t)stack * 64 * sizeof(int32_t) + kStealLdsPerWave<R> +
+                                     (light_work ? kLightWorkBytes : 0));
 }
 constexpr uint32_t kPersistResident = 0xFFFFFFFFu;   // KParams::persist: one resident grid
 
@@ -208,7 +214,8 @@ struct KParams {
     R* partial;                       // [n_local_tiles][64][n_chunks][3] item (chunk) sums
     unsigned long long* counters;     // [0] segments, [1] lambertian, [2] node visits,
                                       // [3] sphere tests, [4] plane-UV panics, [5] empty-light panics,
-                                      // [6] next task (persistent waves)
+                                      // [6] next task (persistent waves), [7] light tests and
+                                      // [8] light-grid cells of the light BVH / grid walks
     R center[3], p00[3], du[3], dv[3], disk_u[3], disk_v[3], bg[3];
     R u_scale;                        // Uniform::new_inclusive(-0.5, 0.5) scale
     uint64_t seed;

@@ -173,12 +173,13 @@ extern "C" int rtw_probe_timeline_read(unsigned long long* out, size_t n, int re
 #if RTW_EXP == 2 || RTW_EXP == 7
 #define RTW_PROBE_LIGHT_PDF() \
     do { \
+        LightWork lw2; \
         if constexpr (kLightBvh) \
             ntest += (p.light_bvh == 2 \
-                         ? lights_pdf_grid<kRobust>(p.sc, pnt, RTW_EXP == 7 ? dir : mk(dir.y, dir.z, dir.x)) \
+                         ? lights_pdf_grid<kRobust>(p.sc, pnt, RTW_EXP == 7 ? dir : mk(dir.y, dir.z, dir.x), lw2) \
                          : lights_pdf_bvh<kRobust>(p.sc, pnt, RTW_EXP == 7 ? dir : mk(dir.y, dir.z, dir.x), \
                                                    reinterpret_cast<int32_t*>(smem) + wave * p.stack * 64 + \
-                                                       lane)) == (R)-7 ? 1u : 0u; \
+                                                       lane, lw2)) == (R)-7 ? 1u : 0u; \
         else \
             ntest += lights_pdf_sum<kRobust>(li, p.sc.n_lights, pnt, mk(dir.y, dir.z, dir.x)) == (R)-7 ? 1u : 0u; \
     } while (0)

@@ -112,3 +112,89 @@ def test_n_device_context_is_bit_identical(prec):
         assert r.stats.samples == samples
     ok = ~np.isnan(ref)
     assert np.array_equal(np.isnan(img), np.isnan(ref)) and np.array_equal(img[ok], ref[ok])
+
+
+# ---- the n-rank path on one GPU: rtw_create_virtual (ABI 9, test mode) ------
+# Every rank of the context lives on device 0 and the gather is device copies
+# on rank 0's stream; everything else is the product path (per-rank contexts,
+# streams, buffers and scene copies, rank 0 rendering into its gather slot,
+# the assembly, the summed stats, the per-rank longest-first task lists).
+
+
+@pytest.mark.parametrize("prec", [rtw.RTW_F64, rtw.RTW_F32])
+@pytest.mark.parametrize("n", [2, 3, 8])
+def test_virtual_ranks_bit_identical(prec, n):
+    scene, cam = _cam(w=120, h=72, spp=40)          # 15 x 9 tiles: ragged over 2, 3 and 8 ranks
+    with rtw.Renderer(device=0, precision=prec) as r:
+        r.set_tuning("lpt_min_spp", 8)
+        r.set_scene(scene)
+        ref = r.render(cam, 9)
+        st = r.stats
+        ref_samples, ref_segments, ref_lamb = st.samples, st.segments, st.lambertian
+    with rtw.Renderer(device=0, precision=prec, virtual_ranks=n) as r:
+        assert r.n_devices == n
+        r.set_tuning("lpt_min_spp", 8)
+        r.set_scene(scene)
+        a = r.render(cam, 9)                         # counting render (tile index order)
+        assert r.stats.samples == ref_samples == cam.image_width * cam.image_height * cam.samples_per_pixel
+        assert r.stats.segments == ref_segments and r.stats.lambertian == ref_lamb
+        assert r.stats.light_tests == ref_lamb * np.asarray(scene.lights).reshape(-1, 4).shape[0]
+        b = r.render(cam, 9)                         # every rank's longest-first task list
+        assert r.stats.segments == ref_segments
+        per_rank = sum(r.rank_view(k).get_stats().samples for k in range(n))
+        assert per_rank == ref_samples
+    ok = ~np.isnan(ref)
+    for img in (a, b):
+        assert np.array_equal(np.isnan(img), np.isnan(ref)) and np.array_equal(img[ok], ref[ok])
+
+
+def test_virtual_ranks_image_device_streams_and_stats():
+    """rtw_render_image_device of a virtual 3-rank context on two different
+    torch streams back to back (the second call's renders wait for the first
+    call's gather + assembly), then rtw_render_device on the same context:
+    its stats are rank 0's alone."""
+    scene, cam = _cam(w=64, h=48, spp=6)
+    ref, samples, _ = _single(scene, cam, rtw.RTW_F64, seed=4)
+    with rtw.Renderer(device=0, precision=rtw.RTW_F64, virtual_ranks=3) as r:
+        r.set_scene(scene)
+        imgs = []
+        for k in range(2):
+            s = torch.cuda.Stream()
+            with torch.cuda.stream(s):
+                img = torch.full((cam.image_height, cam.image_width, 3), float("nan"), dtype=torch.float64,
+                                 device="cuda:0")
+                r.render_image_device(cam, 4, img.data_ptr(), img.numel() * 8)
+                imgs.append(img.cpu().numpy())
+        assert r.get_stats().samples == samples
+        n0 = rtw.tiles_for_rank(cam.image_width, cam.image_height, 0, 1) * 64 * 3
+        out = torch.zeros(n0, dtype=torch.float64, device="cuda:0")
+        r.render_device(cam, 4, out.data_ptr(), out.numel() * 8)
+        torch.cuda.synchronize()
+        assert r.get_stats().samples == samples      # one rank rendered everything: rank 0's stats
+        v = r.rank_view(1)
+    with pytest.raises(rtw.RenderError):
+        v.get_stats()                                # the parent is closed
+    ok = ~np.isnan(ref)
+    for got in imgs:
+        assert np.array_equal(np.isnan(got), np.isnan(ref)) and np.array_equal(got[ok], ref[ok])
+
+
+def test_virtual_ranks_light_grid_counters():
+    """A scene whose light pdf takes the light grid (>= 64 lights): the light
+    tests and grid cells counted by the kernel (ABI 9) are properties of the
+    samples, so a 3-rank render sums to the one-rank counts; the image too."""
+    scene, b = rtw.scenes.simple_soa(SEED, n=20)
+    cam = b.with_image_width(48).with_image_height(32).with_samples_per_pixel(4).with_max_depth(50).build()
+    assert np.asarray(scene.lights).reshape(-1, 4).shape[0] >= 64
+    with rtw.Renderer(device=0, precision=rtw.RTW_F64) as r:
+        r.set_scene(scene)
+        ref = r.render(cam, 2)
+        st = (r.stats.light_tests, r.stats.grid_cells, r.stats.segments)
+        assert r.last_kernel()[1] & 2                # the light grid / BVH kernel ran
+    assert st[0] > 0 and st[1] > 0
+    with rtw.Renderer(device=0, precision=rtw.RTW_F64, virtual_ranks=3) as r:
+        r.set_scene(scene)
+        img = r.render(cam, 2)
+        assert (r.stats.light_tests, r.stats.grid_cells, r.stats.segments) == st
+    ok = ~np.isnan(ref)
+    assert np.array_equal(np.isnan(img), np.isnan(ref)) and np.array_equal(img[ok], ref[ok])
