@@ -337,6 +337,9 @@ int rtw_assemble_tiles(rtw_ctx *ctx, const void *d_ranks, size_t rank_stride_byt
  * context sums the ranks that took part in its last render (all of them after
  * rtw_render / rtw_render_image_device; rank 0 after rtw_render_device). */
 int rtw_get_stats(rtw_ctx *ctx, rtw_stats *stats);
+/* Rank k's own counters of its last render (k = 0 included: rtw_get_stats on
+ * rtw_device_ctx(ctx, 0) == ctx sums the ranks), ABI 9. */
+int rtw_get_stats_rank(rtw_ctx *ctx, uint32_t k, rtw_stats *stats);
 /* Device times (HIP events) of the last min(max, 64) renders, oldest first:
  * render_ms = the render kernel alone, total_ms = render + chunk reduction.
  * Waits for them; returns how many were written. */

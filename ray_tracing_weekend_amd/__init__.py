@@ -528,7 +528,7 @@ class Renderer:
         sub = _lib.rtw_device_ctx(self.ctx, k)
         if not sub:
             raise RenderError(_capi.RTW_E_INVALID, f"no rank {k}")
-        return _RankView(self, sub, int(_lib.rtw_device_of(sub)), self.precision)
+        return _RankView(self, k, sub, int(_lib.rtw_device_of(sub)), self.precision)
 
     def close(self):
         if self.ctx:
@@ -632,8 +632,9 @@ class _RankView(Renderer):
     It keeps its parent alive and refuses to run once the parent is closed
     (the rank's context is freed with it)."""
 
-    def __init__(self, parent, ctx, device, precision):   # noqa: D107  (no rtw_create)
+    def __init__(self, parent, k, ctx, device, precision):   # noqa: D107  (no rtw_create)
         self._parent = parent
+        self._k = k
         self._sub = ctx
         self.device = device
         self.precision = precision
@@ -644,6 +645,12 @@ class _RankView(Renderer):
         if self._parent is None or not self._parent.ctx:
             raise RenderError(_capi.RTW_E_INVALID, "rank view of a closed Renderer")
         return self._sub
+
+    def get_stats(self) -> "_capi.rtw_stats":
+        """This rank's own counters (rtw_get_stats_rank; rank 0 too)."""
+        self.ctx
+        self._check(_lib.rtw_get_stats_rank(self._parent.ctx, self._k, C.byref(self.stats)), "rtw_get_stats_rank")
+        return self.stats
 
     def close(self):
         self._parent = None

@@ -113,6 +113,7 @@ PROTOTYPES = [
     ("rtw_assemble_tiles", C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_uint32, C.c_uint32,
                                      C.c_uint32, C.c_void_p, C.c_void_p]),
     ("rtw_get_stats", C.c_int, [C.c_void_p, C.POINTER(rtw_stats)]),
+    ("rtw_get_stats_rank", C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(rtw_stats)]),
     ("rtw_get_timings", C.c_int, [C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_float), C.c_int]),
     ("rtw_last_kernel", C.c_int, [C.c_void_p]),
     ("rtw_scene_simple", C.c_void_p, [C.c_uint64, C.c_int]),

@@ -1763,6 +1763,16 @@ int rtw_last_kernel(const rtw_ctx* c) {
 
 static int rtw_get_stats_one(rtw_ctx* c, rtw_stats* out);
 
+int rtw_get_stats_rank(rtw_ctx* c, uint32_t k, rtw_stats* out) {
+    if (!c || !out) return RTW_E_INVALID;
+    rtw_ctx* ck = rtw_device_ctx(c, k);
+    if (!ck) return fail(c, RTW_E_INVALID, "no rank " + std::to_string(k));
+    const int rc = rtw_get_stats_one(ck, out);
+    if (k && rc) c->err = ck->err;
+    (void)hipSetDevice(c->device);
+    return rc;
+}
+
 int rtw_get_stats(rtw_ctx* c, rtw_stats* out) {
     if (!c || !out) return RTW_E_INVALID;
     if (!c->peers.empty() && c->stats_ranks > 1) {

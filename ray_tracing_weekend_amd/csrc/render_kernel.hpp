@@ -2305,9 +2305,6 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
     // cooperative grid walk at the end of the trip (lights_pdf_grid_coop); the
     // bounce's att * scattering pdf and half its cosine pdf wait with it
     constexpr bool kCoopGrid = kLightBvh && !kPrims;
-    bool pend = false;
-    V3<R> pend_aw = zero;
-    R pend_ch = (R)0;
     RTW_PROBE_WAVE_BEGIN();
     RTW_PROBE_CLK_INIT();
     RTW_PROBE_HIT_INIT();
@@ -2402,6 +2399,12 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
         if (live == 0) break;
         segs += (uint32_t)__popcll(live);   // every active lane runs one segment of this trip
         bool lamb = false;                  // the lane's segment ended in a Lambertian scatter
+        // (kCoopGrid) this trip's pending light pdf and the bounce's weights: set by
+        // the Lambertian branch, consumed by the walk at the end of the same trip --
+        // declared per trip, so the compiler does not carry them across trips
+        bool pend = false;
+        V3<R> pend_aw = zero;
+        R pend_ch = (R)0;
         RTW_PROBE_CLK(12);
         RTW_PROBE_LANES(3);
         if (active) {
