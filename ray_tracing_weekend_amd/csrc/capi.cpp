@@ -429,6 +429,9 @@ std::vector<unsigned char> stage_scene(const rtw_scene* s, rtw::DevScene<R>* ds,
     const size_t o_lgs = reserve(sizeof(uint32_t) * lg.start.size());
     const size_t o_lgsph = reserve(sizeof(R4) * lg.items.size());
     const size_t o_lgid = reserve(sizeof(uint32_t) * lg.items.size());
+    // f64: the grid's lights rounded to f32 with |r| -- the f64 kernels' walk runs
+    // in f32 on them (render_kernel.hpp lights_pdf_grid_coop64)
+    const size_t o_lgsph32 = reserve(std::is_same<R, double>::value ? sizeof(rtw::R4<float>) * lg.items.size() : 0);
     std::vector<unsigned char> blob(align_up(off, 64) + 64, 0);
     unsigned char* b = blob.data();
     for (uint32_t k = 0; k < s->n_spheres; ++k) {
@@ -706,6 +709,11 @@ std::vector<unsigned char> stage_scene(const rtw_scene* s, rtw::DevScene<R>* ds,
         const uint32_t id = lg.items[k];
         reinterpret_cast<R4*>(b + o_lgsph)[k] = reinterpret_cast<const R4*>(b + o_li)[id];
         reinterpret_cast<uint32_t*>(b + o_lgid)[k] = id;
+        if constexpr (std::is_same<R, double>::value) {
+            const double* l = s->lights + 4 * (size_t)id;
+            reinterpret_cast<rtw::R4<float>*>(b + o_lgsph32)[k] =
+                rtw::R4<float>{(float)l[0], (float)l[1], (float)l[2], fabsf((float)l[3])};
+        }
     }
     ds->lg_start = reinterpret_cast<const uint32_t*>(base + o_lgs);
     ds->lg_sph = reinterpret_cast<const R4*>(base + o_lgsph);
@@ -726,6 +734,7 @@ std::vector<unsigned char> stage_scene(const rtw_scene* s, rtw::DevScene<R>* ds,
     if constexpr (std::is_same<R, double>::value) {
         ds->bvh32 = reinterpret_cast<const rtw::BvhNode<float>*>(base + o_nodes32);
         ds->bsph32 = reinterpret_cast<const rtw::R4<float>*>(base + o_bsph32);
+        ds->lg_sph32 = reinterpret_cast<const rtw::R4<float>*>(base + o_lgsph32);
     }
     ds->bsph = reinterpret_cast<const R4*>(base + o_bsph);
     ds->bid = reinterpret_cast<const uint32_t*>(base + o_bid);
@@ -1570,6 +1579,7 @@ static int upload_scene(rtw_ctx* c, const rtw_scene* s, const std::vector<unsign
         if constexpr (std::is_same<std::decay_t<decltype(ds)>, rtw::DevScene<double>>::value) {
             fix(ds.bvh32);
             fix(ds.bsph32);
+            fix(ds.lg_sph32);
         }
         fix(ds.boxes); fix(ds.box_mat);
         if (ds.mat_tex) fix(ds.mat_tex);

@@ -1790,37 +1790,73 @@ __device__ __forceinline__ double lights_pdf_grid(const DevScene<double>& sc, V3
     });
 }
 
-// lights_pdf_grid (f64) by the whole wave: the pieces of
-// lights_pdf_grid_coop (the same cut of each pending ray's grid interval into
-// k = ceil(cells / P) pieces, dealt to the 64 lanes), each piece walking its
-// cells in f64 exactly as lights_pdf_grid does -- pre-pass, f64 sphere test,
-// the closest-approach cell rule, so every hit light is found by exactly one
-// piece.  The sum must run in LIST order (lights_sum_in_list_order), so it
-// goes in passes over list indices >= lo: a piece keeps the kPieceIds
-// smallest indices >= lo it finds, sorted, in its LDS slot ([count, ids]);
-// each owner merges its pieces' indices and the big list's into its kMax
-// smallest.  Every index up to `bound` is then known -- bound = the largest
-// kept index of a piece or an owner list that had to drop some, else
-// unbounded -- so the owner sums those pdfs in order and, when something was
-// dropped, the wave walks again for its rays with lo = bound + 1 (each pass
-// sums at least one index: the walk always ends).  A ray skimming C5's light
-// layer (~10 hits) takes two passes; the walk never falls back to one lane.
-// Bit-identical to lights_pdf_grid.  Every lane of the wave calls this
+// lights_pdf_grid (f64) by the whole wave.  The sum needs the SET of lights
+// the f64 test hits, summed in LIST order; which structure finds them is free.
+// So the walk runs in f32 -- the f32 kernels' piece cut (lights_pdf_grid_coop:
+// each pending ray's grid interval cut into k = ceil(cells / P) pieces of
+// equal length in t, dealt to the 64 lanes), on the f32 copy of the grid
+// (DevScene::lg_sph32 and the grid box rounded to f32) -- and a light of a
+// visited cell is a candidate when the f64 path's f32 pre-pass (LightPre /
+// light_may_hit: slack far above the f32 error) says the ray may hit it and
+// its f32 closest-approach parameter falls in the cell's interval: every light
+// the f64 test hits is a candidate exactly once (the intervals partition the
+// line; the host pads the cells' lists beyond the f32 rounding).  The owner
+// sums Sphere::pdf_value over its candidates in list order, in f64 (a
+// candidate the f64 test misses adds +0.0: no bit changes).  In passes over
+// list indices >= lo: a piece keeps the kPieceIds smallest candidate indices
+// >= lo it finds, sorted, in its LDS slot ([count, ids]); each owner merges
+// its pieces' indices and the big list's into its kMax smallest; every index
+// up to `bound` -- the largest kept index of a piece or an owner list that
+// had to drop some, else unbounded -- is then known, so the owner sums those
+// and, when something was dropped, the wave walks again for its rays with
+// lo = bound + 1 (each pass sums at least one index: the walk always ends).
+// Bit-identical to lights_pdf_grid and the linear list-order sum.  (Round 4
+// walked in f64 -- f64 DDA, f64 records, the f64 test in the piece: C3 / C5
+// spilled the path state at every trip.)  Every lane of the wave calls this
 // (converged), with wave-uniform P; `cap_words` (a multiple of 64) of LDS at
 // `slots`.
-__device__ __forceinline__ double lights_pdf_grid_coop64(const DevScene<double>& sc, bool pend, V3<double> o,
-                                                         V3<double> d, uint32_t P, uint32_t* __restrict__ slots,
-                                                         uint32_t cap_words, uint32_t lane, LightWork& lw) {
+// The pending f64 ray (o, d) is read from the wave's LDS stash (`ray`: words
+// [(2k) 64 + lane], [(2k + 1) 64 + lane] for k = 0..5, the kernel's layout)
+// where it is needed -- the f32 ray at the start of a pass, the pdfs at its
+// end -- so it is not held in registers across the walk's rounds.
+__device__ __forceinline__ double lights_pdf_grid_coop64(const DevScene<double>& sc, bool pend,
+                                                         const uint32_t* __restrict__ ray, uint32_t P,
+                                                         uint32_t* __restrict__ slots, uint32_t cap_words,
+                                                         uint32_t lane, LightWork& lw) {
     constexpr uint32_t kPieceIds = kCoop64PieceIds, kSlot = kPieceIds + 1, kMax = RTW_COOP64_MAX;
+    auto ray_at = [&](uint32_t q) {
+        return __longlong_as_double((long long)((uint64_t)ray[(2 * q) * 64 + lane] |
+                                                ((uint64_t)ray[(2 * q + 1) * 64 + lane] << 32)));
+    };
+    auto ray_o = [&]() { return mk(ray_at(0), ray_at(1), ray_at(2)); };
+    auto ray_d = [&]() { return mk(ray_at(3), ray_at(4), ray_at(5)); };
     const uint32_t cap = cap_words / (kSlot * 64) * 64;   // pieces per round
     // (the host sizes the stack area for at least one round of 64 pieces; a
     // smaller area takes the per-lane walk -- never a loop that cannot advance)
-    if (cap == 0) return pend ? lights_pdf_grid<false>(sc, o, d, lw) : 0.0;
-    double tn = 0.0, tf = 0.0;
+    if (cap == 0) return pend ? lights_pdf_grid<false>(sc, ray_o(), ray_d(), lw) : 0.0;
+    // the grid in f32 (only the fields the walk reads)
+    DevScene<float> g;
+    g.lg_start = sc.lg_start;
+    g.lg_sph = sc.lg_sph32;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        g.lg_lo[a] = (float)sc.lg_lo[a];
+        g.lg_hi[a] = (float)sc.lg_hi[a];
+        g.lg_cell[a] = (float)sc.lg_cell[a];
+        g.lg_inv[a] = (float)sc.lg_inv[a];
+        g.lg_n[a] = sc.lg_n[a];
+    }
+    V3<float> of, df;           // the f32 ray
+    {
+        const LightPre pre(ray_o(), ray_d());
+        of = mk(pre.ox, pre.oy, pre.oz);
+        df = mk(pre.dx, pre.dy, pre.dz);
+    }
+    float tn = 0.f, tf = 0.f;
     uint32_t k = 0;
     if (pend) {
         uint32_t cells = 0;
-        if (light_grid_span(sc, o, d, grid_inv(d.x), grid_inv(d.y), grid_inv(d.z), tn, tf, cells))
+        if (light_grid_span(g, of, df, grid_inv(df.x), grid_inv(df.y), grid_inv(df.z), tn, tf, cells))
             k = (cells + P - 1u) / P;
     }
     double acc = 0.0;
@@ -1844,14 +1880,15 @@ __device__ __forceinline__ double lights_pdf_grid_coop64(const DevScene<double>&
             ids[q] = id;
             ++n;
         };
-        if (more) {
-            const LightPre pre(o, d);
+        if (more && sc.lg_big) {
             lw.tests += sc.lg_big;
+            const float ia = __builtin_amdgcn_rcpf(__builtin_fmaf(df.x, df.x, __builtin_fmaf(df.y, df.y, df.z * df.z)));
+            const float on = fabsf(of.x) + fabsf(of.y) + fabsf(of.z), dn = fabsf(df.x) + fabsf(df.y) + fabsf(df.z);
             for (uint32_t q = 0; q < sc.lg_big; ++q) {
-                const R4<double> L = sc.lg_sph[q];
-                double t;
+                const R4<float> L = g.lg_sph[q];
                 const uint32_t id = sc.lg_id[q];
-                if (id >= lo && pre.may_hit(L) && sphere_t(mk(L.x, L.y, L.z), L.w * L.w, o, d, 0.0, t)) add(id);
+                if (id >= lo && light_may_hit(L.x, L.y, L.z, L.w, of.x, of.y, of.z, df.x, df.y, df.z, ia, on, dn))
+                    add(id);
             }
         }
         const uint32_t kp = more ? k : 0u;   // this pass's pieces
@@ -1865,36 +1902,37 @@ __device__ __forceinline__ double lights_pdf_grid_coop64(const DevScene<double>&
         for (uint32_t b = 0; b < total; b += cap) {
             const uint32_t e = min(b + cap, total);
             for (uint32_t r = b; r < e; r += 64) {
-                const uint32_t g = r + lane;
+                const uint32_t gi = r + lane;
                 uint32_t own = 0;
 #pragma unroll
                 for (uint32_t step = 32; step; step >>= 1) {
                     const uint32_t f = (uint32_t)__shfl((int)first, (int)(own + step));
-                    own = f <= g ? own + step : own;
+                    own = f <= gi ? own + step : own;
                 }
-                const V3<double> ro = mk(bperm_d(o.x, own), bperm_d(o.y, own), bperm_d(o.z, own));
-                const V3<double> rd = mk(bperm_d(d.x, own), bperm_d(d.y, own), bperm_d(d.z, own));
-                const double rtn = bperm_d(tn, own), rtf = bperm_d(tf, own);
+                const V3<float> ro = mk(bperm_f(of.x, own), bperm_f(of.y, own), bperm_f(of.z, own));
+                const V3<float> rd = mk(bperm_f(df.x, own), bperm_f(df.y, own), bperm_f(df.z, own));
+                const float rtn = bperm_f(tn, own), rtf = bperm_f(tf, own);
                 const uint32_t rk = (uint32_t)bperm_i((int32_t)kp, own), rfirst = (uint32_t)bperm_i((int32_t)first, own);
                 const uint32_t rlo = (uint32_t)bperm_i((int32_t)lo, own);
-                if (g < e) {
-                    const uint32_t j = g - rfirst;
-                    const double step = (rtf - rtn) / (double)rk;
-                    auto t_at = [&](uint32_t q) { return q == 0 ? rtn : (double)q * step + rtn; };
-                    const LightPre rpre(ro, rd);
-                    const double ria = 1.0 / (rd.x * rd.x + rd.y * rd.y + rd.z * rd.z);
-                    uint32_t* ent = slots + (g - b) * kSlot + 1;
+                if (gi < e) {
+                    const uint32_t j = gi - rfirst;
+                    const float step = (rtf - rtn) / (float)rk;
+                    auto t_at = [&](uint32_t q) { return q == 0 ? rtn : __builtin_fmaf((float)q, step, rtn); };
+                    // the owner's LightPre quantities, recomputed from the same f32 ray
+                    const float ria = __builtin_amdgcn_rcpf(__builtin_fmaf(rd.x, rd.x, __builtin_fmaf(rd.y, rd.y, rd.z * rd.z)));
+                    const float ron = fabsf(ro.x) + fabsf(ro.y) + fabsf(ro.z), rdn = fabsf(rd.x) + fabsf(rd.y) + fabsf(rd.z);
+                    uint32_t* ent = slots + (gi - b) * kSlot + 1;
                     uint32_t cnt = 0;
-                    light_grid_walk_piece(sc, ro, rd, grid_inv(rd.x), grid_inv(rd.y), grid_inv(rd.z), t_at(j),
-                                          t_at(j + 1), j == 0, j + 1 == rk, [&](uint32_t q, double te, double tx) {
+                    light_grid_walk_piece(g, ro, rd, grid_inv(rd.x), grid_inv(rd.y), grid_inv(rd.z), t_at(j),
+                                          t_at(j + 1), j == 0, j + 1 == rk, [&](uint32_t q, float te, float tx) {
                         ++lw.tests;
-                        const R4<double> L = sc.lg_sph[q];
-                        double t;
-                        if (rpre.may_hit(L) && sphere_t(mk(L.x, L.y, L.z), L.w * L.w, ro, rd, 0.0, t)) {
-                            const double tc = -((ro.x - L.x) * rd.x + (ro.y - L.y) * rd.y + (ro.z - L.z) * rd.z) * ria;
+                        const R4<float> L = g.lg_sph[q];
+                        if (light_may_hit(L.x, L.y, L.z, L.w, ro.x, ro.y, ro.z, rd.x, rd.y, rd.z, ria, ron, rdn)) {
+                            const float tc = -__builtin_fmaf(rd.z, ro.z - L.z, __builtin_fmaf(rd.y, ro.y - L.y,
+                                                                                               rd.x * (ro.x - L.x))) * ria;
                             const uint32_t id = sc.lg_id[q];
                             if (tc >= te && tc < tx && id >= rlo) {
-                                // the piece's kPieceIds smallest, sorted (rare: a hit)
+                                // the piece's kPieceIds smallest, sorted (rare: a candidate)
                                 uint32_t m = min(cnt, kPieceIds);
                                 ++cnt;
                                 if (m == kPieceIds) {
@@ -1917,8 +1955,8 @@ __device__ __forceinline__ double lights_pdf_grid_coop64(const DevScene<double>&
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             if (kp) {
                 const uint32_t g0 = max(first, b), g1 = min(first + kp, e);
-                for (uint32_t g = g0; g < g1; ++g) {
-                    const uint32_t* ent = slots + (g - b) * kSlot + 1;
+                for (uint32_t gi = g0; gi < g1; ++gi) {
+                    const uint32_t* ent = slots + (gi - b) * kSlot + 1;
                     const uint32_t cnt = ent[-1];
                     for (uint32_t q = 0; q < min(cnt, kPieceIds); ++q) add(ent[q]);
                     if (cnt > kPieceIds) bound = min(bound, ent[kPieceIds - 1]);
@@ -1930,6 +1968,7 @@ __device__ __forceinline__ double lights_pdf_grid_coop64(const DevScene<double>&
         }
         if (more) {
             if (dropped) bound = min(bound, ids[kMax - 1]);
+            const V3<double> o = ray_o(), d = ray_d();
             for (uint32_t q = 0; q < n; ++q) {
                 if (ids[q] > bound) break;
                 const R4<double> L = sc.lights[ids[q]];
@@ -2929,7 +2968,8 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                 R acc;
                 LightWork lw;
                 if constexpr (sizeof(R) == 8) {
-                    acc = lights_pdf_grid_coop64(p.sc, pend, po, pd, kargs()->grid_piece, area + kStash * 64,
+                    // (the pending ray: stash words 4..9, put above)
+                    acc = lights_pdf_grid_coop64(p.sc, pend, area + 8 * 64, kargs()->grid_piece, area + kStash * 64,
                                                  (p.stack - kStash) * 64, lane, lw);
                 } else {
                     float* slots = reinterpret_cast<float*>(area + kStash * 64);

@@ -84,6 +84,7 @@ template <>
 struct DevSceneCull<double> {
     const BvhNode<float>* bvh32;
     const R4<float>* bsph32;          // bsph rounded to f32 {c, r^2}: the leaf pre-pass
+    const R4<float>* lg_sph32;        // lg_sph rounded to f32 {c, |r|}: the light grid's f32 walk
 };
 
 template <typename R>
