@@ -236,3 +236,25 @@ def test_kernel_isa_identity_covers_every_render_kernel_variant():
     assert name == "void rtw::dev::render_kernel<float, 5, 16>(rtw::KParams<float>)"
     assert isa.demangled_to_symbol(name) == isa.render_kernel_symbol("f32", 5, 16)
     assert isa.kernel_isa_sha("_ZN3rtw3dev13no_such_kernelEv") is None
+
+
+def test_device_list_arguments_refused_before_any_hip_call():
+    """ABI 9: rtw_create_virtual / rtw_create_mask_ex / rtw_create_devices
+    reject bad arguments with RTW_E_INVALID before touching HIP (no GPU
+    here); rtw_visible_devices reports no device (or a HIP error) on this host."""
+    lib = rtw._lib
+    out = C.c_void_p()
+    inv = _capi.RTW_E_INVALID
+    assert lib.rtw_create_virtual(0, 0, _capi.RTW_F64, C.byref(out)) == inv          # no ranks
+    assert lib.rtw_create_virtual(-1, 2, _capi.RTW_F64, C.byref(out)) == inv         # negative device
+    assert lib.rtw_create_virtual(0, 2, 7, C.byref(out)) == inv                      # bad precision
+    assert lib.rtw_create_virtual(0, 65, _capi.RTW_F64, C.byref(out)) == inv         # more ranks than the ABI allows
+    assert lib.rtw_create_virtual(0, 2, _capi.RTW_F64, None) == inv
+    assert lib.rtw_create_mask_ex(0, _capi.RTW_F64, C.byref(out)) == inv             # empty mask
+    assert lib.rtw_create_mask_ex(1, 7, C.byref(out)) == inv
+    devs = (C.c_int * 2)(0, 0)
+    assert lib.rtw_create_devices(devs, 2, _capi.RTW_F64, C.byref(out)) == inv       # repeated device
+    assert out.value is None
+    assert lib.rtw_visible_devices() <= 0
+    st = _capi.rtw_stats()
+    assert lib.rtw_get_stats_rank(None, 0, C.byref(st)) == inv
