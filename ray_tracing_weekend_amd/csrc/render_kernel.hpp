@@ -783,6 +783,29 @@ __device__ __forceinline__ float cull_bound(double t) {   // t rounded up to f32
     const float f = (float)t;
     return (double)f < t ? __uint_as_float(__float_as_uint(f) + 1u) : f;   // t > 0
 }
+// RTW_NT_NODES (experiment): the while-while traversal's node loads non-temporal
+// (trees outside LDS: C3 / C5), so that streaming a large tree through L2 does
+// not evict the light grid the walk reads
+#ifndef RTW_NT_NODES
+#define RTW_NT_NODES 0
+#endif
+__device__ __forceinline__ BvhNode<float> load_node(const BvhNode<float>* __restrict__ nodes, int32_t i) {
+    if constexpr (RTW_NT_NODES != 0) {
+        static_assert(sizeof(BvhNode<float>) == 64, "node = 4 x 16 B");
+        typedef float f4v __attribute__((ext_vector_type(4)));
+        const f4v* q = reinterpret_cast<const f4v*>(nodes + i);
+        const f4v a = __builtin_nontemporal_load(q), b = __builtin_nontemporal_load(q + 1),
+                  c = __builtin_nontemporal_load(q + 2), e = __builtin_nontemporal_load(q + 3);
+        BvhNode<float> n;
+        n.lo_x[0] = a.x; n.lo_x[1] = a.y; n.lo_y[0] = a.z; n.lo_y[1] = a.w;
+        n.lo_z[0] = b.x; n.lo_z[1] = b.y; n.hi_x[0] = b.z; n.hi_x[1] = b.w;
+        n.hi_y[0] = c.x; n.hi_y[1] = c.y; n.hi_z[0] = c.z; n.hi_z[1] = c.w;
+        n.child[0] = __float_as_int(e.x); n.child[1] = __float_as_int(e.y);
+        return n;
+    } else {
+        return nodes[i];
+    }
+}
 template <typename R, typename TT>
 __device__ __forceinline__ void bvh_traverse_ww(const DevScene<R>& sc, int32_t base, V3<R> o, V3<R> d,
                                                 TT& T, int32_t* __restrict__ stk,
@@ -815,7 +838,7 @@ __device__ __forceinline__ void bvh_traverse_ww(const DevScene<R>& sc, int32_t b
             if (inner) {
                 RTW_PROBE_LANES(1);
                 ++nvis;
-                const BvhNode<float>& nd = nodes[node];
+                const BvhNode<float> nd = load_node(nodes, node);
                 const float tb = kWide ? tbw : (float)T.bound();
                 float tn[2], tf[2];
 #pragma unroll
@@ -1856,42 +1879,18 @@ __device__ __forceinline__ double lights_pdf_grid_coop64(const DevScene<double>&
     uint32_t k = 0;
     if (pend) {
         uint32_t cells = 0;
+        // at most `cap` pieces (longer pieces for a longer ray): every ray's
+        // pieces fit one round, so its owner finds all of them in the slots
         if (light_grid_span(g, of, df, grid_inv(df.x), grid_inv(df.y), grid_inv(df.z), tn, tf, cells))
-            k = (cells + P - 1u) / P;
+            k = min((cells + P - 1u) / P, cap);
     }
+    const uint32_t ia_bits = __float_as_uint(
+        __builtin_amdgcn_rcpf(__builtin_fmaf(df.x, df.x, __builtin_fmaf(df.y, df.y, df.z * df.z))));
     double acc = 0.0;
     uint32_t lo = 0;
-    bool more = pend;
+    bool more = pend;           // the ray still needs a walk (over list indices >= lo)
     while (__any(more)) {
-        uint32_t ids[kMax];
-        uint32_t n = 0, bound = 0xffffffffu;
-        bool dropped = false;
-        auto add = [&](uint32_t id) {   // the kMax smallest list indices (lights_sum_in_list_order)
-            if (n == kMax) {
-                dropped = true;
-                if (id > ids[kMax - 1]) return;
-                --n;
-            }
-            uint32_t q = n;
-            while (q > 0 && ids[q - 1] > id) {
-                ids[q] = ids[q - 1];
-                --q;
-            }
-            ids[q] = id;
-            ++n;
-        };
-        if (more && sc.lg_big) {
-            lw.tests += sc.lg_big;
-            const float ia = __builtin_amdgcn_rcpf(__builtin_fmaf(df.x, df.x, __builtin_fmaf(df.y, df.y, df.z * df.z)));
-            const float on = fabsf(of.x) + fabsf(of.y) + fabsf(of.z), dn = fabsf(df.x) + fabsf(df.y) + fabsf(df.z);
-            for (uint32_t q = 0; q < sc.lg_big; ++q) {
-                const R4<float> L = g.lg_sph[q];
-                const uint32_t id = sc.lg_id[q];
-                if (id >= lo && light_may_hit(L.x, L.y, L.z, L.w, of.x, of.y, of.z, df.x, df.y, df.z, ia, on, dn))
-                    add(id);
-            }
-        }
-        const uint32_t kp = more ? k : 0u;   // this pass's pieces
+        const uint32_t kp = more ? k : 0u;   // this walk's pieces
         uint32_t incl = kp;
 #pragma unroll
         for (uint32_t off = 1; off < 64; off <<= 1) {
@@ -1899,9 +1898,15 @@ __device__ __forceinline__ double lights_pdf_grid_coop64(const DevScene<double>&
             if (lane >= off) incl += v;
         }
         const uint32_t first = incl - kp, total = (uint32_t)__shfl((int)incl, 63);
-        for (uint32_t b = 0; b < total; b += cap) {
-            const uint32_t e = min(b + cap, total);
-            for (uint32_t r = b; r < e; r += 64) {
+        bool walk_again = false;
+        // rounds of whole rays: [B, Bn) holds the pieces of the rays that start
+        // at B or later and end by B + cap (a pending ray without pieces -- it
+        // misses the grid -- sums its big-list candidates in the first round)
+        for (uint32_t B = 0;;) {
+            const bool mine = more && (kp ? first >= B && first + kp <= B + cap : B == 0);   // the ray is in the round
+            const uint64_t later = __ballot(kp && first >= B && !mine);
+            const uint32_t Bn = later ? (uint32_t)__shfl((int)first, (int)__builtin_ctzll(later)) : total;
+            for (uint32_t r = B; r < Bn; r += 64) {
                 const uint32_t gi = r + lane;
                 uint32_t own = 0;
 #pragma unroll
@@ -1914,14 +1919,14 @@ __device__ __forceinline__ double lights_pdf_grid_coop64(const DevScene<double>&
                 const float rtn = bperm_f(tn, own), rtf = bperm_f(tf, own);
                 const uint32_t rk = (uint32_t)bperm_i((int32_t)kp, own), rfirst = (uint32_t)bperm_i((int32_t)first, own);
                 const uint32_t rlo = (uint32_t)bperm_i((int32_t)lo, own);
-                if (gi < e) {
+                const float ria = __uint_as_float((uint32_t)bperm_i((int32_t)ia_bits, own));
+                if (gi < Bn) {
                     const uint32_t j = gi - rfirst;
                     const float step = (rtf - rtn) / (float)rk;
                     auto t_at = [&](uint32_t q) { return q == 0 ? rtn : __builtin_fmaf((float)q, step, rtn); };
-                    // the owner's LightPre quantities, recomputed from the same f32 ray
-                    const float ria = __builtin_amdgcn_rcpf(__builtin_fmaf(rd.x, rd.x, __builtin_fmaf(rd.y, rd.y, rd.z * rd.z)));
+                    // the owner's LightPre quantities, from the same f32 ray
                     const float ron = fabsf(ro.x) + fabsf(ro.y) + fabsf(ro.z), rdn = fabsf(rd.x) + fabsf(rd.y) + fabsf(rd.z);
-                    uint32_t* ent = slots + (gi - b) * kSlot + 1;
+                    uint32_t* ent = slots + (gi - B) * kSlot + 1;
                     uint32_t cnt = 0;
                     light_grid_walk_piece(g, ro, rd, grid_inv(rd.x), grid_inv(rd.y), grid_inv(rd.z), t_at(j),
                                           t_at(j + 1), j == 0, j + 1 == rk, [&](uint32_t q, float te, float tx) {
@@ -1953,30 +1958,74 @@ __device__ __forceinline__ double lights_pdf_grid_coop64(const DevScene<double>&
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            if (kp) {
-                const uint32_t g0 = max(first, b), g1 = min(first + kp, e);
-                for (uint32_t gi = g0; gi < g1; ++gi) {
-                    const uint32_t* ent = slots + (gi - b) * kSlot + 1;
-                    const uint32_t cnt = ent[-1];
-                    for (uint32_t q = 0; q < min(cnt, kPieceIds); ++q) add(ent[q]);
-                    if (cnt > kPieceIds) bound = min(bound, ent[kPieceIds - 1]);
+            if (mine) {
+                // every candidate >= lo of this ray is in its pieces' slots (and the
+                // big list) unless a piece kept only its kPieceIds smallest: merge
+                // the kMax smallest, sum them in list order, and merge again above
+                // the last one summed until done -- or until a piece's dropped
+                // candidates are needed, which takes another walk
+                const float ia = __uint_as_float(ia_bits);
+                const float on = fabsf(of.x) + fabsf(of.y) + fabsf(of.z), dn = fabsf(df.x) + fabsf(df.y) + fabsf(df.z);
+                for (;;) {
+                    uint32_t ids[kMax];
+                    uint32_t n = 0, bp = 0xffffffffu;   // bp: below a piece's dropped candidates
+                    bool dropped = false;
+                    auto add = [&](uint32_t id) {   // the kMax smallest list indices (lights_sum_in_list_order)
+                        if (n == kMax) {
+                            dropped = true;
+                            if (id > ids[kMax - 1]) return;
+                            --n;
+                        }
+                        uint32_t q = n;
+                        while (q > 0 && ids[q - 1] > id) {
+                            ids[q] = ids[q - 1];
+                            --q;
+                        }
+                        ids[q] = id;
+                        ++n;
+                    };
+                    if (sc.lg_big) {
+                        lw.tests += sc.lg_big;
+                        for (uint32_t q = 0; q < sc.lg_big; ++q) {
+                            const R4<float> L = g.lg_sph[q];
+                            const uint32_t id = sc.lg_id[q];
+                            if (id >= lo && light_may_hit(L.x, L.y, L.z, L.w, of.x, of.y, of.z, df.x, df.y, df.z, ia,
+                                                          on, dn))
+                                add(id);
+                        }
+                    }
+                    for (uint32_t gi = first; gi < first + kp; ++gi) {
+                        const uint32_t* ent = slots + (gi - B) * kSlot + 1;
+                        const uint32_t cnt = ent[-1];
+                        for (uint32_t q = 0; q < min(cnt, kPieceIds); ++q)
+                            if (ent[q] >= lo) add(ent[q]);
+                        if (cnt > kPieceIds) bp = min(bp, ent[kPieceIds - 1]);
+                    }
+                    const uint32_t bound = dropped ? min(bp, ids[kMax - 1]) : bp;
+                    const V3<double> o = ray_o(), d = ray_d();
+                    for (uint32_t q = 0; q < n; ++q) {
+                        if (ids[q] > bound) break;
+                        const R4<double> L = sc.lights[ids[q]];
+                        acc = acc + sphere_pdf_value(mk(L.x, L.y, L.z), L.w, o, d);
+                    }
+                    if (bound == 0xffffffffu) {
+                        more = false;                       // every candidate summed
+                        break;
+                    }
+                    lo = bound + 1u;
+                    if (bound == bp) {                      // a piece's dropped candidates are next
+                        walk_again = true;
+                        break;
+                    }
                 }
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            B = Bn;
+            if (B >= total) break;
         }
-        if (more) {
-            if (dropped) bound = min(bound, ids[kMax - 1]);
-            const V3<double> o = ray_o(), d = ray_d();
-            for (uint32_t q = 0; q < n; ++q) {
-                if (ids[q] > bound) break;
-                const R4<double> L = sc.lights[ids[q]];
-                acc = acc + sphere_pdf_value(mk(L.x, L.y, L.z), L.w, o, d);
-            }
-            more = bound != 0xffffffffu;
-            lo = bound + 1u;
-        }
+        more = more && walk_again;
     }
     return acc;
 }

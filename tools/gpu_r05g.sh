@@ -7,4 +7,4 @@ for v in tree lamb64; do
   timeout -k 10 200 python tools/sweep.py --precision f32 --grid "hit64=1" --rounds 3 >> $OUT/sweep_r05g_$v.log 2>&1 || exit $?
   echo "$v done"
 done
-bash tools/gpu_ab_walk.sh old cmax12 cmax16
+
