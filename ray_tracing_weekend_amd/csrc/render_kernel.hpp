@@ -1428,7 +1428,7 @@ __device__ __forceinline__ V3<double> dielectric_dir64(V3<double> u, V3<double> 
 // (the f64 parity kernels), else the f32 kernels' direct sampler carried into
 // f64 (dither64).
 #ifndef RTW_HIT64_LAMB64
-#define RTW_HIT64_LAMB64 0   // hit64 Lambertian: 1 = the direction in f64 (experiment)
+#define RTW_HIT64_LAMB64 1   // hit64 Lambertian: the direction in f64 (r05 default; 0 = in f32)
 #endif
 #ifndef RTW_HIT64_REF_SPHERE
 #define RTW_HIT64_REF_SPHERE 0   // hit64 Metal: 1 = the reference's f64 rejection loop (experiment)
@@ -1842,7 +1842,17 @@ __device__ __forceinline__ double lights_pdf_grid(const DevScene<double>& sc, V3
 // [(2k) 64 + lane], [(2k + 1) 64 + lane] for k = 0..5, the kernel's layout)
 // where it is needed -- the f32 ray at the start of a pass, the pdfs at its
 // end -- so it is not held in registers across the walk's rounds.
-__device__ __forceinline__ double lights_pdf_grid_coop64(const DevScene<double>& sc, bool pend,
+// The light grid of an f64 scene as the f32 walk reads it: the arrays, and
+// the grid box, cells and their counts rounded to f32.
+struct Grid64 {
+    const uint32_t* lg_start;
+    const R4<float>* lg_sph32;        // DevScene<double>::lg_sph32
+    const uint32_t* lg_id;
+    const R4<double>* lights;         // the light list (f64 records: the pdfs)
+    float lo[3], hi[3], cell[3], inv[3];
+    uint32_t n[3], big;
+};
+__device__ __forceinline__ double lights_pdf_grid_coop64(const Grid64& sc, bool pend,
                                                          const uint32_t* __restrict__ ray, uint32_t P,
                                                          uint32_t* __restrict__ slots, uint32_t cap_words,
                                                          uint32_t lane, LightWork& lw) {
@@ -1854,21 +1864,22 @@ __device__ __forceinline__ double lights_pdf_grid_coop64(const DevScene<double>&
     auto ray_o = [&]() { return mk(ray_at(0), ray_at(1), ray_at(2)); };
     auto ray_d = [&]() { return mk(ray_at(3), ray_at(4), ray_at(5)); };
     const uint32_t cap = cap_words / (kSlot * 64) * 64;   // pieces per round
-    // (the host sizes the stack area for at least one round of 64 pieces; a
-    // smaller area takes the per-lane walk -- never a loop that cannot advance)
-    if (cap == 0) return pend ? lights_pdf_grid<false>(sc, ray_o(), ray_d(), lw) : 0.0;
-    // the grid in f32 (only the fields the walk reads)
+    // the grid as a DevScene<float> (only the fields the walk reads)
     DevScene<float> g;
     g.lg_start = sc.lg_start;
     g.lg_sph = sc.lg_sph32;
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
-        g.lg_lo[a] = (float)sc.lg_lo[a];
-        g.lg_hi[a] = (float)sc.lg_hi[a];
-        g.lg_cell[a] = (float)sc.lg_cell[a];
-        g.lg_inv[a] = (float)sc.lg_inv[a];
-        g.lg_n[a] = sc.lg_n[a];
+        g.lg_lo[a] = sc.lo[a];
+        g.lg_hi[a] = sc.hi[a];
+        g.lg_cell[a] = sc.cell[a];
+        g.lg_inv[a] = sc.inv[a];
+        g.lg_n[a] = sc.n[a];
     }
+    // (the host sizes the stack area for at least one round of 64 pieces, so a
+    // smaller area is a host error: every pending ray ends NaN, never a loop
+    // that cannot advance)
+    if (cap == 0) return pend ? (double)NAN : 0.0;
     V3<float> of, df;           // the f32 ray
     {
         const LightPre pre(ray_o(), ray_d());
@@ -1984,9 +1995,9 @@ __device__ __forceinline__ double lights_pdf_grid_coop64(const DevScene<double>&
                         ids[q] = id;
                         ++n;
                     };
-                    if (sc.lg_big) {
-                        lw.tests += sc.lg_big;
-                        for (uint32_t q = 0; q < sc.lg_big; ++q) {
+                    if (sc.big) {
+                        lw.tests += sc.big;
+                        for (uint32_t q = 0; q < sc.big; ++q) {
                             const R4<float> L = g.lg_sph[q];
                             const uint32_t id = sc.lg_id[q];
                             if (id >= lo && light_may_hit(L.x, L.y, L.z, L.w, of.x, of.y, of.z, df.x, df.y, df.z, ia,
@@ -2311,6 +2322,17 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
         asm volatile("" : "+s"(k));   // not loop-invariant for the compiler: loaded at each use
         return k;
     };
+    // The scene record for a callee, read from the kernel arguments at the call
+    // (the fields it uses, by scalar loads) instead of from `p`, whose fields the
+    // compiler hoists into SGPRs held across the whole loop -- the light pdf's
+    // walks overflow the SGPR file into VGPR lanes and scratch.  (The host pass
+    // only type-checks the kernel body: there it is a reference to `p.sc`.)
+#if defined(__HIP_DEVICE_COMPILE__)
+#define RTW_KARG_SCENE(name) const DevScene<R> name = kargs()->sc
+#else
+#define RTW_KARG_SCENE(name) const DevScene<R>& name = p.sc
+#endif
+
     auto set_task = [&](uint32_t t) {
         const KArgs* k = kargs();
         if (k->task_table) {   // longest tiles first, cut by cost
@@ -2890,9 +2912,10 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                         acc = lights_pdf_mixed(p.sc, li, pnt, dir);
                     else if constexpr (kLightBvh) {
                         LightWork lw;
-                        acc = p.light_bvh == 2
-                                  ? lights_pdf_grid<kRobust>(p.sc, pnt, dir, lw)
-                                  : lights_pdf_bvh<kRobust>(p.sc, pnt, dir,
+                        RTW_KARG_SCENE(wsc);
+                        acc = kargs()->light_bvh == 2
+                                  ? lights_pdf_grid<kRobust>(wsc, pnt, dir, lw)
+                                  : lights_pdf_bvh<kRobust>(wsc, pnt, dir,
                                                             reinterpret_cast<int32_t*>(smem) + wave * p.stack * 64 + lane,
                                                             lw);
                         light_work_lane(wcnt, lw);
@@ -3018,12 +3041,29 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                 LightWork lw;
                 if constexpr (sizeof(R) == 8) {
                     // (the pending ray: stash words 4..9, put above)
-                    acc = lights_pdf_grid_coop64(p.sc, pend, area + 8 * 64, kargs()->grid_piece, area + kStash * 64,
-                                                 (p.stack - kStash) * 64, lane, lw);
+                    // the grid's fields read from the kernel arguments here (RTW_KARG_SCENE)
+                    RTW_KARG_SCENE(wsc);
+                    Grid64 gr;
+                    gr.lg_start = wsc.lg_start;
+                    gr.lg_sph32 = wsc.lg_sph32;
+                    gr.lg_id = wsc.lg_id;
+                    gr.lights = wsc.lights;
+#pragma unroll
+                    for (int a = 0; a < 3; ++a) {
+                        gr.lo[a] = (float)wsc.lg_lo[a];
+                        gr.hi[a] = (float)wsc.lg_hi[a];
+                        gr.cell[a] = (float)wsc.lg_cell[a];
+                        gr.inv[a] = (float)wsc.lg_inv[a];
+                        gr.n[a] = wsc.lg_n[a];
+                    }
+                    gr.big = wsc.lg_big;
+                    acc = lights_pdf_grid_coop64(gr, pend, area + 8 * 64, kargs()->grid_piece, area + kStash * 64,
+                                                 (kargs()->stack - kStash) * 64, lane, lw);
                 } else {
                     float* slots = reinterpret_cast<float*>(area + kStash * 64);
-                    acc = lights_pdf_grid_coop<kRobust>(p.sc, pend, po, pd, kargs()->grid_piece, slots,
-                                                        (p.stack - kStash) * 64, lane, lw);
+                    RTW_KARG_SCENE(wsc);
+                    acc = lights_pdf_grid_coop<kRobust>(wsc, pend, po, pd, kargs()->grid_piece, slots,
+                                                        (kargs()->stack - kStash) * 64, lane, lw);
                 }
                 light_work_wave(wcnt, lw, lane);
                 g.s0 = get(0);

@@ -6,8 +6,9 @@ f64::EPSILON (camera.rs:473) makes every bounce's self-intersection an
 ulp-level coin flip, so f32 and f64 paths part within a few bounces and a
 per-pixel comparison at a fixed seed measures Monte-Carlo noise.  The f32
 kernel therefore decides those flips in f64 (kOptHit64: f64 ray origin,
-own-sphere re-hit test, hit t and point, Metal / Dielectric directions;
-render_kernel.hpp) and the tolerance is statistical, two-sample against the
+own-sphere re-hit test, hit t and point, Metal / Dielectric directions and,
+since round 5, the Lambertian direction; render_kernel.hpp) and the
+tolerance is statistical, two-sample against the
 f64 parity mode (tests/f32_stats.py): f32 at seed X vs f64 at seed Y, the noise
 calibrated by f64 at seed Z vs f64 at seed Y.
 
@@ -15,8 +16,10 @@ STATED f32 TOLERANCE (C2, full frame, 500 spp):
   image-mean relative bias          |b| < 5e-4 and |z| < 6
   mean-square difference ratio      msd_ratio < 1.10
   per-pixel |diff| / sigma, p99      <= 1.05 x the f64 two-seed p99
-  16x16-block mean z, p99           < 8 (4e-6 relative f32 rounding floor)
-  NaN-pixel fraction                within 10 % (relative) of f64's
+  16x16-block mean z, p99           < 6 (4e-6 relative f32 rounding floor;
+                                    measured r05 5.09 vs the f64 two-seed 2.24:
+                                    VERDICT r04's 1.5 x f64 is NOT met)
+  NaN-pixel fraction                within 1 % (relative) of f64's (r05 14.68 % vs 14.67 %)
   segments per sample               within 2 % of f64's
 The f64 renders used here are pinned to the oracle bit for bit on two C2 rows
 (the f64 parity tolerance: per-pixel MAE < 1e-5, identical NaN masks).
@@ -32,7 +35,7 @@ pytestmark = pytest.mark.gpu
 
 W, H, SPP, DEPTH = 1200, 800, 500, 50
 TOL = {"mean_rel_bias": 5e-4, "mean_bias_z": 6.0, "msd_ratio": 1.10, "pixel_z_p99_ratio": 1.05,
-       "block_z_p99": 8.0, "nan_rel": 0.10, "segments_rel": 0.02}
+       "block_z_p99": 6.0, "nan_rel": 0.01, "segments_rel": 0.02}
 
 
 def _render(soa, cam, seed, prec, rows=None):
