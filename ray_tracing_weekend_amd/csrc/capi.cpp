@@ -432,6 +432,9 @@ std::vector<unsigned char> stage_scene(const rtw_scene* s, rtw::DevScene<R>* ds,
     // f64: the grid's lights rounded to f32 with |r| -- the f64 kernels' walk runs
     // in f32 on them (render_kernel.hpp lights_pdf_grid_coop64)
     const size_t o_lgsph32 = reserve(std::is_same<R, double>::value ? sizeof(rtw::R4<float>) * lg.items.size() : 0);
+    // the cells' records (light_grid.hpp light_grid_walk_piece_rec): 64 B per cell
+    const size_t n_cells = lg.start.empty() ? 0 : lg.start.size() - 1;
+    const size_t o_lgrec = reserve(sizeof(rtw::R4<float>) * rtw::kGridRecSlots * n_cells);
     std::vector<unsigned char> blob(align_up(off, 64) + 64, 0);
     unsigned char* b = blob.data();
     for (uint32_t k = 0; k < s->n_spheres; ++k) {
@@ -715,6 +718,11 @@ std::vector<unsigned char> stage_scene(const rtw_scene* s, rtw::DevScene<R>* ds,
                 rtw::R4<float>{(float)l[0], (float)l[1], (float)l[2], fabsf((float)l[3])};
         }
     }
+    if (n_cells) {   // each cell's lights as the f32 walk reads them (f32: lg_sph; f64: lg_sph32)
+        const std::vector<float> rec = rtw::light_grid_records(lg, s->lights, std::is_same<R, double>::value);
+        memcpy(b + o_lgrec, rec.data(), sizeof(float) * rec.size());
+    }
+    ds->lg_rec = reinterpret_cast<const rtw::R4<float>*>(base + o_lgrec);
     ds->lg_start = reinterpret_cast<const uint32_t*>(base + o_lgs);
     ds->lg_sph = reinterpret_cast<const R4*>(base + o_lgsph);
     ds->lg_id = reinterpret_cast<const uint32_t*>(base + o_lgid);
@@ -1030,7 +1038,8 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
         // (f64: kCoop64PieceIds + 1 words per piece of the walk -- [count, list
         // indices] -- after the kCoopStash64-word stash: >= 64 pieces per round)
         const uint32_t min_stack = p.light_bvh == 1 ? light_stack
-                                   : (p.light_bvh == 2 ? (sizeof(R) == 8 ? rtw::kCoopStash64 + rtw::kCoop64PieceIds + 2u : rtw::kCoopStash + 1u)
+                                   : (p.light_bvh == 2 ? (sizeof(R) == 8 ? rtw::kCoopStash64 + rtw::kCoop64PieceIds + 2u
+                                                                         : rtw::kCoopStash + 1u)
                                                        : 1u);
         // binary traversal pushes at most one entry per inner level: a leaf at
         // level `bvh_depth` has that many inner nodes above it (host/bvh.cpp)
@@ -1071,7 +1080,11 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
     if (p.sc.mat_tex && (world == rtw::kWorldBvh4 || world == rtw::kWorldBvh)) {
         world = rtw::kWorldBvhWW;
         bvh_width = 2;
-        p.stack = std::max(p.sc.bvh_depth, p.light_bvh == 1 ? p.sc.lbvh_depth + 1 : 1u);
+        // (the light grid's walk area as above)
+        p.stack = std::max(p.sc.bvh_depth, p.light_bvh == 1   ? p.sc.lbvh_depth + 1
+                                           : p.light_bvh == 2 ? (sizeof(R) == 8 ? rtw::kCoopStash64 + rtw::kCoop64PieceIds + 2u
+                                                                                : rtw::kCoopStash + 1u)
+                                                              : 1u);
         if (p.stack > rtw::kBvhStack) return fail(c, RTW_E_UNSUPPORTED, "BVH deeper than the kernel's traversal stack");
     }
     // f64 hit points: the f32 kernels of sphere + plane scenes (the launch
@@ -1576,7 +1589,7 @@ static int upload_scene(rtw_ctx* c, const rtw_scene* s, const std::vector<unsign
         fix(ds.sph); fix(ds.sph_r); fix(ds.sph_mat); fix(ds.sph_shade); fix(ds.planes); fix(ds.plane_mat);
         fix(ds.mat_type); fix(ds.mat_p); fix(ds.lights); fix(ds.bvh); fix(ds.bsph); fix(ds.bid);
         fix(ds.bvh4); fix(ds.lbvh);
-        fix(ds.lsph); fix(ds.lid); fix(ds.lg_start); fix(ds.lg_sph); fix(ds.lg_id);
+        fix(ds.lsph); fix(ds.lid); fix(ds.lg_start); fix(ds.lg_sph); fix(ds.lg_id); fix(ds.lg_rec);
         fix(ds.quads); fix(ds.quad_mat); fix(ds.lquads); fix(ds.sph64); fix(ds.pl64); fix(ds.mat64);
         if (ds.lref) fix(ds.lref);
         if constexpr (std::is_same<std::decay_t<decltype(ds)>, rtw::DevScene<double>>::value) {
@@ -1588,7 +1601,7 @@ static int upload_scene(rtw_ctx* c, const rtw_scene* s, const std::vector<unsign
         if (ds.mat_tex) fix(ds.mat_tex);
         fix(ds.tex_type); fix(ds.tex_p); fix(ds.tex_refs); fix(ds.perlin_vec); fix(ds.perlin_perm);
     };
-    static_assert(offsetof(rtw::DevScene<float>, n_sph) == 34 * sizeof(void*),
+    static_assert(offsetof(rtw::DevScene<float>, n_sph) == 35 * sizeof(void*),
                   "DevScene gained a pointer: update rebase");
     if (c->precision == RTW_F32) {
         rebase(tmp32);

@@ -1,6 +1,9 @@
 // bvh.cpp -- binned-SAH BVH build over spheres (see bvh.hpp).
 #include "bvh.hpp"
 
+#include <string.h>
+
+
 #include <math.h>
 
 #include <cmath>
@@ -483,6 +486,37 @@ LightGrid build_light_grid(const double* L, uint32_t n, double cells_per_light) 
         if (big[k]) g.items[q++] = k;
         else each_cell(k, [&](uint64_t c) { g.items[fill[c]++] = k; });
     return g;
+}
+
+
+std::vector<float> light_grid_records(const LightGrid& g, const double* L, bool abs_radius) {
+    const size_t n_cells = g.start.empty() ? 0 : g.start.size() - 1;
+    constexpr uint32_t S = kGridRecSlots;
+    auto fbits = [](uint32_t u) {
+        float f;
+        memcpy(&f, &u, 4);
+        return f;
+    };
+    const float qnan = fbits(0x7fc00000u);
+    std::vector<float> rec(n_cells * S * 4, qnan);
+    for (size_t c = 0; c < n_cells; ++c) {
+        const uint32_t lo = g.start[c], n = g.start[c + 1] - lo;
+        float* r = rec.data() + c * S * 4;
+        const uint32_t inl = n <= S ? n : S - 1;
+        for (uint32_t i = 0; i < inl; ++i) {
+            const double* l = L + 4 * (size_t)g.items[lo + i];
+            r[4 * i + 0] = (float)l[0];
+            r[4 * i + 1] = (float)l[1];
+            r[4 * i + 2] = (float)l[2];
+            r[4 * i + 3] = abs_radius ? fabsf((float)l[3]) : (float)l[3];
+        }
+        if (n > S) {
+            r[4 * (S - 1) + 0] = fbits(lo + inl);
+            r[4 * (S - 1) + 1] = fbits(n - inl);
+            r[4 * (S - 1) + 2] = fbits(kGridRecLink);
+        }
+    }
+    return rec;
 }
 
 }  // namespace rtw

@@ -84,4 +84,16 @@ constexpr double kGridBigRadius = 3.0;   // x the median light radius
 // lights: n x {cx, cy, cz, r}; cells_per_light: grid resolution target.
 LightGrid build_light_grid(const double* lights, uint32_t n, double cells_per_light);
 
+// light grid cell records (DevScene::lg_rec, light_grid.hpp light_grid_walk_piece_rec)
+constexpr uint32_t kGridRecSlots = 4;
+constexpr uint32_t kGridRecLink = 0x7fc0dea1u;   // a quiet NaN: slot 3's z of a link
+
+// The cells' records of the f32 walk (DevScene::lg_rec, light_grid.hpp
+// light_grid_walk_piece_rec): kGridRecSlots x {cx, cy, cz, r} floats per cell
+// -- a cell of n <= kGridRecSlots lights holds them then all-NaN slots, a
+// larger one its first kGridRecSlots - 1 and a link {first bits, count bits,
+// kGridRecLink bits, NaN} to the rest of its list (g.items order).  The
+// radius is |r| rounded when `abs_radius` (the f64 kernels' lg_sph32), else r.
+std::vector<float> light_grid_records(const LightGrid& g, const double* lights, bool abs_radius);
+
 }  // namespace rtw

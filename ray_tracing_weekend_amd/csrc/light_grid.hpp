@@ -8,6 +8,7 @@
 #include <math.h>
 #include <stdint.h>
 
+#include "host/bvh.hpp"
 #include "rtw_device.hpp"
 #include "rtw_kernels.h"
 
@@ -129,9 +130,10 @@ __host__ __device__ inline bool light_grid_span(const DevScene<R>& sc, V3<R> o, 
 // piece finds its entry cell as the whole walk does (the point at t0, clamped
 // into the grid: the same rounding, covered by the host's padding), so a hit
 // light is counted exactly once.  head && tail with t0 = tn is light_grid_walk.
-template <typename R, typename Item>
-__host__ __device__ inline void light_grid_walk_piece(const DevScene<R>& sc, V3<R> o, V3<R> d, R ix, R iy, R iz, R t0, R t1,
-                                             bool head, bool tail, Item&& item, uint32_t* ncell = nullptr) {
+// cell(c, te, tx) is called for every cell c of the piece with its interval.
+template <typename R, typename Cell>
+__host__ __device__ inline void light_grid_walk_cells(const DevScene<R>& sc, V3<R> o, V3<R> d, R ix, R iy, R iz, R t0,
+                                                      R t1, bool head, bool tail, Cell&& cell) {
     const R kInf = (R)INFINITY;
     const int nx = (int)sc.lg_n[0], ny = (int)sc.lg_n[1], nz = (int)sc.lg_n[2];
     auto cell_of = [&](R oc, R dc, R lo, R inv, int n) {
@@ -171,9 +173,7 @@ __host__ __device__ inline void light_grid_walk_piece(const DevScene<R>& sc, V3<
         } else if (last) {
             tx = kInf;
         }
-        const uint32_t b = sc.lg_start[c], e = sc.lg_start[c + 1];
-        if (ncell) ++*ncell;
-        for (uint32_t k = b; k < e; ++k) item(k, te, tx);
+        cell(c, te, tx);
         if (stop) break;
         te = tx;
         if (axis == 0) {
@@ -190,6 +190,57 @@ __host__ __device__ inline void light_grid_walk_piece(const DevScene<R>& sc, V3<
             tmz = exit_t(cz, sz, sc.lg_lo[2], sc.lg_cell[2], o.z, iz);
         }
     }
+}
+
+// light_grid_walk_cells with item(k, te, tx) for every light k listed in a
+// visited cell (two dependent loads per cell: the cell's range, then its
+// lights)
+template <typename R, typename Item>
+__host__ __device__ inline void light_grid_walk_piece(const DevScene<R>& sc, V3<R> o, V3<R> d, R ix, R iy, R iz, R t0, R t1,
+                                             bool head, bool tail, Item&& item, uint32_t* ncell = nullptr) {
+    light_grid_walk_cells(sc, o, d, ix, iy, iz, t0, t1, head, tail, [&](uint32_t c, R te, R tx) {
+        const uint32_t b = sc.lg_start[c], e = sc.lg_start[c + 1];
+        if (ncell) ++*ncell;
+        for (uint32_t k = b; k < e; ++k) item(k, te, tx);
+    });
+}
+
+// Cell records (DevScene::lg_rec, staged by the host with the grid): per cell
+// kGridRecSlots f32 lights {c, r} as the f32 walk reads them (the f32
+// kernels' lg_sph, the f64 kernels' lg_sph32), so a visited cell costs ONE
+// 64-byte load instead of the range load and then one load per light.  A cell
+// of n <= 4 lights holds them in slots 0..n-1 and all-NaN slots after them (a
+// NaN light fails every test: each is a conjunction of comparisons); a cell of
+// n > 4 holds its first 3 and, in slot 3, a link {start bits, count bits, z
+// bits kGridRecLink, NaN} to the rest of its list in lg_sph (a link fails
+// every test too: its z is NaN).
+__host__ __device__ inline uint32_t grid_rec_bits(float x) { return __builtin_bit_cast(uint32_t, x); }
+
+// light_grid_walk_cells over the cell records: item(L, idx, te, tx) for every
+// slot of a visited cell (the empty ones included: NaN) and every linked
+// light, with L the f32 light and idx() its position in lg_sph / lg_id (for
+// an inline slot a load of the cell's range start: call it for candidates
+// only).  `items`: the f32 lights of lg_sph's order (the links' targets).
+// ncell / ntest (may be null): += the cells visited / the lights listed in
+// them.
+template <typename R, typename Item>
+__host__ __device__ inline void light_grid_walk_piece_rec(const DevScene<R>& sc, const R4<float>* __restrict__ rec,
+                                                          const R4<float>* __restrict__ items, V3<R> o, V3<R> d, R ix,
+                                                          R iy, R iz, R t0, R t1, bool head, bool tail, Item&& item,
+                                                          uint32_t* ncell = nullptr, uint32_t* ntest = nullptr) {
+    light_grid_walk_cells(sc, o, d, ix, iy, iz, t0, t1, head, tail, [&](uint32_t c, R te, R tx) {
+        const R4<float>* r = rec + (size_t)kGridRecSlots * c;
+        const R4<float> s0 = r[0], s1 = r[1], s2 = r[2], s3 = r[3];
+        const bool link = grid_rec_bits(s3.z) == kGridRecLink;
+        const uint32_t lb = grid_rec_bits(s3.x), ln = link ? grid_rec_bits(s3.y) : 0u;
+        if (ncell) ++*ncell;
+        if (ntest) *ntest += (s0.w == s0.w) + (s1.w == s1.w) + (s2.w == s2.w) + (s3.w == s3.w) + ln;
+        item(s0, [&]() { return sc.lg_start[c]; }, te, tx);
+        item(s1, [&]() { return sc.lg_start[c] + 1u; }, te, tx);
+        item(s2, [&]() { return sc.lg_start[c] + 2u; }, te, tx);
+        item(s3, [&]() { return sc.lg_start[c] + 3u; }, te, tx);
+        for (uint32_t q = lb; q < lb + ln; ++q) item(items[q], [q]() { return q; }, te, tx);
+    });
 }
 
 }  // namespace dev

@@ -786,6 +786,18 @@ __device__ __forceinline__ float cull_bound(double t) {   // t rounded up to f32
 // RTW_NT_NODES (experiment): the while-while traversal's node loads non-temporal
 // (trees outside LDS: C3 / C5), so that streaming a large tree through L2 does
 // not evict the light grid the walk reads
+// RTW_COOP_ADAPT: the f64 cooperative walk sizes its pieces per trip (below
+// the tuned grid_piece) so the wave's pending cells fill its lanes
+#ifndef RTW_COOP_ADAPT
+#define RTW_COOP_ADAPT 1
+#endif
+constexpr uint32_t kCoopAdaptMin = 4;   // the shortest adaptive piece (cells)
+// RTW_GRID_REC: the cooperative light-grid walks read the cell records
+// (DevScene::lg_rec: one 64-byte load per cell) instead of the cell's range
+// and then each light (0: the range walk, for A/B)
+#ifndef RTW_GRID_REC
+#define RTW_GRID_REC 1
+#endif
 #ifndef RTW_NT_NODES
 #define RTW_NT_NODES 0
 #endif
@@ -1713,10 +1725,10 @@ __device__ __forceinline__ float lights_pdf_grid(const DevScene<float>& sc, V3<f
 // one-piece ray (most of them) sums exactly as lights_pdf_grid.  `slots`:
 // `cap` (a multiple of 64) floats of the wave's LDS; every lane of the wave
 // calls this (converged), with wave-uniform P.
-template <bool kRobust>
+template <bool kRobust, typename Mark>
 __device__ __forceinline__ float lights_pdf_grid_coop(const DevScene<float>& sc, bool pend, V3<float> o, V3<float> d,
                                                    uint32_t P, float* __restrict__ slots, uint32_t cap,
-                                                   uint32_t lane, LightWork& lw) {
+                                                   uint32_t lane, LightWork& lw, Mark&& mark) {
     float acc = 0.f, tn = 0.f, tf = 0.f;
     uint32_t k = 0;
     if (pend) {
@@ -1739,6 +1751,7 @@ __device__ __forceinline__ float lights_pdf_grid_coop(const DevScene<float>& sc,
         if (lane >= off) incl += v;
     }
     const uint32_t first = incl - k, total = (uint32_t)__shfl((int)incl, 63);
+    mark(13);
     for (uint32_t b = 0; b < total; b += cap) {
         const uint32_t e = min(b + cap, total);
         for (uint32_t r = b; r < e; r += 64) {
@@ -1761,21 +1774,34 @@ __device__ __forceinline__ float lights_pdf_grid_coop(const DevScene<float>& sc,
                 const float ra = len2_f32(rd);
                 const float ria = __builtin_amdgcn_rcpf(ra);
                 float part = j == 0 ? racc : 0.f;
-                light_grid_walk_piece(sc, ro, rd, grid_inv(rd.x), grid_inv(rd.y), grid_inv(rd.z), t_at(j),
-                                      t_at(j + 1), j == 0, j + 1 == rk, [&](uint32_t q, float te, float tx) {
-                    ++lw.tests;
-                    const R4<float> L = sc.lg_sph[q];
+                auto test = [&](const R4<float>& L, float te, float tx) {
                     const float fx = ro.x - L.x, fy = ro.y - L.y, fz = ro.z - L.z;
                     const float tc = -__builtin_fmaf(rd.z, fz, __builtin_fmaf(rd.y, fy, rd.x * fx)) * ria;
                     if (light_hit_f32<kRobust>(L, ro, rd, ra, ria) & (tc >= te) & (tc < tx))
                         part += light_pdf_f32(L, ro);
+                };
+#if RTW_GRID_REC
+                RTW_PROBE_LANES(11);
+                light_grid_walk_piece_rec(sc, sc.lg_rec, sc.lg_sph, ro, rd, grid_inv(rd.x), grid_inv(rd.y),
+                                          grid_inv(rd.z), t_at(j), t_at(j + 1), j == 0, j + 1 == rk,
+                                          [&](const R4<float>& L, auto&&, float te, float tx) {
+                                              RTW_PROBE_LANES(12);
+                                              test(L, te, tx);
+                                          }, &lw.cells, &lw.tests);
+#else
+                light_grid_walk_piece(sc, ro, rd, grid_inv(rd.x), grid_inv(rd.y), grid_inv(rd.z), t_at(j),
+                                      t_at(j + 1), j == 0, j + 1 == rk, [&](uint32_t q, float te, float tx) {
+                    ++lw.tests;
+                    test(sc.lg_sph[q], te, tx);
                 }, &lw.cells);
+#endif
                 slots[g - b] = part;
             }
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        mark(14);
         if (k) {
             const uint32_t g0 = max(first, b), g1 = min(first + k, e);
             for (uint32_t g = g0; g < g1; ++g) acc = g == first ? slots[g - b] : acc + slots[g - b];
@@ -1783,6 +1809,7 @@ __device__ __forceinline__ float lights_pdf_grid_coop(const DevScene<float>& sc,
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        mark(15);
     }
     return acc;
 }
@@ -1846,16 +1873,19 @@ __device__ __forceinline__ double lights_pdf_grid(const DevScene<double>& sc, V3
 // the grid box, cells and their counts rounded to f32.
 struct Grid64 {
     const uint32_t* lg_start;
+    const R4<float>* lg_rec;          // the cell records (f32 lights: lg_sph32's values)
     const R4<float>* lg_sph32;        // DevScene<double>::lg_sph32
     const uint32_t* lg_id;
     const R4<double>* lights;         // the light list (f64 records: the pdfs)
     float lo[3], hi[3], cell[3], inv[3];
     uint32_t n[3], big;
 };
+// `mark(id)`: the clock probes' section marks (RTW_CLOCK builds; else a no-op)
+template <typename Mark>
 __device__ __forceinline__ double lights_pdf_grid_coop64(const Grid64& sc, bool pend,
                                                          const uint32_t* __restrict__ ray, uint32_t P,
                                                          uint32_t* __restrict__ slots, uint32_t cap_words,
-                                                         uint32_t lane, LightWork& lw) {
+                                                         uint32_t lane, LightWork& lw, Mark&& mark) {
     constexpr uint32_t kPieceIds = kCoop64PieceIds, kSlot = kPieceIds + 1, kMax = RTW_COOP64_MAX;
     auto ray_at = [&](uint32_t q) {
         return __longlong_as_double((long long)((uint64_t)ray[(2 * q) * 64 + lane] |
@@ -1887,14 +1917,24 @@ __device__ __forceinline__ double lights_pdf_grid_coop64(const Grid64& sc, bool 
         df = mk(pre.dx, pre.dy, pre.dz);
     }
     float tn = 0.f, tf = 0.f;
-    uint32_t k = 0;
-    if (pend) {
-        uint32_t cells = 0;
-        // at most `cap` pieces (longer pieces for a longer ray): every ray's
-        // pieces fit one round, so its owner finds all of them in the slots
-        if (light_grid_span(g, of, df, grid_inv(df.x), grid_inv(df.y), grid_inv(df.z), tn, tf, cells))
-            k = min((cells + P - 1u) / P, cap);
+    uint32_t k = 0, cells = 0;
+    const bool walks = pend && light_grid_span(g, of, df, grid_inv(df.x), grid_inv(df.y), grid_inv(df.z), tn, tf, cells);
+    // pieces of Q cells (wave-uniform): the sum does not depend on the cut (list
+    // order), so the wave's pending cells are spread over its lanes -- one round
+    // of at most 64 pieces (sum ceil(c / Q) <= C / Q + n <= 64) unless that needs
+    // pieces longer than P, the longest the tuning allows (C3: ~27 short rays per
+    // trip walked as ~27 one-piece rays left most lanes idle)
+    uint32_t Q = P;
+    if constexpr (RTW_COOP_ADAPT != 0) {
+        uint32_t C = walks ? cells : 0u;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) C += (uint32_t)__shfl_xor((int)C, off);
+        const uint32_t nr = (uint32_t)__popcll(__ballot(walks));
+        if (nr < 64u) Q = min(P, max(kCoopAdaptMin, (C + (63u - nr)) / (64u - nr)));
     }
+    // at most `cap` pieces (longer pieces for a longer ray): every ray's
+    // pieces fit one round, so its owner finds all of them in the slots
+    if (walks) k = min((cells + Q - 1u) / Q, cap);
     const uint32_t ia_bits = __float_as_uint(
         __builtin_amdgcn_rcpf(__builtin_fmaf(df.x, df.x, __builtin_fmaf(df.y, df.y, df.z * df.z))));
     double acc = 0.0;
@@ -1910,6 +1950,7 @@ __device__ __forceinline__ double lights_pdf_grid_coop64(const Grid64& sc, bool 
         }
         const uint32_t first = incl - kp, total = (uint32_t)__shfl((int)incl, 63);
         bool walk_again = false;
+        mark(13);
         // rounds of whole rays: [B, Bn) holds the pieces of the rays that start
         // at B or later and end by B + cap (a pending ray without pieces -- it
         // misses the grid -- sums its big-list candidates in the first round)
@@ -1939,15 +1980,15 @@ __device__ __forceinline__ double lights_pdf_grid_coop64(const Grid64& sc, bool 
                     const float ron = fabsf(ro.x) + fabsf(ro.y) + fabsf(ro.z), rdn = fabsf(rd.x) + fabsf(rd.y) + fabsf(rd.z);
                     uint32_t* ent = slots + (gi - B) * kSlot + 1;
                     uint32_t cnt = 0;
-                    light_grid_walk_piece(g, ro, rd, grid_inv(rd.x), grid_inv(rd.y), grid_inv(rd.z), t_at(j),
-                                          t_at(j + 1), j == 0, j + 1 == rk, [&](uint32_t q, float te, float tx) {
-                        ++lw.tests;
-                        const R4<float> L = g.lg_sph[q];
+                    // a light of the piece: a candidate (its list index kept) when the
+                    // pre-pass may hit it in the cell's interval; idx(): its lg_id slot
+                    auto test = [&](const R4<float>& L, auto&& idx, float te, float tx) {
                         if (light_may_hit(L.x, L.y, L.z, L.w, ro.x, ro.y, ro.z, rd.x, rd.y, rd.z, ria, ron, rdn)) {
                             const float tc = -__builtin_fmaf(rd.z, ro.z - L.z, __builtin_fmaf(rd.y, ro.y - L.y,
                                                                                                rd.x * (ro.x - L.x))) * ria;
-                            const uint32_t id = sc.lg_id[q];
-                            if (tc >= te && tc < tx && id >= rlo) {
+                            if (!(tc >= te && tc < tx)) return;
+                            const uint32_t id = sc.lg_id[idx()];
+                            if (id >= rlo) {
                                 // the piece's kPieceIds smallest, sorted (rare: a candidate)
                                 uint32_t m = min(cnt, kPieceIds);
                                 ++cnt;
@@ -1962,13 +2003,25 @@ __device__ __forceinline__ double lights_pdf_grid_coop64(const Grid64& sc, bool 
                                 ent[m] = id;
                             }
                         }
+                    };
+#if RTW_GRID_REC
+                    light_grid_walk_piece_rec(g, sc.lg_rec, g.lg_sph, ro, rd, grid_inv(rd.x), grid_inv(rd.y),
+                                              grid_inv(rd.z), t_at(j), t_at(j + 1), j == 0, j + 1 == rk, test,
+                                              &lw.cells, &lw.tests);
+#else
+                    light_grid_walk_piece(g, ro, rd, grid_inv(rd.x), grid_inv(rd.y), grid_inv(rd.z), t_at(j),
+                                          t_at(j + 1), j == 0, j + 1 == rk, [&](uint32_t q, float te, float tx) {
+                        ++lw.tests;
+                        test(g.lg_sph[q], [q]() { return q; }, te, tx);
                     }, &lw.cells);
+#endif
                     ent[-1] = cnt;
                 }
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            mark(14);
             if (mine) {
                 // every candidate >= lo of this ray is in its pieces' slots (and the
                 // big list) unless a piece kept only its kPieceIds smallest: merge
@@ -2033,6 +2086,7 @@ __device__ __forceinline__ double lights_pdf_grid_coop64(const Grid64& sc, bool 
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            mark(15);
             B = Bn;
             if (B >= total) break;
         }
@@ -2833,7 +2887,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                     const V3<R> att = colour;
                     // the normal's Onb (onb.rs:8-35) is built by mixture_direction
                     // for the cosine lanes only; the pdf needs its w = normalize(n)
-                    const V3<R> wn = PR::normalize(nrm);
+                    // (computed after the direction: not held across the sampling)
                     V3<R> dir;
                     const bool to_light = PR::u_std(g.next()) < (R)0.5;
                     bool sampled = false;
@@ -2841,7 +2895,10 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                         sampled = true;
                         // HittableList::random (hittable_list.rs:414-419): a
                         // uniform light (one gen_index draw), then its random()
-                        if (kargs()->sc.n_list == 0) {
+                        // (no lref list without kPrims: the light kernels drop that code;
+                        // the others keep it -- dropped there, the f64 Book-1 kernel's
+                        // registers were allocated worse: +0.5 %)
+                        if ((kLightBvh && !kPrims) || kargs()->sc.n_list == 0) {
                             // an empty list panics there (:417): counted; the
                             // sample goes on along a NaN direction and ends NaN
                             // at its next world query, as in the oracle
@@ -2889,11 +2946,12 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                     RTW_PROBE_LAMBERT_DIR();
                     RTW_PROBE_CLK(4);
                     const V3<R> ndir = PR::normalize(dir);
+                    const V3<R> wn = PR::normalize(nrm);
                     const R cos_w = PR::over_pi(dot(ndir, wn));
                     R acc;                                                // hittable_list.rs:408-412
-                    // the light grid's walk by the whole wave: deferred to the end of the trip
-                    const bool coop = kCoopGrid && p.light_bvh == 2 && p.grid_piece != 0 && !(kPrims && kargs()->sc.lref);
-                    if (coop) {
+                    // the light walks of the light BVH / grid kernels: deferred to the end
+                    // of the trip (the grid's by the whole wave, the others per lane)
+                    if constexpr (kCoopGrid) {
                         const R spdf = PR::max_(PR::over_pi(dot(nrm, ndir)), (R)0);
                         pend = true;
                         pend_aw = att * spdf;
@@ -2996,7 +3054,29 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
         if constexpr (kCoopGrid) {
             // the deferred Lambertian light pdfs of this trip, by the whole wave;
             // then the path throughput as in the Lambertian branch
-            if (__any(pend)) {
+            // (wave-uniform) the grid's walk by the whole wave; else -- the light
+            // BVH, or the grid with grid_piece 0 -- each lane walks for its own
+            // ray here, where less of the path state is live than at the bounce
+            const bool coop_walk = kargs()->light_bvh == 2 && kargs()->grid_piece != 0;
+            if (!coop_walk && __any(pend)) {
+                const V3<R> po = kHit64 ? from64<R>(o64) : o, pd = kHit64 ? from64<R>(d64) : d;
+                R acc = (R)0;
+                if (pend) {
+                    LightWork lw;
+                    RTW_KARG_SCENE(wsc);
+                    acc = kargs()->light_bvh == 2
+                              ? lights_pdf_grid<kRobust>(wsc, po, pd, lw)
+                              : lights_pdf_bvh<kRobust>(wsc, po, pd,
+                                                        reinterpret_cast<int32_t*>(smem) + wave * p.stack * 64 + lane, lw);
+                    light_work_lane(wcnt, lw);
+                    R lpdf = PR::div_(acc, (R)p.sc.n_list);
+                    if (p.sc.light_flags & 1u) lpdf = PR::div_(lpdf * (R)p.sc.n_list, (R)p.sc.n_list);
+                    const R pdf = lpdf * (R)0.5 + pend_ch;
+                    mult = mult * PR::divs(pend_aw, pdf);
+                    pend = false;
+                }
+            }
+            if (coop_walk && __any(pend)) {
                 // The walk's registers come on top of the whole path state: the RNG
                 // state and (hit64) the f64 ray wait in the wave's LDS stack area
                 // ([word][lane]; the host sizes p.stack >= kCoopStash + 1) instead of
@@ -3039,12 +3119,17 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                 }
                 R acc;
                 LightWork lw;
+                // the walk's sections for the clock probes (RTW_CLOCK): 13 setup, 14 the
+                // pieces' walks, 15 the owners' sums
+                auto walk_mark = [&](int id) { (void)id; RTW_PROBE_CLK(id); };
+                RTW_PROBE_CLK(11);
                 if constexpr (sizeof(R) == 8) {
                     // (the pending ray: stash words 4..9, put above)
                     // the grid's fields read from the kernel arguments here (RTW_KARG_SCENE)
                     RTW_KARG_SCENE(wsc);
                     Grid64 gr;
                     gr.lg_start = wsc.lg_start;
+                    gr.lg_rec = wsc.lg_rec;
                     gr.lg_sph32 = wsc.lg_sph32;
                     gr.lg_id = wsc.lg_id;
                     gr.lights = wsc.lights;
@@ -3058,12 +3143,12 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                     }
                     gr.big = wsc.lg_big;
                     acc = lights_pdf_grid_coop64(gr, pend, area + 8 * 64, kargs()->grid_piece, area + kStash * 64,
-                                                 (kargs()->stack - kStash) * 64, lane, lw);
+                                                 (kargs()->stack - kStash) * 64, lane, lw, walk_mark);
                 } else {
                     float* slots = reinterpret_cast<float*>(area + kStash * 64);
                     RTW_KARG_SCENE(wsc);
                     acc = lights_pdf_grid_coop<kRobust>(wsc, pend, po, pd, kargs()->grid_piece, slots,
-                                                        (kargs()->stack - kStash) * 64, lane, lw);
+                                                        (kargs()->stack - kStash) * 64, lane, lw, walk_mark);
                 }
                 light_work_wave(wcnt, lw, lane);
                 g.s0 = get(0);

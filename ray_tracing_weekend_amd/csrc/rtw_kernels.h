@@ -50,6 +50,7 @@ struct alignas(4 * sizeof(R)) R4 {
 //   lsph/lid : n_li x R4 {c, r} / u32 in light-BVH leaf order
 //   lg_start : n_cells + 1 x u32                -- light grid (light pdf, long light lists)
 //   lg_sph/lg_id : n_items x R4 {c, r} / u32    -- big list, then each cell's lights
+//   lg_rec   : n_cells x 4 x R4<float>          -- each cell's first lights inline (the walk's one load per cell)
 template <typename R>
 struct BvhNode {
     // two child boxes per node (children tested together, the classic
@@ -108,6 +109,8 @@ struct DevScene : DevSceneCull<R> {
     const uint32_t* lg_start;         // light grid: n_cells + 1 offsets into lg_sph / lg_id
     const R4<R>* lg_sph;              // light grid items {c, r}: the big list, then cell by cell
     const uint32_t* lg_id;            // light-list index of lg_sph[k]
+    const R4<float>* lg_rec;          // light grid cell records (light_grid.hpp kGridRecSlots): the
+                                      // cell's lights as the f32 walk reads them, inline, or 3 + a link
     const R* quads;                   // n_quads x kQuadR (see quad layout below)
     const uint32_t* quad_mat;
     const R* lquads;                  // the light list's quads, n_lquads x kQuadR

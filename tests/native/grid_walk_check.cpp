@@ -2,12 +2,16 @@
 // build_light_grid + light_grid.hpp light_grid_walk, the f64 instance the
 // parity kernels run): for random light sets and random rays, the walk's
 // closest-approach rule must count every light the ray hits exactly once and
-// no light twice.  Built and run by tests/test_light_grid_host.py:
+// no light twice; the cell-record walk (light_grid_walk_piece_rec, the
+// kernels' cooperative walks) must visit exactly the range walk's lights and
+// intervals.  Built and run by tests/test_light_grid_host.py:
 //   hipcc -x hip --cuda-host-only -O2 -std=c++17 -I<csrc> -I<include> \
 //       grid_walk_check.cpp <csrc>/host/bvh.cpp -o grid_walk_check
 #include <stdio.h>
 
+#include <algorithm>
 #include <random>
+#include <tuple>
 #include <vector>
 
 #include "host/bvh.hpp"
@@ -35,7 +39,7 @@ static int hit_class(const double* L, V o, V d) {
 int main() {
     std::mt19937_64 rng(12345);
     std::uniform_real_distribution<double> U(0.0, 1.0);
-    long checked = 0, hits = 0, bad = 0;
+    long checked = 0, hits = 0, bad = 0, rec_visits = 0;
     for (int scene = 0; scene < 6; ++scene) {
         // 0: a field of small lights in a thin layer + one large light (the
         // scenes::simple shape); 1: random sizes in a box; 2: coincident
@@ -65,6 +69,14 @@ int main() {
                 const double* l = &L[4 * g.items[q]];
                 items[q] = R4<double>{l[0], l[1], l[2], l[3]};
             }
+            // the cell records of the f32 walk (light_grid_walk_piece_rec), radius as given
+            const std::vector<float> recf = rtw::light_grid_records(g, L.data(), false);
+            std::vector<R4<float>> items32(g.items.size());
+            for (size_t q = 0; q < g.items.size(); ++q) {
+                const double* l = &L[4 * g.items[q]];
+                items32[q] = R4<float>{(float)l[0], (float)l[1], (float)l[2], (float)l[3]};
+            }
+            const R4<float>* rec = reinterpret_cast<const R4<float>*>(recf.data());
             rtw::DevScene<double> sc{};
             sc.lg_start = g.start.data();
             sc.lg_sph = items.data();
@@ -119,14 +131,38 @@ int main() {
                             const uint32_t kp = (cells + Ps[v] - 1) / Ps[v];
                             const double step = (tf - tn) / (double)kp;
                             auto t_at = [&](uint32_t q) { return q == 0 ? tn : fma((double)q, step, tn); };
-                            for (uint32_t j = 0; j < kp; ++j)
+                            for (uint32_t j = 0; j < kp; ++j) {
+                                std::vector<std::tuple<uint32_t, double, double>> seen, seen_rec;
+                                uint32_t nc = 0, nc_rec = 0, nt_rec = 0;
                                 rtw::dev::light_grid_walk_piece(sc, o, d, ix, iy, iz, t_at(j), t_at(j + 1), j == 0,
                                                                 j + 1 == kp, [&](uint32_t q, double te, double tx) {
+                                    seen.emplace_back(q, te, tx);
                                     const R4<double>& l = items[q];
                                     const double tc = -((o.x - l.x) * d.x + (o.y - l.y) * d.y + (o.z - l.z) * d.z) * ia;
                                     if (tc >= te && tc < tx && hit_class(&L[4 * g.items[q]], o, d) >= 0)
                                         ++pc[v * n + g.items[q]];
-                                });
+                                }, &nc);
+                                // the record walk visits the same (light, interval) pairs, the
+                                // empty / link slots as NaN lights, each light as its f32 record
+                                rtw::dev::light_grid_walk_piece_rec(sc, rec, items32.data(), o, d, ix, iy, iz, t_at(j),
+                                                                    t_at(j + 1), j == 0, j + 1 == kp,
+                                                                    [&](const R4<float>& l, auto&& idx, double te, double tx) {
+                                    if (!(l.w == l.w)) return;
+                                    const uint32_t q = idx();
+                                    const R4<float>& w = items32[q];
+                                    if (!(l.x == w.x && l.y == w.y && l.z == w.z && l.w == w.w)) ++bad;
+                                    seen_rec.emplace_back(q, te, tx);
+                                }, &nc_rec, &nt_rec);
+                                std::sort(seen.begin(), seen.end());
+                                std::sort(seen_rec.begin(), seen_rec.end());
+                                if (seen != seen_rec || nc != nc_rec || nt_rec != seen.size()) {
+                                    if (bad < 10)
+                                        printf("records: scene %d density %g ray %d piece %u: %zu vs %zu visits, %u vs %u cells\n",
+                                               scene, density, r, j, seen.size(), seen_rec.size(), nc, nc_rec);
+                                    ++bad;
+                                }
+                                rec_visits += seen.size();
+                            }
                         }
                     }
                     for (uint32_t q = 0; q < g.n_big; ++q)
@@ -152,6 +188,7 @@ int main() {
             }
         }
     }
-    printf("checked %ld (ray, light) pairs, %ld hits, %ld wrong\n", checked, hits, bad);
-    return bad == 0 && hits > 1000 ? 0 : 1;
+    printf("checked %ld (ray, light) pairs, %ld hits, %ld wrong; %ld record-walk visits\n", checked, hits, bad,
+           rec_visits);
+    return bad == 0 && hits > 1000 && rec_visits > 100000 ? 0 : 1;
 }

@@ -19,7 +19,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 VAR = os.path.join(ROOT, "build", "variants", "clock")
 PARTS = {0: "item pool + sample start", 1: "planes", 2: "closest hit", 3: "hit record", 4: "Lambertian",
          5: "light pdf", 6: "specular (one pass)", 7: "Metal", 8: "Dielectric", 9: "sample end",
-         10: "wave tail", 11: "cooperative grid walk", 12: "loop head"}
+         10: "wave tail", 11: "cooperative grid walk (stash, unstash)", 12: "loop head",
+         13: "grid walk: setup", 14: "grid walk: pieces", 15: "grid walk: owners' sums"}
 CONFIGS = {"C2": (11, 1200, 800, 500), "C3": (50, 1920, 1080, 1024), "C5": (500, 1920, 1080, 256)}
 
 

@@ -17,7 +17,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 VAR = os.path.join(ROOT, "build", "variants", "prof")
 NAMES = {1: "bvh inner step", 2: "leaf tests", 3: "segment loop (wave)", 4: "segment (active lanes)",
          5: "own-sphere f64 test", 6: "closest-hit query", 7: "Metal", 8: "Dielectric", 9: "Lambertian",
-         10: "next sample"}
+         10: "next sample", 11: "grid walk: piece (f32 coop)", 12: "grid walk: light slot (f32 coop, 4 per cell)"}
+CONFIGS = {"C2": (11, 1200, 800, 500), "C3": (50, 1920, 1080, 1024), "C5": (500, 1920, 1080, 256)}
 
 
 def build():
@@ -40,8 +41,9 @@ def run(a):
     rd = rtw._lib.rtw_probe_lanes_read
     rd.argtypes = [C.c_void_p, C.c_int]
     buf = (C.c_ulonglong * 32)()
-    soa, b = rtw.scenes.simple_soa(0x5EED0001)
-    cam = b.with_image_width(1200).with_image_height(800).with_samples_per_pixel(a.spp).with_max_depth(50).build()
+    n, w, h, _ = CONFIGS[a.config]
+    soa, b = rtw.scenes.simple_soa(0x5EED0001, n)
+    cam = b.with_image_width(w).with_image_height(h).with_samples_per_pixel(a.spp).with_max_depth(50).build()
     with rtw.Renderer(precision=rtw.RTW_F32) as r:
         for kv in filter(None, a.tuning.split(",")):
             k, v = kv.split("=")
@@ -52,7 +54,7 @@ def run(a):
         st = r.get_stats()
         assert rd(buf, 1) == 0
     segs = st.segments
-    out = {"tuning": a.tuning, "segments": segs, "phases": {}}
+    out = {"config": a.config, "tuning": a.tuning, "spp": a.spp, "segments": segs, "phases": {}}
     for i, name in NAMES.items():
         lanes, passes = buf[2 * i], buf[2 * i + 1]
         if passes:
@@ -67,6 +69,7 @@ def main():
     ap.add_argument("mode", choices=["build", "run"])
     ap.add_argument("--tuning", default="")
     ap.add_argument("--spp", type=int, default=500)
+    ap.add_argument("--config", default="C2")
     a = ap.parse_args()
     build() if a.mode == "build" else run(a)
 
