@@ -350,11 +350,11 @@ struct LightPre {
 // the kMax smallest list indices >= lo; their pdfs are added in index order
 // and, when the pass had to drop hits, the next pass continues above the last
 // index summed.  (A ray skimming C5's flat light layer hits ~10 lights.)
-template <typename Walk>
-__device__ __forceinline__ double lights_sum_in_list_order(const R4<double>* __restrict__ lights, V3<double> o,
-                                                           V3<double> d, Walk&& walk) {
+// (R: the sum's type; pdf(id): light id's pdf)
+template <typename R, typename Walk, typename Pdf>
+__device__ __forceinline__ R lights_sum_ids_in_list_order(Walk&& walk, Pdf&& pdf) {
     constexpr uint32_t kMax = 8;
-    double acc = 0.0;
+    R acc = (R)0;
     uint32_t lo = 0;
     for (;;) {
         uint32_t ids[kMax];
@@ -375,13 +375,18 @@ __device__ __forceinline__ double lights_sum_in_list_order(const R4<double>* __r
             ids[q] = id;
             ++n;
         });
-        for (uint32_t q = 0; q < n; ++q) {
-            const R4<double> L = lights[ids[q]];
-            acc = acc + sphere_pdf_value(mk(L.x, L.y, L.z), L.w, o, d);
-        }
+        for (uint32_t q = 0; q < n; ++q) acc = acc + pdf(ids[q]);
         if (!dropped) return acc;
         lo = ids[kMax - 1] + 1u;
     }
+}
+template <typename Walk>
+__device__ __forceinline__ double lights_sum_in_list_order(const R4<double>* __restrict__ lights, V3<double> o,
+                                                           V3<double> d, Walk&& walk) {
+    return lights_sum_ids_in_list_order<double>(walk, [&](uint32_t id) {
+        const R4<double> L = lights[id];
+        return sphere_pdf_value(mk(L.x, L.y, L.z), L.w, o, d);
+    });
 }
 
 template <bool kRobust = false>
@@ -1880,42 +1885,29 @@ struct Grid64 {
     float lo[3], hi[3], cell[3], inv[3];
     uint32_t n[3], big;
 };
-// `mark(id)`: the clock probes' section marks (RTW_CLOCK builds; else a no-op)
-template <typename Mark>
-__device__ __forceinline__ double lights_pdf_grid_coop64(const Grid64& sc, bool pend,
-                                                         const uint32_t* __restrict__ ray, uint32_t P,
-                                                         uint32_t* __restrict__ slots, uint32_t cap_words,
-                                                         uint32_t lane, LightWork& lw, Mark&& mark) {
+// The cooperative walk with the list-order sum, both precisions (R: the sum).
+// `g`: the grid as the f32 walk reads it (lg_start, lg_sph, box, cells);
+// `rec` its cell records, `lg_id` the items' list indices, `big` the big
+// list's length; (of, df) the pending ray in f32 and ia_own = 1 / (df . df)
+// as the owner's tests compute it.  cand(L, ro, rd, ra, ria, ron, rdn): may
+// the ray hit light L (a piece's test; the owner's ray bperm'd, ra = its
+// len2_f32, ron / rdn = |o|_1, |d|_1); big_hit(L): the owner's test of a big
+// light; sum_ids(ids, n, bound, acc): acc += the pdfs of ids[0..n) up to
+// `bound`, in that (list) order.  `mark(id)`: the clock probes' section marks
+// (RTW_CLOCK builds; else a no-op).
+template <typename R, typename Cand, typename BigHit, typename SumIds, typename Mark>
+__device__ __forceinline__ R lights_pdf_grid_coop_list(const DevScene<float>& g, const R4<float>* __restrict__ rec,
+                                                       const uint32_t* __restrict__ lg_id, uint32_t big, V3<float> of,
+                                                       V3<float> df, float ia_own, bool pend, uint32_t P,
+                                                       uint32_t* __restrict__ slots, uint32_t cap_words, uint32_t lane,
+                                                       LightWork& lw, Cand&& cand, BigHit&& big_hit, SumIds&& sum_ids,
+                                                       Mark&& mark) {
     constexpr uint32_t kPieceIds = kCoop64PieceIds, kSlot = kPieceIds + 1, kMax = RTW_COOP64_MAX;
-    auto ray_at = [&](uint32_t q) {
-        return __longlong_as_double((long long)((uint64_t)ray[(2 * q) * 64 + lane] |
-                                                ((uint64_t)ray[(2 * q + 1) * 64 + lane] << 32)));
-    };
-    auto ray_o = [&]() { return mk(ray_at(0), ray_at(1), ray_at(2)); };
-    auto ray_d = [&]() { return mk(ray_at(3), ray_at(4), ray_at(5)); };
     const uint32_t cap = cap_words / (kSlot * 64) * 64;   // pieces per round
-    // the grid as a DevScene<float> (only the fields the walk reads)
-    DevScene<float> g;
-    g.lg_start = sc.lg_start;
-    g.lg_sph = sc.lg_sph32;
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-        g.lg_lo[a] = sc.lo[a];
-        g.lg_hi[a] = sc.hi[a];
-        g.lg_cell[a] = sc.cell[a];
-        g.lg_inv[a] = sc.inv[a];
-        g.lg_n[a] = sc.n[a];
-    }
     // (the host sizes the stack area for at least one round of 64 pieces, so a
     // smaller area is a host error: every pending ray ends NaN, never a loop
     // that cannot advance)
-    if (cap == 0) return pend ? (double)NAN : 0.0;
-    V3<float> of, df;           // the f32 ray
-    {
-        const LightPre pre(ray_o(), ray_d());
-        of = mk(pre.ox, pre.oy, pre.oz);
-        df = mk(pre.dx, pre.dy, pre.dz);
-    }
+    if (cap == 0) return pend ? (R)NAN : (R)0;
     float tn = 0.f, tf = 0.f;
     uint32_t k = 0, cells = 0;
     const bool walks = pend && light_grid_span(g, of, df, grid_inv(df.x), grid_inv(df.y), grid_inv(df.z), tn, tf, cells);
@@ -1935,9 +1927,8 @@ __device__ __forceinline__ double lights_pdf_grid_coop64(const Grid64& sc, bool 
     // at most `cap` pieces (longer pieces for a longer ray): every ray's
     // pieces fit one round, so its owner finds all of them in the slots
     if (walks) k = min((cells + Q - 1u) / Q, cap);
-    const uint32_t ia_bits = __float_as_uint(
-        __builtin_amdgcn_rcpf(__builtin_fmaf(df.x, df.x, __builtin_fmaf(df.y, df.y, df.z * df.z))));
-    double acc = 0.0;
+    const uint32_t ia_bits = __float_as_uint(ia_own);
+    R acc = (R)0;
     uint32_t lo = 0;
     bool more = pend;           // the ray still needs a walk (over list indices >= lo)
     while (__any(more)) {
@@ -1976,18 +1967,19 @@ __device__ __forceinline__ double lights_pdf_grid_coop64(const Grid64& sc, bool 
                     const uint32_t j = gi - rfirst;
                     const float step = (rtf - rtn) / (float)rk;
                     auto t_at = [&](uint32_t q) { return q == 0 ? rtn : __builtin_fmaf((float)q, step, rtn); };
-                    // the owner's LightPre quantities, from the same f32 ray
+                    // the owner's test quantities, from the same f32 ray
                     const float ron = fabsf(ro.x) + fabsf(ro.y) + fabsf(ro.z), rdn = fabsf(rd.x) + fabsf(rd.y) + fabsf(rd.z);
+                    const float ra = len2_f32(rd);
                     uint32_t* ent = slots + (gi - B) * kSlot + 1;
                     uint32_t cnt = 0;
                     // a light of the piece: a candidate (its list index kept) when the
-                    // pre-pass may hit it in the cell's interval; idx(): its lg_id slot
+                    // test may hit it in the cell's interval; idx(): its lg_id slot
                     auto test = [&](const R4<float>& L, auto&& idx, float te, float tx) {
-                        if (light_may_hit(L.x, L.y, L.z, L.w, ro.x, ro.y, ro.z, rd.x, rd.y, rd.z, ria, ron, rdn)) {
+                        if (cand(L, ro, rd, ra, ria, ron, rdn)) {
                             const float tc = -__builtin_fmaf(rd.z, ro.z - L.z, __builtin_fmaf(rd.y, ro.y - L.y,
                                                                                                rd.x * (ro.x - L.x))) * ria;
                             if (!(tc >= te && tc < tx)) return;
-                            const uint32_t id = sc.lg_id[idx()];
+                            const uint32_t id = lg_id[idx()];
                             if (id >= rlo) {
                                 // the piece's kPieceIds smallest, sorted (rare: a candidate)
                                 uint32_t m = min(cnt, kPieceIds);
@@ -2005,7 +1997,7 @@ __device__ __forceinline__ double lights_pdf_grid_coop64(const Grid64& sc, bool 
                         }
                     };
 #if RTW_GRID_REC
-                    light_grid_walk_piece_rec(g, sc.lg_rec, g.lg_sph, ro, rd, grid_inv(rd.x), grid_inv(rd.y),
+                    light_grid_walk_piece_rec(g, rec, g.lg_sph, ro, rd, grid_inv(rd.x), grid_inv(rd.y),
                                               grid_inv(rd.z), t_at(j), t_at(j + 1), j == 0, j + 1 == rk, test,
                                               &lw.cells, &lw.tests);
 #else
@@ -2028,8 +2020,6 @@ __device__ __forceinline__ double lights_pdf_grid_coop64(const Grid64& sc, bool 
                 // the kMax smallest, sum them in list order, and merge again above
                 // the last one summed until done -- or until a piece's dropped
                 // candidates are needed, which takes another walk
-                const float ia = __uint_as_float(ia_bits);
-                const float on = fabsf(of.x) + fabsf(of.y) + fabsf(of.z), dn = fabsf(df.x) + fabsf(df.y) + fabsf(df.z);
                 for (;;) {
                     uint32_t ids[kMax];
                     uint32_t n = 0, bp = 0xffffffffu;   // bp: below a piece's dropped candidates
@@ -2048,14 +2038,11 @@ __device__ __forceinline__ double lights_pdf_grid_coop64(const Grid64& sc, bool 
                         ids[q] = id;
                         ++n;
                     };
-                    if (sc.big) {
-                        lw.tests += sc.big;
-                        for (uint32_t q = 0; q < sc.big; ++q) {
-                            const R4<float> L = g.lg_sph[q];
-                            const uint32_t id = sc.lg_id[q];
-                            if (id >= lo && light_may_hit(L.x, L.y, L.z, L.w, of.x, of.y, of.z, df.x, df.y, df.z, ia,
-                                                          on, dn))
-                                add(id);
+                    if (big) {
+                        lw.tests += big;
+                        for (uint32_t q = 0; q < big; ++q) {
+                            const uint32_t id = lg_id[q];
+                            if (id >= lo && big_hit(g.lg_sph[q])) add(id);
                         }
                     }
                     for (uint32_t gi = first; gi < first + kp; ++gi) {
@@ -2066,12 +2053,7 @@ __device__ __forceinline__ double lights_pdf_grid_coop64(const Grid64& sc, bool 
                         if (cnt > kPieceIds) bp = min(bp, ent[kPieceIds - 1]);
                     }
                     const uint32_t bound = dropped ? min(bp, ids[kMax - 1]) : bp;
-                    const V3<double> o = ray_o(), d = ray_d();
-                    for (uint32_t q = 0; q < n; ++q) {
-                        if (ids[q] > bound) break;
-                        const R4<double> L = sc.lights[ids[q]];
-                        acc = acc + sphere_pdf_value(mk(L.x, L.y, L.z), L.w, o, d);
-                    }
+                    sum_ids(ids, n, bound, acc);
                     if (bound == 0xffffffffu) {
                         more = false;                       // every candidate summed
                         break;
@@ -2093,6 +2075,59 @@ __device__ __forceinline__ double lights_pdf_grid_coop64(const Grid64& sc, bool 
         more = more && walk_again;
     }
     return acc;
+}
+
+
+// the f64 instance: candidates by the f64 path's f32 pre-pass (light_may_hit),
+// the pdfs in f64 from the pending ray in the wave's LDS stash
+template <typename Mark>
+__device__ __forceinline__ double lights_pdf_grid_coop64(const Grid64& sc, bool pend,
+                                                         const uint32_t* __restrict__ ray, uint32_t P,
+                                                         uint32_t* __restrict__ slots, uint32_t cap_words,
+                                                         uint32_t lane, LightWork& lw, Mark&& mark) {
+    auto ray_at = [&](uint32_t q) {
+        return __longlong_as_double((long long)((uint64_t)ray[(2 * q) * 64 + lane] |
+                                                ((uint64_t)ray[(2 * q + 1) * 64 + lane] << 32)));
+    };
+    auto ray_o = [&]() { return mk(ray_at(0), ray_at(1), ray_at(2)); };
+    auto ray_d = [&]() { return mk(ray_at(3), ray_at(4), ray_at(5)); };
+    // the grid as a DevScene<float> (only the fields the walk reads)
+    DevScene<float> g;
+    g.lg_start = sc.lg_start;
+    g.lg_sph = sc.lg_sph32;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        g.lg_lo[a] = sc.lo[a];
+        g.lg_hi[a] = sc.hi[a];
+        g.lg_cell[a] = sc.cell[a];
+        g.lg_inv[a] = sc.inv[a];
+        g.lg_n[a] = sc.n[a];
+    }
+    V3<float> of, df;           // the f32 ray
+    {
+        const LightPre pre(ray_o(), ray_d());
+        of = mk(pre.ox, pre.oy, pre.oz);
+        df = mk(pre.dx, pre.dy, pre.dz);
+    }
+    const float ia = __builtin_amdgcn_rcpf(__builtin_fmaf(df.x, df.x, __builtin_fmaf(df.y, df.y, df.z * df.z)));
+    auto cand = [&](const R4<float>& L, V3<float> ro, V3<float> rd, float, float ria, float ron, float rdn) {
+        return light_may_hit(L.x, L.y, L.z, L.w, ro.x, ro.y, ro.z, rd.x, rd.y, rd.z, ria, ron, rdn);
+    };
+    auto big_hit = [&](const R4<float>& L) {
+        const float ib = __builtin_amdgcn_rcpf(__builtin_fmaf(df.x, df.x, __builtin_fmaf(df.y, df.y, df.z * df.z)));
+        const float on = fabsf(of.x) + fabsf(of.y) + fabsf(of.z), dn = fabsf(df.x) + fabsf(df.y) + fabsf(df.z);
+        return light_may_hit(L.x, L.y, L.z, L.w, of.x, of.y, of.z, df.x, df.y, df.z, ib, on, dn);
+    };
+    auto sum_ids = [&](const uint32_t* ids, uint32_t n, uint32_t bound, double& acc) {
+        const V3<double> o = ray_o(), d = ray_d();
+        for (uint32_t q = 0; q < n; ++q) {
+            if (ids[q] > bound) break;
+            const R4<double> L = sc.lights[ids[q]];
+            acc = acc + sphere_pdf_value(mk(L.x, L.y, L.z), L.w, o, d);
+        }
+    };
+    return lights_pdf_grid_coop_list<double>(g, sc.lg_rec, sc.lg_id, sc.big, of, df, ia, pend, P, slots, cap_words,
+                                             lane, lw, cand, big_hit, sum_ids, mark);
 }
 
 // Light list with quads (DevScene::lref set): HittableList::pdf_value over
