@@ -2285,7 +2285,14 @@ template <typename R, int kWorld, int kOpt>
 #ifndef RTW_WAVES_F64_LBVH
 #define RTW_WAVES_F64_LBVH 3
 #endif
-__global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ? RTW_WAVES_H64 : RTW_WAVES)
+// f32 (hit64) kernels with the light grid / BVH: 4 waves per SIMD (3, 168
+// VGPRs: C3 / C5 f32 +15 % time; profiles/r05_f32_list_waves_ab.jsonl)
+#ifndef RTW_WAVES_H64_LBVH
+#define RTW_WAVES_H64_LBVH 4
+#endif
+__global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ? ((kOpt & kOptLightBvh) ? RTW_WAVES_H64_LBVH
+                                                                                                      : RTW_WAVES_H64)
+                                                                             : RTW_WAVES)
                                                          : ((kOpt & (kOptPrims | kOptTex)) ? 1
                                                             : ((kOpt & kOptLightBvh) ? RTW_WAVES_F64_LBVH
                                                                                      : RTW_WAVES_F64)))
