@@ -564,11 +564,14 @@ __device__ __forceinline__ float bperm_f(float x, int32_t src) {
     return __int_as_float(__builtin_amdgcn_ds_bpermute(src << 2, __float_as_int(x)));
 }
 __device__ __forceinline__ int32_t bperm_i(int32_t x, int32_t src) { return __builtin_amdgcn_ds_bpermute(src << 2, x); }
+__device__ __forceinline__ float bperm_any(float x, int32_t src) { return bperm_f(x, src); }
+__device__ __forceinline__ double bperm_any(double x, int32_t src);
 __device__ __forceinline__ double bperm_d(double x, int32_t src) {
     const uint64_t b = (uint64_t)__double_as_longlong(x);
     const uint32_t lo = (uint32_t)bperm_i((int32_t)(uint32_t)b, src), hi = (uint32_t)bperm_i((int32_t)(b >> 32), src);
     return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
 }
+__device__ __forceinline__ double bperm_any(double x, int32_t src) { return bperm_d(x, src); }
 
 template <bool kRobust>
 struct SphereTester<double, kRobust> {   // exact reference arithmetic (sphere.rs:61-80)
@@ -797,6 +800,11 @@ __device__ __forceinline__ float cull_bound(double t) {   // t rounded up to f32
 #define RTW_COOP_ADAPT 1
 #endif
 constexpr uint32_t kCoopAdaptMin = 4;   // the shortest adaptive piece (cells)
+// RTW_COOP_DEAL: the f64 cooperative walk deals its owners' candidate pdfs to
+// the whole wave (lights_pdf_grid_coop_list)
+#ifndef RTW_COOP_DEAL
+#define RTW_COOP_DEAL 1
+#endif
 // RTW_GRID_REC: the cooperative light-grid walks read the cell records
 // (DevScene::lg_rec: one 64-byte load per cell) instead of the cell's range
 // and then each light (0: the range walk, for A/B)
@@ -1893,16 +1901,20 @@ struct Grid64 {
 // the ray hit light L (a piece's test; the owner's ray bperm'd, ra = its
 // len2_f32, ron / rdn = |o|_1, |d|_1); big_hit(L): the owner's test of a big
 // light; sum_ids(ids, n, bound, acc): acc += the pdfs of ids[0..n) up to
-// `bound`, in that (list) order.  `mark(id)`: the clock probes' section marks
+// `bound`, in that (list) order; pdf_at(id, owner): light id's pdf for the ray
+// of lane `owner` (RTW_COOP_DEAL: evaluated by any lane).  `mark(id)`: the clock probes' section marks
 // (RTW_CLOCK builds; else a no-op).
-template <typename R, typename Cand, typename BigHit, typename SumIds, typename Mark>
+template <typename R, typename Cand, typename BigHit, typename SumIds, typename PdfAt, typename Mark>
 __device__ __forceinline__ R lights_pdf_grid_coop_list(const DevScene<float>& g, const R4<float>* __restrict__ rec,
                                                        const uint32_t* __restrict__ lg_id, uint32_t big, V3<float> of,
                                                        V3<float> df, float ia_own, bool pend, uint32_t P,
                                                        uint32_t* __restrict__ slots, uint32_t cap_words, uint32_t lane,
                                                        LightWork& lw, Cand&& cand, BigHit&& big_hit, SumIds&& sum_ids,
-                                                       Mark&& mark) {
-    constexpr uint32_t kPieceIds = kCoop64PieceIds, kSlot = kPieceIds + 1, kMax = RTW_COOP64_MAX;
+                                                       PdfAt&& pdf_at, Mark&& mark) {
+    // a piece's slot: [count, ids...] padded to 8 words (the owner reads it as two
+    // 16-byte LDS loads)
+    constexpr uint32_t kPieceIds = kCoop64PieceIds, kSlot = 8, kMax = RTW_COOP64_MAX;
+    static_assert(kPieceIds + 1 <= kSlot, "slot = count + ids");
     const uint32_t cap = cap_words / (kSlot * 64) * 64;   // pieces per round
     // (the host sizes the stack area for at least one round of 64 pieces, so a
     // smaller area is a host error: every pending ray ends NaN, never a loop
@@ -1928,6 +1940,21 @@ __device__ __forceinline__ R lights_pdf_grid_coop_list(const DevScene<float>& g,
     // pieces fit one round, so its owner finds all of them in the slots
     if (walks) k = min((cells + Q - 1u) / Q, cap);
     const uint32_t ia_bits = __float_as_uint(ia_own);
+    // the big list's candidates of the pending ray: tested once per walk, not at
+    // each of the owner's merges (their loads were on the merge's critical path)
+    constexpr uint32_t kBigC = 2;
+    uint32_t bigc[kBigC] = {0u, 0u};
+    uint32_t nbig = 0;
+    bool big_over = false;
+    if (pend && big) {
+        lw.tests += big;
+        for (uint32_t q = 0; q < big; ++q) {
+            if (big_hit(g.lg_sph[q])) {
+                if (nbig < kBigC) bigc[nbig++] = lg_id[q];
+                else big_over = true;
+            }
+        }
+    }
     R acc = (R)0;
     uint32_t lo = 0;
     bool more = pend;           // the ray still needs a walk (over list indices >= lo)
@@ -2014,15 +2041,22 @@ __device__ __forceinline__ R lights_pdf_grid_coop_list(const DevScene<float>& g,
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             mark(14);
-            if (mine) {
-                // every candidate >= lo of this ray is in its pieces' slots (and the
-                // big list) unless a piece kept only its kPieceIds smallest: merge
-                // the kMax smallest, sum them in list order, and merge again above
-                // the last one summed until done -- or until a piece's dropped
-                // candidates are needed, which takes another walk
-                for (;;) {
-                    uint32_t ids[kMax];
-                    uint32_t n = 0, bp = 0xffffffffu;   // bp: below a piece's dropped candidates
+            // every candidate >= lo of this ray is in its pieces' slots (and the
+            // big list) unless a piece kept only its kPieceIds smallest: its owner
+            // merges the kMax smallest, sums them in list order, and merges again
+            // above the last one summed until done -- or until a piece's dropped
+            // candidates are needed, which takes another walk.  RTW_COOP_DEAL: the
+            // owners' merges run together and the pdfs of all their summable ids
+            // are dealt to the wave's lanes (pdf_at(id, owner): any lane evaluates
+            // a candidate for the owner's ray); each owner then adds its values
+            // in list order, fetched by ds_bpermute -- the sum of each ray is the
+            // same, its pdfs no longer computed by its owner lane alone
+            bool owning = mine;
+            while (RTW_COOP_DEAL ? __any(owning) : owning) {
+                uint32_t ids[kMax];
+                uint32_t n = 0, bp = 0xffffffffu, bound = 0xffffffffu;   // bp: below a piece's dropped candidates
+                if (owning) {
+                    RTW_PROBE_LANES(13);
                     bool dropped = false;
                     auto add = [&](uint32_t id) {   // the kMax smallest list indices (lights_sum_in_list_order)
                         if (n == kMax) {
@@ -2038,30 +2072,87 @@ __device__ __forceinline__ R lights_pdf_grid_coop_list(const DevScene<float>& g,
                         ids[q] = id;
                         ++n;
                     };
-                    if (big) {
-                        lw.tests += big;
+                    // the big list's candidates, tested once per walk (bigc below)
+                    if (!big_over) {
+                        for (uint32_t q = 0; q < nbig; ++q)
+                            if (bigc[q] >= lo) add(bigc[q]);
+                    } else {
                         for (uint32_t q = 0; q < big; ++q) {
                             const uint32_t id = lg_id[q];
                             if (id >= lo && big_hit(g.lg_sph[q])) add(id);
                         }
                     }
                     for (uint32_t gi = first; gi < first + kp; ++gi) {
-                        const uint32_t* ent = slots + (gi - B) * kSlot + 1;
-                        const uint32_t cnt = ent[-1];
-                        for (uint32_t q = 0; q < min(cnt, kPieceIds); ++q)
-                            if (ent[q] >= lo) add(ent[q]);
-                        if (cnt > kPieceIds) bp = min(bp, ent[kPieceIds - 1]);
+                        typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+                        const u4* sl = reinterpret_cast<const u4*>(slots + (gi - B) * kSlot);
+                        RTW_PROBE_LANES(14);
+                        const u4 w0 = sl[0], w1 = sl[1];
+                        const uint32_t cnt = w0.x;
+                        const uint32_t e[7] = {w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+#pragma unroll
+                        for (uint32_t q = 0; q < kPieceIds; ++q)
+                            if (q < cnt && e[q] >= lo) add(e[q]);
+                        if (cnt > kPieceIds) bp = min(bp, e[kPieceIds - 1]);
                     }
-                    const uint32_t bound = dropped ? min(bp, ids[kMax - 1]) : bp;
+                    bound = dropped ? min(bp, ids[kMax - 1]) : bp;
+                }
+                mark(16);
+                if constexpr (RTW_COOP_DEAL != 0) {
+                    // the owner's summable ids: ids[0..m) (sorted, <= bound)
+                    uint32_t m = 0;
+                    if (owning) {
+#pragma unroll
+                        for (uint32_t q = 0; q < kMax; ++q) m += (q < n && ids[q] <= bound) ? 1u : 0u;
+                    }
+                    uint32_t incl_m = m;
+#pragma unroll
+                    for (uint32_t off = 1; off < 64; off <<= 1) {
+                        const uint32_t v = (uint32_t)__shfl_up((int)incl_m, off);
+                        if (lane >= off) incl_m += v;
+                    }
+                    const uint32_t fm = incl_m - m, T = (uint32_t)__shfl((int)incl_m, 63);
+                    for (uint32_t r = 0; r < T; r += 64) {
+                        const uint32_t gi = r + lane;
+                        uint32_t own = 0;   // the owner of candidate gi: the last lane whose first is <= gi
+#pragma unroll
+                        for (uint32_t step = 32; step; step >>= 1) {
+                            const uint32_t f = (uint32_t)__shfl((int)fm, (int)(own + step));
+                            own = f <= gi ? own + step : own;
+                        }
+                        const uint32_t q = gi - (uint32_t)__shfl((int)fm, (int)own);
+                        uint32_t id = 0;
+#pragma unroll
+                        for (uint32_t k2 = 0; k2 < kMax; ++k2) {
+                            const uint32_t v = (uint32_t)bperm_i((int32_t)(k2 < n ? ids[k2] : 0u), (int32_t)own);
+                            id = k2 == q ? v : id;
+                        }
+                        RTW_PROBE_LANES(15);
+                        const R val = gi < T ? pdf_at(id, own) : (R)0;
+                        // each owner adds its values of this pass, in list order
+                        const uint32_t g0 = max(fm, r), g1 = min(fm + m, r + 64u);   // its candidates in this pass
+                        const uint32_t q0 = g0 - r, cnt = g1 > g0 ? g1 - g0 : 0u;
+                        uint32_t cmax = cnt;
+#pragma unroll
+                        for (int off = 32; off > 0; off >>= 1) cmax = max(cmax, (uint32_t)__shfl_xor((int)cmax, off));
+                        for (uint32_t jq = 0; jq < cmax; ++jq) {
+                            const R v = bperm_any(val, (int32_t)((q0 + jq) & 63u));
+                            if (jq < cnt) acc = acc + v;
+                        }
+                    }
+                } else {
                     sum_ids(ids, n, bound, acc);
+                }
+                mark(15);
+                if (owning) {
                     if (bound == 0xffffffffu) {
                         more = false;                       // every candidate summed
-                        break;
-                    }
-                    lo = bound + 1u;
-                    if (bound == bp) {                      // a piece's dropped candidates are next
-                        walk_again = true;
-                        break;
+                        owning = false;
+                    } else {
+                        lo = bound + 1u;
+                        if (bound == bp) {                  // a piece's dropped candidates are next
+                            walk_again = true;
+                            owning = false;
+                        }
                     }
                 }
             }
@@ -2126,8 +2217,16 @@ __device__ __forceinline__ double lights_pdf_grid_coop64(const Grid64& sc, bool 
             acc = acc + sphere_pdf_value(mk(L.x, L.y, L.z), L.w, o, d);
         }
     };
+    auto pdf_at = [&](uint32_t id, uint32_t owner) {   // the owner's f64 ray from its stash column
+        auto at = [&](uint32_t q) {
+            return __longlong_as_double((long long)((uint64_t)ray[(2 * q) * 64 + owner] |
+                                                    ((uint64_t)ray[(2 * q + 1) * 64 + owner] << 32)));
+        };
+        const R4<double> L = sc.lights[id];
+        return sphere_pdf_value(mk(L.x, L.y, L.z), L.w, mk(at(0), at(1), at(2)), mk(at(3), at(4), at(5)));
+    };
     return lights_pdf_grid_coop_list<double>(g, sc.lg_rec, sc.lg_id, sc.big, of, df, ia, pend, P, slots, cap_words,
-                                             lane, lw, cand, big_hit, sum_ids, mark);
+                                             lane, lw, cand, big_hit, sum_ids, pdf_at, mark);
 }
 
 // Light list with quads (DevScene::lref set): HittableList::pdf_value over

@@ -283,7 +283,7 @@ static __device__ unsigned long long g_lanes[2 * 16];
             atomicAdd(&g_lanes[2 * (id) + 1], 1ull); \
         } \
     } while (0)
-extern "C" int rtw_probe_lanes_read(unsigned long long* out, int reset) {
+extern "C" int RTW_CAT(rtw_probe_lanes_read_, RTW_PROF)(unsigned long long* out, int reset) {
     if (hipDeviceSynchronize() != hipSuccess) return -1;
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_lanes), sizeof g_lanes) != hipSuccess) return -1;
     if (reset) {
@@ -297,7 +297,7 @@ extern "C" int rtw_probe_lanes_read(unsigned long long* out, int reset) {
 #endif
 
 #ifdef RTW_CLOCK
-constexpr int kClkParts = 16;
+constexpr int kClkParts = 20;
 static __device__ unsigned long long g_clk[kClkParts];
 #define RTW_PROBE_CLK_INIT() \
     __shared__ unsigned long long clk_lds_[kWavesPerBlock][kClkParts]; \

@@ -20,7 +20,8 @@ VAR = os.path.join(ROOT, "build", "variants", "clock")
 PARTS = {0: "item pool + sample start", 1: "planes", 2: "closest hit", 3: "hit record", 4: "Lambertian",
          5: "light pdf", 6: "specular (one pass)", 7: "Metal", 8: "Dielectric", 9: "sample end",
          10: "wave tail", 11: "cooperative grid walk (stash, unstash)", 12: "loop head",
-         13: "grid walk: setup", 14: "grid walk: pieces", 15: "grid walk: owners' sums"}
+         13: "grid walk: setup", 14: "grid walk: pieces", 15: "grid walk: owners' pdf sums",
+         16: "grid walk: owners' merges"}
 CONFIGS = {"C2": (11, 1200, 800, 500), "C3": (50, 1920, 1080, 1024), "C5": (500, 1920, 1080, 256)}
 
 
@@ -46,7 +47,7 @@ def run(a):
     import ray_tracing_weekend_amd as rtw
     rd = getattr(rtw._lib, f"rtw_probe_clock_read_{a.precision}")
     rd.argtypes = [C.c_void_p, C.c_int]
-    buf = (C.c_ulonglong * 16)()
+    buf = (C.c_ulonglong * 20)()
     n, w, h, spp = CONFIGS[a.config]
     soa, b = rtw.scenes.simple_soa(0x5EED0001, n)
     cam = b.with_image_width(w).with_image_height(h).with_samples_per_pixel(a.spp or spp).with_max_depth(50).build()

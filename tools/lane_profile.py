@@ -17,7 +17,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 VAR = os.path.join(ROOT, "build", "variants", "prof")
 NAMES = {1: "bvh inner step", 2: "leaf tests", 3: "segment loop (wave)", 4: "segment (active lanes)",
          5: "own-sphere f64 test", 6: "closest-hit query", 7: "Metal", 8: "Dielectric", 9: "Lambertian",
-         10: "next sample", 11: "grid walk: piece (f32 coop)", 12: "grid walk: light slot (f32 coop, 4 per cell)"}
+         10: "next sample", 11: "grid walk: piece (f32 coop)", 12: "grid walk: light slot (f32 coop, 4 per cell)",
+         13: "f64 walk: owner merge iteration", 14: "f64 walk: merged piece slot", 15: "f64 walk: dealt pdf pass"}
 CONFIGS = {"C2": (11, 1200, 800, 500), "C3": (50, 1920, 1080, 1024), "C5": (500, 1920, 1080, 256)}
 
 
@@ -26,11 +27,14 @@ def build():
     b = os.path.join(ROOT, "ray_tracing_weekend_amd", "build")
     os.makedirs(VAR, exist_ok=True)
     subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "-fno-slp-vectorize", "--offload-arch=gfx950",
-                    f"-I{cs}", f"-I{ROOT}/include", "-ffp-contract=on", "-DRTW_PROF", "-c", f"{cs}/render_f32.hip",
+                    f"-I{cs}", f"-I{ROOT}/include", "-ffp-contract=on", "-DRTW_PROF=f32", "-c", f"{cs}/render_f32.hip",
                     "-o", f"{VAR}/render_f32.o"], check=True)
+    subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "-fno-slp-vectorize", "--offload-arch=gfx950",
+                    f"-I{cs}", f"-I{ROOT}/include", "-ffp-contract=off", "-DRTW_PROF=f64", "-c", f"{cs}/render_f64.hip",
+                    "-o", f"{VAR}/render_f64.o"], check=True)
     subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o", f"{VAR}/librtw.so",
-                    f"{VAR}/render_f32.o", f"{b}/render_f64.o", f"{b}/capi.o", f"{b}/rtw_host.o", f"{b}/bvh.o"],
-                   check=True)
+                    f"{VAR}/render_f32.o", f"{VAR}/render_f64.o", f"{b}/capi.o", f"{b}/rtw_host.o", f"{b}/bvh.o",
+                    "-ldl"], check=True)
     print("built", f"{VAR}/librtw.so")
 
 
@@ -38,13 +42,13 @@ def run(a):
     os.environ["RTW_LIB_OVERRIDE"] = os.path.join(VAR, "librtw.so")
     sys.path.insert(0, ROOT)
     import ray_tracing_weekend_amd as rtw
-    rd = rtw._lib.rtw_probe_lanes_read
+    rd = getattr(rtw._lib, f"rtw_probe_lanes_read_{a.precision}")
     rd.argtypes = [C.c_void_p, C.c_int]
     buf = (C.c_ulonglong * 32)()
     n, w, h, _ = CONFIGS[a.config]
     soa, b = rtw.scenes.simple_soa(0x5EED0001, n)
     cam = b.with_image_width(w).with_image_height(h).with_samples_per_pixel(a.spp).with_max_depth(50).build()
-    with rtw.Renderer(precision=rtw.RTW_F32) as r:
+    with rtw.Renderer(precision=rtw.RTW_F64 if a.precision == "f64" else rtw.RTW_F32) as r:
         for kv in filter(None, a.tuning.split(",")):
             k, v = kv.split("=")
             r.set_tuning(k, int(v))
@@ -54,7 +58,7 @@ def run(a):
         st = r.get_stats()
         assert rd(buf, 1) == 0
     segs = st.segments
-    out = {"config": a.config, "tuning": a.tuning, "spp": a.spp, "segments": segs, "phases": {}}
+    out = {"config": a.config, "precision": a.precision, "tuning": a.tuning, "spp": a.spp, "segments": segs, "lambertian": st.lambertian, "phases": {}}
     for i, name in NAMES.items():
         lanes, passes = buf[2 * i], buf[2 * i + 1]
         if passes:
@@ -70,6 +74,7 @@ def main():
     ap.add_argument("--tuning", default="")
     ap.add_argument("--spp", type=int, default=500)
     ap.add_argument("--config", default="C2")
+    ap.add_argument("--precision", default="f32")
     a = ap.parse_args()
     build() if a.mode == "build" else run(a)
 
