@@ -3032,20 +3032,28 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                     V3<R> dir;
                     const bool to_light = PR::u_std(g.next()) < (R)0.5;
                     bool sampled = false;
+                    bool nan_dir = false;   // (light kernels) an empty light list: a NaN direction
                     if (to_light && (kargs()->sc.n_list == 0 || (kPrims && kargs()->sc.lref))) {
-                        sampled = true;
                         // HittableList::random (hittable_list.rs:414-419): a
                         // uniform light (one gen_index draw), then its random()
-                        // (no lref list without kPrims: the light kernels drop that code;
-                        // the others keep it -- dropped there, the f64 Book-1 kernel's
-                        // registers were allocated worse: +0.5 %)
-                        if ((kLightBvh && !kPrims) || kargs()->sc.n_list == 0) {
+                        // (no lref list without kPrims: the light kernels drop that code
+                        // and take an empty list's NaN direction below, as a select after
+                        // the cosine lobe's draws -- a direction assigned on two paths was
+                        // spilled at every Lambertian bounce; the Book-1 kernels keep this
+                        // code -- dropped there, the f64 kernel's registers were allocated
+                        // worse: +0.5 %)
+                        if constexpr (kLightBvh && !kPrims) {
+                            nan_dir = true;
+                            atomicAdd(p.counters + 5, 1ull);
+                        } else if (kargs()->sc.n_list == 0) {
                             // an empty list panics there (:417): counted; the
                             // sample goes on along a NaN direction and ends NaN
                             // at its next world query, as in the oracle
+                            sampled = true;
                             atomicAdd(p.counters + 5, 1ull);
                             dir = mk((R)NAN, (R)NAN, (R)NAN);
                         } else {
+                            sampled = true;
                             const uint32_t ref = kargs()->sc.lref[g.index(kargs()->sc.n_list)];
                             if (ref & kLrefQuad) {
                                 dir = quad_random(kargs()->sc.lquads + kQuadR * (ref & 0x3fffffffu), pnt, g);
@@ -3064,7 +3072,8 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                         // a sphere light (one gen_index draw, then Sphere::random)
                         // or the cosine lobe, in one pass (mixture_direction)
                         R4<R> L = R4<R>{0, 0, 0, 0};
-                        if (to_light) {
+                        const bool tl = to_light && !nan_dir;
+                        if (tl) {
                             lsel = (int32_t)g.index(kargs()->sc.n_lights);
                             L = li[lsel];
                         }
@@ -3076,13 +3085,17 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                                 nl = sphere_normal64(pnt64, kargs()->sc.sph64[best - sbase]);
                                 if (!front64(d64, nl)) nl = -nl;
                             }
-                            dir64l = mixture_direction<double>(to_light, nl, V3<double>{(double)L.x, (double)L.y, (double)L.z},
+                            dir64l = mixture_direction<double>(tl, nl, V3<double>{(double)L.x, (double)L.y, (double)L.z},
                                                                (double)L.w, pnt64, g);
                             dir = from64<R>(dir64l);
                             have64 = true;
                         } else {
-                            dir = mixture_direction(to_light, nrm, mk(L.x, L.y, L.z), L.w, pnt, g);
+                            dir = mixture_direction(tl, nrm, mk(L.x, L.y, L.z), L.w, pnt, g);
                         }
+                    }
+                    if constexpr (kLightBvh && !kPrims) {
+                        dir = nan_dir ? mk((R)NAN, (R)NAN, (R)NAN) : dir;
+                        dir64l = nan_dir ? V3<double>{(double)NAN, (double)NAN, (double)NAN} : dir64l;
                     }
                     RTW_PROBE_LAMBERT_DIR();
                     RTW_PROBE_CLK(4);
