@@ -1098,11 +1098,12 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
     // profiles/r04_w_grid_piece_sweep.jsonl)
     const uint32_t grid_w = std::max(p.sc.lg_n[0], std::max(p.sc.lg_n[1], p.sc.lg_n[2]));
     // r05: the f64 walk runs in f32 too, but each piece also keeps and merges
-    // candidate list indices: 11..24 cells (C3 11: 626 -> 613 ms at half spp;
-    // C5 22; profiles/r05_piece_sweep.jsonl)
+    // candidate list indices: 16..24 cells, the longest a trip may cut (pieces
+    // are sized per trip below it: C3 16 vs 11: 554 -> 546 ms at half spp; C5
+    // 22; profiles/r05_piece_sweep.jsonl, r05_piece_sweep_final.jsonl)
     p.grid_piece = c->grid_piece != rtw_ctx::kGridPieceAuto
                        ? c->grid_piece
-                       : (sizeof(R) == 8 ? std::max(11u, std::min(24u, grid_w / 7u))
+                       : (sizeof(R) == 8 ? std::max(16u, std::min(24u, grid_w / 7u))
                                          : std::max(4u, std::min(16u, grid_w / 14u)));
     p.task_table = nullptr;
     p.tile_cost = nullptr;
