@@ -1455,6 +1455,13 @@ __device__ __forceinline__ V3<double> dielectric_dir64(V3<double> u, V3<double> 
 #ifndef RTW_HIT64_LAMB64
 #define RTW_HIT64_LAMB64 1   // hit64 Lambertian: the direction in f64 (r05 default; 0 = in f32)
 #endif
+#ifndef RTW_HIT64_TRIG32
+// hit64 f64 Lambertian direction with the azimuth's sin / cos in f32 (experiment:
+// -1.9 % time, but the f32 paths' statistics fall back to the f32 direction's --
+// 2.793 segments per sample vs f64's 2.764, NaN pixels 15.0 % vs 14.7 %;
+// profiles/r05_hit64_trig32_ab.jsonl)
+#define RTW_HIT64_TRIG32 0
+#endif
 #ifndef RTW_HIT64_REF_SPHERE
 #define RTW_HIT64_REF_SPHERE 0   // hit64 Metal: 1 = the reference's f64 rejection loop (experiment)
 #endif
@@ -3085,8 +3092,8 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                                 nl = sphere_normal64(pnt64, kargs()->sc.sph64[best - sbase]);
                                 if (!front64(d64, nl)) nl = -nl;
                             }
-                            dir64l = mixture_direction<double>(tl, nl, V3<double>{(double)L.x, (double)L.y, (double)L.z},
-                                                               (double)L.w, pnt64, g);
+                            dir64l = mixture_direction<double, RTW_HIT64_TRIG32 != 0>(
+                                tl, nl, V3<double>{(double)L.x, (double)L.y, (double)L.z}, (double)L.w, pnt64, g);
                             dir = from64<R>(dir64l);
                             have64 = true;
                         } else {

@@ -456,7 +456,9 @@ __device__ __forceinline__ V3<R> sphere_random(V3<R> c, R radius, V3<R> o, Rng& 
 // the operations are those of the separate sampler, so the result is the
 // same bit for bit (f64: the oracle's rtwo_sphere_random /
 // rtwo_cosine_hemisphere).
-template <typename R>
+// kTrig32 (the f32 kernels' f64 Lambertian direction, RTW_HIT64_LAMB64): the
+// azimuth's sine and cosine by the f32 hardware instructions, the rest in R
+template <typename R, bool kTrig32 = false>
 __device__ __forceinline__ V3<R> mixture_direction(bool to_light, V3<R> n, V3<R> c, R radius, V3<R> o, Rng& g) {
     // one Onb per lane: the light direction's (Sphere::random) or the normal's
     // (CosinePdf::generate), built by the same code for both
@@ -472,7 +474,14 @@ __device__ __forceinline__ V3<R> mixture_direction(bool to_light, V3<R> n, V3<R>
     const R r1 = P<R>::u_std(g.next());
     const R r2 = P<R>::u_std(g.next());
     R s, cph;
-    P<R>::sincos_2pi(to_light ? r2 : r1, &s, &cph);
+    if constexpr (kTrig32 && sizeof(R) == 8) {
+        float sf, cf;
+        P<float>::sincos_2pi((float)(to_light ? r2 : r1), &sf, &cf);
+        s = (R)sf;
+        cph = (R)cf;
+    } else {
+        P<R>::sincos_2pi(to_light ? r2 : r1, &s, &cph);
+    }
     const R t = P<R>::sqrt_((R)1 - (to_light ? q : r2));   // light: sqrt(1 - r^2/d^2); cosine: z
     R z, sxy;
     if constexpr (sizeof(R) == 4) {
