@@ -85,6 +85,9 @@ def parse():
                     help="skip the secondary single-GPU lines (f64 parity mode, f32 without f64 hit points)")
     ap.add_argument("--accel", choices=["auto", "brute", "bvh"], default="auto")
     ap.add_argument("--tuning", default="", help="rtw_set_tuning overrides, e.g. bvh_kind=1,auto_chunk=4")
+    ap.add_argument("--balance", type=int, default=1,
+                    help="N > 1: deal the tiles to the ranks by their counted costs (1, the default) or keep the "
+                         "round robin (0)")
     return ap.parse_args()
 
 
@@ -362,6 +365,23 @@ def make_step(render, assemble, dist, rank, world_size, buf, gathered, image):
     return step
 
 
+def balance_split(local_costs, dist, device, deal, set_split):
+    """The cost-dealt rank split of the one-process-per-GPU launch (DESIGN.md
+    §7): `local_costs` = this rank's counted tile costs (uint32 [n_tiles],
+    its own tiles filled, zeros elsewhere: rtw_tile_costs after one counting
+    render), summed over the ranks by ONE all-reduce (the tiles are disjoint,
+    so the sum is every tile's cost) -- a planning exchange, once per scene and
+    camera, outside the timed steps -- then dealt on every rank by the same
+    deterministic rtw_split_deal, so every rank holds the same split.  Returns
+    (split, costs)."""
+    t = torch.from_numpy(np.asarray(local_costs, np.int64)).to(device)
+    dist.all_reduce(t)
+    cost = t.cpu().numpy().astype(np.uint32)
+    split = deal(cost)
+    set_split(split, cost)
+    return split, cost
+
+
 CONFIGS = {   # BASELINE configs[2] and configs[4] (SURVEY.md §8 C3 / C5), one GPU each
     "C3": dict(n=50, w=1920, h=1080, spp=1024, steps=2, warmup=1),
     "C5": dict(n=500, w=1920, h=1080, spp=256, steps=1, warmup=1),
@@ -487,6 +507,8 @@ def main():
         k, v = kv.split("=")
         r.set_tuning(k, int(v))
     r.set_scene(scene)
+    r.set_tuning("balance", a.balance)
+    plan = None
     assert rtw.tile_size() == sharding.TILE
     image = torch.empty((H, W, 3), dtype=tdtype, device=dev) if rank == 0 else None
     stream = rtw.torch_stream(dev.index)
@@ -518,6 +540,19 @@ def main():
 
         def sync():
             torch.cuda.synchronize(dev)
+        if dist is not None and a.balance:
+            # the tiles dealt to the ranks by their costs: one counting render (the
+            # round robin, tile index order), the costs all-reduced, the same deal on
+            # every rank (the in-process path does this inside rtw_render_image_device)
+            t0 = time.perf_counter()
+            render(999, buf)
+            sync()
+            balance_split(r.tile_costs(cam, rank, world_size), dist, dev,
+                          lambda c: rtw.split_deal(c, W, H, world_size),
+                          lambda s, c: r.set_split(W, H, world_size, s, c))
+            plan = {"renders": 1, "s": round(time.perf_counter() - t0, 3),
+                    "what": "one counting render + one all-reduce of the tile costs + rtw_split_deal, before "
+                            "the warm-up"}
     elapsed = run_steps(step, a.steps, a.warmup, dist, sync, device=dev)
 
     # live per-launch kernel times of the timed steps (HIP events on the launch
@@ -565,7 +600,9 @@ def main():
                 f"{n_li} lights), per-(pixel,sample) xoshiro256++ streams",
         "config": {"workload": f"book1_simple_{W}x{H}_{SPP}spp_depth{DEPTH}", "width": W,
                    "height": H, "spp": SPP, "max_depth": DEPTH, "spheres": n_sph,
-                   "lights": n_li, "parallelism": f"tile8x8_interleave{world_size}",
+                   "lights": n_li,
+                   "parallelism": (f"tile8x8_cost_dealt{world_size}" if world_size > 1 and a.balance
+                                   else f"tile8x8_interleave{world_size}"),
                    "launch": {"torchrun": "one process per GPU (torch.distributed, RCCL gather)",
                               "inproc": "one process, rtw_create_devices (one rank per GPU, RCCL gather)",
                               "single": "one GPU"}[launch],
@@ -594,6 +631,8 @@ def main():
     }
     if per_rank_ms is not None:
         out["roofline"]["kernel_ms_per_rank"] = per_rank_ms
+    if plan is not None:
+        out["config"]["split_plan"] = plan
     attach_pmc(out["roofline"], out["config"]["workload"], kname, sha,
                chunk_sum_bytes=W * H * -(-SPP // int(st.chunk)) * 3 * (4 if prec == rtw.RTW_F32 else 8) // world_size)
     if world_size == 1 and not a.no_modes:

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define RTW_ABI_VERSION 9
+#define RTW_ABI_VERSION 10
 
 /* error codes */
 #define RTW_OK 0
@@ -328,9 +328,54 @@ uint32_t rtw_tiles_for_rank(uint32_t image_width, uint32_t image_height, uint32_
 /* The gathered packed tiles of all ranks -> the image [H][W][3] (sums, j = 0
  * bottom row), on the device: d_ranks holds nranks rank buffers, each
  * rank_stride_bytes apart (>= rank 0's packed size; equal-size buffers as an
- * RCCL gather delivers them).  Asynchronous on `stream`. */
+ * RCCL gather delivers them).  Follows the context's split for (W, H,
+ * nranks) (rtw_set_split; the round robin without one).  Asynchronous on
+ * `stream`. */
 int rtw_assemble_tiles(rtw_ctx *ctx, const void *d_ranks, size_t rank_stride_bytes, uint32_t nranks,
                        uint32_t image_width, uint32_t image_height, void *d_image, void *stream);
+
+/* ---- cost-balanced rank split (ABI 10) ---------------------------------
+ * The round robin (T mod nranks) gives every rank the same NUMBER of tiles
+ * but not the same work: a rank's share of glass and mirror tiles varies.
+ * The reference balances dynamically -- one rayon task per pixel,
+ * work-stealing over every host core (camera.rs:340-353); across GPUs the
+ * tiles are dealt once by their costs instead.  A split keeps the round
+ * robin's per-rank tile counts (rtw_tiles_for_rank), so packed buffers and the
+ * gather stay the same size, and the image does not depend on the split. */
+#define RTW_MAX_RANKS 256
+/* Deal the tiles of a W x H image (n_tiles = ceil(W/8) * ceil(H/8) entries of
+ * tile_cost, any cost unit) to nranks ranks: costliest first (ties: lower
+ * tile index), each to the rank of least dealt cost (ties: lower rank) that
+ * still has room below its round-robin count.  Writes tile_rank[n_tiles].
+ * Deterministic: every process dealing the same costs gets the same split. */
+int rtw_split_deal(const uint32_t *tile_cost, uint32_t image_width, uint32_t image_height,
+                   uint32_t nranks, uint32_t *tile_rank);
+/* Renders (rtw_render_device with this nranks, and the multi-device paths)
+ * and rtw_assemble_tiles of a W x H image over nranks ranks follow this split
+ * from now on: rank r renders the tiles T with tile_rank[T] == r, packed in
+ * increasing T.  tile_rank == NULL restores the round robin.  tile_cost
+ * (optional, n_tiles) orders each rank's tasks longest first without a
+ * counting render.  RTW_E_INVALID unless every rank r gets exactly
+ * rtw_tiles_for_rank(W, H, r, nranks) tiles.  A multi-device context sets it
+ * on every rank. */
+int rtw_set_split(rtw_ctx *ctx, uint32_t image_width, uint32_t image_height, uint32_t nranks,
+                  const uint32_t *tile_rank, const uint32_t *tile_cost);
+/* The split renders of (W, H, nranks) follow: 0 = the round robin (tile_rank
+ * untouched), 1 = set by rtw_set_split, 2 = dealt by the context itself
+ * (tuning "balance"); for 1 and 2 tile_rank (may be NULL) receives it. */
+int rtw_get_split(rtw_ctx *ctx, uint32_t image_width, uint32_t image_height, uint32_t nranks,
+                  uint32_t *tile_rank);
+/* The tile costs the context counted in its first render of (cam, rank,
+ * nranks) under its current split (tuning "lpt", spp >= "lpt_min_spp": BVH
+ * node visits + sphere tests + 12 per segment of each pixel's first
+ * "lpt_pilot_spp" samples, summed per tile), written to tile_cost[T] for the
+ * rank's tiles T (other entries untouched: the ranks' arrays summed give the
+ * whole image's).  Waits for that render.  RTW_E_INVALID when there is no
+ * such count.  With tuning "balance" (1, the default) a multi-device
+ * context deals its split from these costs by itself: the first
+ * rtw_render_image_device of a camera counts, the second deals and renders
+ * balanced (re-dealt when the scene or camera changes). */
+int rtw_tile_costs(rtw_ctx *ctx, const rtw_camera *cam, uint32_t rank, uint32_t nranks, uint32_t *tile_cost);
 /* Counters of the last render (waits for it to finish).  Returns
  * RTW_E_NO_LIGHTS / RTW_E_PANIC (stats still filled) when a sample reached a
  * reference panic, RTW_E_INVALID before the first render.  A multi-device

@@ -606,6 +606,45 @@ class Renderer:
                                             C.c_void_p(stream) if stream else None),
                     "rtw_assemble_tiles")
 
+    def set_split(self, width: int, height: int, nranks: int, tile_rank=None, tile_cost=None):
+        """Renders and assemblies of a width x height image over nranks ranks
+        follow this tile -> rank split from now on (rtw_set_split, ABI 10);
+        None restores the round robin.  tile_cost orders each rank's tasks."""
+        n = n_tiles(width, height)
+
+        def arr(a):
+            if a is None:
+                return None, None
+            a = np.ascontiguousarray(np.asarray(a, np.uint32).reshape(-1))
+            if a.size != n:
+                raise RenderError(_capi.RTW_E_INVALID, f"split arrays need {n} entries, got {a.size}")
+            return a, a.ctypes.data_as(_capi._u32p)
+        r, rp = arr(tile_rank)
+        c, cp = arr(tile_cost)
+        self._check(_lib.rtw_set_split(self.ctx, width, height, nranks, rp, cp), "rtw_set_split")
+
+    def get_split(self, width: int, height: int, nranks: int):
+        """(kind, tile_rank) of the split renders of this size and rank count
+        follow (rtw_get_split): kind 0 = the round robin (tile_rank None),
+        1 = set by set_split, 2 = dealt by the context itself (balance)."""
+        out = np.zeros(n_tiles(width, height), np.uint32)
+        kind = _lib.rtw_get_split(self.ctx, width, height, nranks, out.ctypes.data_as(_capi._u32p))
+        if kind < 0:
+            self._check(kind, "rtw_get_split")
+        return int(kind), (out if kind else None)
+
+    def tile_costs(self, cam: Camera, rank: int = 0, nranks: int = 1, out=None) -> np.ndarray:
+        """The tile costs this context counted in its first render of (cam,
+        rank, nranks) (rtw_tile_costs): uint32 [n_tiles], the rank's tiles
+        filled in (zeros elsewhere, or `out`'s entries kept).  Waits."""
+        n = n_tiles(cam.image_width, cam.image_height)
+        out = np.zeros(n, np.uint32) if out is None else out
+        if out.dtype != np.uint32 or out.size != n or not out.flags.c_contiguous:
+            raise RenderError(_capi.RTW_E_INVALID, "out must be a contiguous uint32 array of n_tiles")
+        self._check(_lib.rtw_tile_costs(self.ctx, C.byref(cam.raw), rank, nranks, out.ctypes.data_as(_capi._u32p)),
+                    "rtw_tile_costs")
+        return out
+
     def get_timings(self, n: int = 64):
         """(render_ms, total_ms) lists for the last n renders (HIP events)."""
         a, b = (C.c_float * n)(), (C.c_float * n)()
@@ -665,6 +704,25 @@ def tiles_for_rank(width: int, height: int, rank: int, nranks: int) -> int:
 
 def tile_size() -> int:
     return int(_lib.rtw_tile_size())
+
+
+def n_tiles(width: int, height: int) -> int:
+    t = tile_size()
+    return ((width + t - 1) // t) * ((height + t - 1) // t)
+
+
+def split_deal(tile_cost, width: int, height: int, nranks: int) -> np.ndarray:
+    """The tiles dealt to nranks ranks by cost (rtw_split_deal): uint32
+    tile -> rank, each rank keeping its round-robin tile count."""
+    n = n_tiles(width, height)
+    cost = np.ascontiguousarray(np.asarray(tile_cost, np.uint32).reshape(-1))
+    if cost.size != n:
+        raise RenderError(_capi.RTW_E_INVALID, f"tile_cost needs {n} entries, got {cost.size}")
+    out = np.zeros(n, np.uint32)
+    rc = _lib.rtw_split_deal(cost.ctypes.data_as(_capi._u32p), width, height, nranks, out.ctypes.data_as(_capi._u32p))
+    if rc != 0:
+        raise RenderError(rc, "rtw_split_deal failed")
+    return out
 
 
 RTW_STREAM_NULL = 1   # include/rtw.h: the device's null (legacy default) stream

@@ -67,7 +67,7 @@ class rtw_scene(C.Structure):
     ]
 
 
-ABI_VERSION = 9     # RTW_ABI_VERSION of include/rtw.h
+ABI_VERSION = 10    # RTW_ABI_VERSION of include/rtw.h
 
 
 class rtw_stats(C.Structure):
@@ -112,6 +112,10 @@ PROTOTYPES = [
     ("rtw_tiles_for_rank", C.c_uint32, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32]),
     ("rtw_assemble_tiles", C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_uint32, C.c_uint32,
                                      C.c_uint32, C.c_void_p, C.c_void_p]),
+    ("rtw_split_deal", C.c_int, [_u32p, C.c_uint32, C.c_uint32, C.c_uint32, _u32p]),
+    ("rtw_set_split", C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, _u32p, _u32p]),
+    ("rtw_get_split", C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, _u32p]),
+    ("rtw_tile_costs", C.c_int, [C.c_void_p, C.POINTER(rtw_camera), C.c_uint32, C.c_uint32, _u32p]),
     ("rtw_get_stats", C.c_int, [C.c_void_p, C.POINTER(rtw_stats)]),
     ("rtw_get_stats_rank", C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(rtw_stats)]),
     ("rtw_get_timings", C.c_int, [C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_float), C.c_int]),

@@ -103,6 +103,12 @@ struct rtw_ctx {
     uint64_t scene_serial = 0;        // ++ per rtw_upload_scene
     static constexpr uint32_t kMaxGroup = 32;
     uint32_t max_group = kMaxGroup;   // longest-first task list: at most this many chunks per task
+    // longest-first task list with guided sizes (lpt_tasks; guide_div 0: equal-cost
+    // tasks of max_group chunks at most): a task costs the remaining work / guide_div,
+    // at least total / guide_floor, at most guide_max chunks
+    uint32_t guide_div = 8192, guide_max = 4095;
+    uint32_t cost_time = 1;           // tile costs in wave-time shares (KParams::cost_time); 0: work counts
+    uint64_t guide_floor = 1u << 18;
     void* d_lpt = nullptr;            // pilot: [tile cost | chunk sums | tiles]
     size_t lpt_cap = 0;
     bool lpt_valid = false;           // h_lpt_cost is the pilot of (lpt_cam, lpt_serial, rank split, precision)
@@ -111,6 +117,7 @@ struct rtw_ctx {
     rtw_camera lpt_cam{};
     uint64_t lpt_serial = 0;
     uint32_t lpt_rank = 0, lpt_nranks = 0, lpt_prec = 0;
+    uint64_t lpt_split = 0;           // ... and split id (split_id: 0 = the round robin)
     std::vector<uint32_t> h_lpt_cost;
     void* d_lpt_tasks = nullptr;      // the task list of (h_lpt_cost, lpt_tab_*)
     size_t lpt_tasks_cap = 0;
@@ -145,6 +152,30 @@ struct rtw_ctx {
     // ranks whose counters the last render filled (rtw_get_stats): n after
     // rtw_render / rtw_render_image_device, 1 after rtw_render_device
     uint32_t stats_ranks = 1;
+    // Rank split (ABI 10): renders of a split_W x split_H image over split_n
+    // ranks give tile T to rank split_rank[T] (rtw_set_split; empty: T mod n,
+    // the round robin).  Each rank keeps the round robin's tile COUNT, so the
+    // packed buffers and the gather are unchanged.  split_cost: the tile costs
+    // the split was dealt by -- they order the next renders' tasks (no counting
+    // render after a deal).  split_auto: dealt by rtw_render_image_device
+    // (tuning "balance") for split_cam / split_scene, re-dealt when they change.
+    uint32_t split_W = 0, split_H = 0, split_n = 0;
+    uint64_t split_serial = 0;        // ++ per split set: the split's id in the task-order key
+    bool split_auto = false;
+    rtw_camera split_cam{};
+    uint64_t split_scene = 0;
+    std::vector<uint32_t> split_rank, split_cost;
+    uint32_t balance = 1;             // multi-device renders: deal tiles by their counted costs
+    // the device copies of the split: this rank's local tile -> global tile (render
+    // kernel) and global tile -> lt * n + rank (assembly), for split id *_key
+    std::vector<uint32_t> h_tile_map;
+    void* d_tile_map = nullptr;
+    size_t tile_map_cap = 0;
+    uint64_t tile_map_key = 0;
+    uint32_t tile_map_rank = 0;
+    void* d_tile_slot = nullptr;
+    size_t tile_slot_cap = 0;
+    uint64_t tile_slot_key = 0;
 };
 
 namespace {
@@ -833,16 +864,81 @@ int ensure(rtw_ctx* c, void** buf, size_t* cap, size_t bytes) {
     return RTW_OK;
 }
 
-// pixels inside the image of the tiles T = rank (mod nranks)
-uint64_t rank_pixels(uint32_t W, uint32_t H, uint32_t rank, uint32_t nranks) {
-    const uint32_t tiles_x = (W + rtw::kTile - 1) / rtw::kTile, tiles_y = (H + rtw::kTile - 1) / rtw::kTile;
-    const uint64_t n = (uint64_t)tiles_x * tiles_y;
+uint64_t n_tiles_of(uint32_t W, uint32_t H) {
+    return (uint64_t)((W + rtw::kTile - 1) / rtw::kTile) * ((H + rtw::kTile - 1) / rtw::kTile);
+}
+
+// a split is set for renders of this image size and rank count
+bool split_active(const rtw_ctx* c, uint32_t W, uint32_t H, uint32_t nranks) {
+    return !c->split_rank.empty() && c->split_W == W && c->split_H == H && c->split_n == nranks;
+}
+// the id of the split renders of (W, H, nranks) follow: 0 = the round robin
+uint64_t split_id(const rtw_ctx* c, uint32_t W, uint32_t H, uint32_t nranks) {
+    return split_active(c, W, H, nranks) ? c->split_serial : 0;
+}
+
+// the global tiles of `rank`, in the order they are packed (increasing T)
+void local_tiles(const rtw_ctx* c, uint32_t W, uint32_t H, uint32_t rank, uint32_t nranks,
+                 std::vector<uint32_t>& out) {
+    out.clear();
+    const uint64_t n = n_tiles_of(W, H);
+    if (split_active(c, W, H, nranks)) {
+        for (uint64_t T = 0; T < n; ++T)
+            if (c->split_rank[T] == rank) out.push_back((uint32_t)T);
+    } else {
+        for (uint64_t T = rank; T < n; T += nranks) out.push_back((uint32_t)T);
+    }
+}
+
+// pixels inside the image of the rank's tiles
+uint64_t rank_pixels(const rtw_ctx* c, uint32_t W, uint32_t H, uint32_t rank, uint32_t nranks) {
+    const uint32_t tiles_x = (W + rtw::kTile - 1) / rtw::kTile;
+    std::vector<uint32_t> tiles;
+    local_tiles(c, W, H, rank, nranks, tiles);
     uint64_t px = 0;
-    for (uint64_t T = rank; T < n; T += nranks) {
-        const uint32_t tx = (uint32_t)(T % tiles_x), ty = (uint32_t)(T / tiles_x);
+    for (uint32_t T : tiles) {
+        const uint32_t tx = T % tiles_x, ty = T / tiles_x;
         px += (uint64_t)std::min(rtw::kTile, W - tx * rtw::kTile) * std::min(rtw::kTile, H - ty * rtw::kTile);
     }
     return px;
+}
+
+// The device copy of a buffer the kernels read (the split's maps): rewritten
+// only when the split changes, after the device is idle -- a render still
+// queued on another stream may read the old contents.
+int upload_map(rtw_ctx* c, void** buf, size_t* cap, const std::vector<uint32_t>& h) {
+    HIP_TRY(c, hipDeviceSynchronize());
+    int rc = ensure(c, buf, cap, std::max<size_t>(h.size(), 1) * sizeof(uint32_t));
+    if (rc) return rc;
+    if (!h.empty()) HIP_TRY(c, hipMemcpy(*buf, h.data(), h.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    return RTW_OK;
+}
+
+// this rank's local tile -> global tile map of the active split on the device
+int ensure_tile_map(rtw_ctx* c, uint32_t W, uint32_t H, uint32_t rank, uint32_t nranks) {
+    if (c->d_tile_map && c->tile_map_key == c->split_serial && c->tile_map_rank == rank) return RTW_OK;
+    local_tiles(c, W, H, rank, nranks, c->h_tile_map);
+    const int rc = upload_map(c, &c->d_tile_map, &c->tile_map_cap, c->h_tile_map);
+    if (rc) return rc;
+    c->tile_map_key = c->split_serial;
+    c->tile_map_rank = rank;
+    return RTW_OK;
+}
+
+// the assembly's map of the active split: global tile T -> lt * n + rank (the
+// round robin's own index form, so the assembly kernel decodes both alike)
+int ensure_tile_slot(rtw_ctx* c, uint32_t W, uint32_t H, uint32_t nranks) {
+    if (c->d_tile_slot && c->tile_slot_key == c->split_serial) return RTW_OK;
+    std::vector<uint32_t> slot(n_tiles_of(W, H));
+    std::vector<uint32_t> next(nranks, 0);
+    for (size_t T = 0; T < slot.size(); ++T) {
+        const uint32_t k = c->split_rank[T];
+        slot[T] = next[k]++ * nranks + k;
+    }
+    const int rc = upload_map(c, &c->d_tile_slot, &c->tile_slot_cap, slot);
+    if (rc) return rc;
+    c->tile_slot_key = c->split_serial;
+    return RTW_OK;
 }
 
 template <typename R>
@@ -866,6 +962,30 @@ void fill_camera(rtw::KParams<R>& p, const rtw_camera* cam) {
     p.H = cam->image_height;
     p.spp = cam->samples_per_pixel;
     p.max_depth = cam->max_depth;
+}
+
+// The tile costs counted by the last counting render (lpt_pending) -> h_lpt_cost
+// (waits for that render: once per key)
+int lpt_readback(rtw_ctx* c, uint32_t nt) {
+    c->lpt_pending = false;   // (an error below recounts at the next render)
+    HIP_TRY(c, hipEventSynchronize(c->lpt_ev));
+    c->h_lpt_cost.resize(nt);
+    // on the context's own (idle, non-blocking) stream: waits for nothing but the copy
+    if (nt) {
+        HIP_TRY(c, hipMemcpyAsync(c->h_lpt_cost.data(), c->d_lpt, (size_t)nt * sizeof(uint32_t),
+                                  hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+    }
+    c->lpt_valid = true;
+    return RTW_OK;
+}
+
+// the context holds (or has pending) tile costs of this camera, scene, rank and split
+bool lpt_has(const rtw_ctx* c, const rtw_camera* cam, uint32_t rank, uint32_t nranks) {
+    return (c->lpt_valid || c->lpt_pending) && c->lpt_serial == c->scene_serial && c->lpt_rank == rank &&
+           c->lpt_nranks == nranks && c->lpt_prec == (c->precision == RTW_F32 ? 4u : 8u) &&
+           c->lpt_split == split_id(c, cam->image_width, cam->image_height, nranks) &&
+           memcmp(&c->lpt_cam, cam, sizeof *cam) == 0;
 }
 
 // Longest tiles first: a 2-sample-per-pixel pilot render of the rank's tiles
@@ -895,6 +1015,7 @@ int lpt_pilot(rtw_ctx* c, const rtw::KParams<R>& p, int world, size_t launch_lds
     q.partial = d_part;
     q.tile_cost = d_cost;
     q.cost_spp = q.spp;
+    q.cost_time = c->cost_time;
     HIP_TRY(c, hipMemsetAsync(d_cost, 0, (size_t)nt * sizeof(uint32_t), stream));
     HIP_TRY(c, hipMemsetAsync(c->d_counters, 0, rtw_ctx::kCounters * sizeof(unsigned long long), stream));
     int lrc;
@@ -928,7 +1049,32 @@ int lpt_tasks(rtw_ctx* c, const rtw::KParams<R>& p, uint32_t fixed_group, uint64
     const double per_task = total * p.n_chunks / (double)std::max<uint64_t>(target, 1);   // pilot-cost units x chunks
     std::vector<uint32_t>& tab = c->h_lpt_tasks;
     tab.clear();
+    if (!fixed_group && c->guide_div) {
+        // Guided sizes (guided self-scheduling): each task costs about the work
+        // still left after it / guide_div (~ 2 x the resident waves), between
+        // total / guide_floor and guide_max chunks.  The launch starts on large
+        // tasks (few task switches: a wave's lanes then stay on one tile) and
+        // ends on small ones, so the waves run dry together: an 8-rank C2
+        // share's equal-cost 2^17 tasks left 3.4 % of its wave-time idle at the
+        // end and switched tasks 32 times per wave (profiles/r06a_timeline_*).
+        double remaining = total * p.n_chunks;
+        const double floor_cost = total * p.n_chunks / (double)std::max<uint64_t>(c->guide_floor, 1);
+        const uint32_t gmax = std::min<uint32_t>(std::max(c->guide_max, 1u), kTaskMaxChunks);
+        for (uint32_t k : order) {
+            const double ck = (double)std::max<uint32_t>(cost[k], 1);
+            for (uint32_t cb = 0; cb < p.n_chunks;) {
+                const double want = std::max(remaining / (double)c->guide_div, floor_cost) / ck;
+                uint32_t g = (uint32_t)std::max(1.0, std::min((double)gmax, std::floor(want + 0.5)));
+                g = std::min(g, p.n_chunks - cb);
+                tab.push_back(k);
+                tab.push_back(cb | (g << 20));
+                cb += g;
+                remaining -= g * ck;
+            }
+        }
+    }
     for (uint32_t k : order) {
+        if (!fixed_group && c->guide_div) break;
         uint32_t g = fixed_group;
         if (!g) {
             const double want = per_task / (double)std::max<uint32_t>(cost[k], 1);
@@ -965,6 +1111,15 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
     const size_t need_out = (size_t)p.n_local_tiles * 64 * 3 * sizeof(R);
     if (out_bytes < need_out) return fail(c, RTW_E_INVALID, "d_out is smaller than tiles_for_rank*64*3");
     if (need_out && !d_out) return fail(c, RTW_E_INVALID, "d_out is NULL");
+    // the split's local -> global tile map (a dealt split; null: the round robin)
+    const bool split = split_active(c, p.W, p.H, nranks);
+    const uint64_t sid = split_id(c, p.W, p.H, nranks);
+    p.tile_map = nullptr;
+    if (split && p.n_local_tiles) {
+        const int mrc = ensure_tile_map(c, p.W, p.H, rank, nranks);
+        if (mrc) return mrc;
+        p.tile_map = reinterpret_cast<const uint32_t*>(c->d_tile_map);
+    }
     // Work decomposition: ITEM = (pixel, chunk of `chunk` samples) -- the unit
     // a lane folds in sample order; TASK = (8x8 tile, group of chunks) -- one
     // wavefront's dynamic item pool.  Small chunks balance the lanes of a
@@ -1108,6 +1263,7 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
     p.task_table = nullptr;
     p.tile_cost = nullptr;
     p.cost_spp = 0;
+    p.cost_time = 0;
     // Reordering the tiles scatters the tiles in flight over the image: a tree
     // larger than an XCD's L2 (4 MiB) loses its locality (C5, 1M spheres,
     // ~100 MB: +8 %), so by default only worlds held in LDS or small enough
@@ -1117,7 +1273,7 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
         p.max_depth && p.n_local_tiles > 1 && p.n_chunks < (1u << 20)) {
         const bool same = (c->lpt_valid || c->lpt_pending) && c->lpt_serial == c->scene_serial &&
                           c->lpt_rank == rank && c->lpt_nranks == nranks && c->lpt_prec == (uint32_t)sizeof(R) &&
-                          memcmp(&c->lpt_cam, cam, sizeof *cam) == 0;
+                          c->lpt_split == sid && memcmp(&c->lpt_cam, cam, sizeof *cam) == 0;
         const bool dbg = getenv("RTW_DEBUG_LPT") != nullptr;   // cold-render cost breakdown (stderr)
         auto now = [] { return std::chrono::steady_clock::now(); };
         auto t0 = now();
@@ -1127,8 +1283,17 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
             c->lpt_rank = rank;
             c->lpt_nranks = nranks;
             c->lpt_prec = (uint32_t)sizeof(R);
+            c->lpt_split = sid;
         };
-        if (!same && c->lpt_inline) {
+        if (!same && split && !c->split_cost.empty()) {
+            // a split dealt by tile costs: those costs order this rank's tasks (no counting)
+            c->lpt_pending = false;
+            c->lpt_tab_valid = false;
+            c->h_lpt_cost.resize(p.n_local_tiles);
+            for (uint32_t k = 0; k < p.n_local_tiles; ++k) c->h_lpt_cost[k] = c->split_cost[c->h_tile_map[k]];
+            c->lpt_valid = true;
+            keep_key();
+        } else if (!same && c->lpt_inline) {
             // this render counts its tiles' costs on the way (plain tile order);
             // the key is kept and the counts marked pending only once lpt_ev is
             // recorded after the launch (below), so a failed launch leaves no
@@ -1144,6 +1309,7 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
             HIP_TRY(c, hipMemsetAsync(c->d_lpt, 0, (size_t)nt * sizeof(uint32_t), stream));
             p.tile_cost = reinterpret_cast<uint32_t*>(c->d_lpt);
             p.cost_spp = std::min(p.spp, std::max(c->lpt_pilot_spp, 1u));
+            p.cost_time = c->cost_time;
         } else if (!same) {
             c->lpt_valid = c->lpt_pending = false;
             c->lpt_tab_valid = false;
@@ -1157,17 +1323,10 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
             HIP_TRY(c, hipMemsetAsync(c->d_counters, 0, rtw_ctx::kCounters * sizeof(unsigned long long), stream));
         } else if (c->lpt_pending) {
             // the counts of the render before (waits for it: once per key)
-            const uint32_t nt = p.n_local_tiles;
-            c->lpt_pending = false;   // (an error below recounts at the next render)
-            HIP_TRY(c, hipEventSynchronize(c->lpt_ev));
-            c->h_lpt_cost.resize(nt);
-            // on the context's own (idle, non-blocking) stream: waits for nothing but the copy
-            HIP_TRY(c, hipMemcpyAsync(c->h_lpt_cost.data(), c->d_lpt, (size_t)nt * sizeof(uint32_t),
-                                      hipMemcpyDeviceToHost, c->stream));
-            HIP_TRY(c, hipStreamSynchronize(c->stream));
-            c->lpt_valid = true;
+            rc = lpt_readback(c, p.n_local_tiles);
+            if (rc) return rc;
             if (dbg) fprintf(stderr, "lpt counts read back %.3f ms (%u tiles)\n",
-                             std::chrono::duration<double, std::milli>(now() - t0).count(), nt);
+                             std::chrono::duration<double, std::milli>(now() - t0).count(), p.n_local_tiles);
             t0 = now();
         }
         const uint64_t target = c->target_tasks ? c->target_tasks : kAutoTasks;
@@ -1213,13 +1372,14 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
         c->lpt_rank = rank;
         c->lpt_nranks = nranks;
         c->lpt_prec = (uint32_t)sizeof(R);
+        c->lpt_split = sid;
         c->lpt_pending = true;
     }
     HIP_TRY(c, hipEventRecord(c->ev1, stream));
     HIP_TRY(c, hipEventRecord(ev[2], stream));
     ++c->n_renders;
     c->last = rtw_stats{};
-    c->last.samples = rank_pixels(p.W, p.H, rank, nranks) * p.spp;
+    c->last.samples = rank_pixels(c, p.W, p.H, rank, nranks) * p.spp;
     c->last.accel = (uint32_t)accel;
     c->last.bvh_width = bvh_width;
     c->last.kernel = (uint32_t)world;
@@ -1403,6 +1563,8 @@ void rtw_destroy(rtw_ctx* c) {
     if (c->d_counters) (void)hipFree(c->d_counters);
     if (c->d_lpt) (void)hipFree(c->d_lpt);
     if (c->d_lpt_tasks) (void)hipFree(c->d_lpt_tasks);
+    if (c->d_tile_map) (void)hipFree(c->d_tile_map);
+    if (c->d_tile_slot) (void)hipFree(c->d_tile_slot);
     if (c->lpt_ev) (void)hipEventDestroy(c->lpt_ev);
     for (auto& tri : c->ring)
         for (auto& e : tri)
@@ -1455,6 +1617,11 @@ int rtw_set_tuning(rtw_ctx* c, const char* key, int64_t value) {
     else if (k == "bvh_kind") c->bvh_kind = (int)std::min<int64_t>(value, 3);
     else if (k == "bvh_lds_max") c->bvh_lds_max = (size_t)std::min<int64_t>(value, kLdsLimit);
     else if (k == "auto_accel") c->auto_accel = (int)std::min<int64_t>(value, RTW_ACCEL_BVH);
+    else if (k == "balance") c->balance = value ? 1u : 0u;
+    else if (k == "cost_time") c->cost_time = value ? 1u : 0u;
+    else if (k == "guide_div") { c->guide_div = (uint32_t)std::min<int64_t>(value, 1 << 24); c->lpt_tab_valid = false; }
+    else if (k == "guide_max") { c->guide_max = (uint32_t)std::min<int64_t>(std::max<int64_t>(value, 1), 4095); c->lpt_tab_valid = false; }
+    else if (k == "guide_floor") { c->guide_floor = std::max<uint64_t>(1, (uint64_t)value); c->lpt_tab_valid = false; }
     else return fail(c, RTW_E_INVALID, "unknown tuning key " + k);
     return RTW_OK;
 }
@@ -1655,6 +1822,116 @@ uint32_t rtw_tiles_for_rank(uint32_t W, uint32_t H, uint32_t rank, uint32_t nran
     return rank < n ? (uint32_t)((n - rank + nranks - 1) / nranks) : 0u;
 }
 
+int rtw_split_deal(const uint32_t* tile_cost, uint32_t W, uint32_t H, uint32_t nranks, uint32_t* tile_rank) {
+    if (nranks == 0 || nranks > RTW_MAX_RANKS) return RTW_E_INVALID;
+    const uint64_t n = n_tiles_of(W, H);
+    if (n > 0xFFFFFFFFull / nranks) return RTW_E_UNSUPPORTED;
+    if (n && (!tile_cost || !tile_rank)) return RTW_E_INVALID;
+    // costliest tiles first (ties: lower index), each to the rank of least dealt
+    // cost (ties: lower rank) among those below their round-robin tile count
+    std::vector<uint32_t> order(n);
+    for (uint64_t T = 0; T < n; ++T) order[T] = (uint32_t)T;
+    std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return tile_cost[a] > tile_cost[b]; });
+    std::vector<uint64_t> load(nranks, 0);
+    std::vector<uint32_t> room(nranks);
+    for (uint32_t r = 0; r < nranks; ++r) room[r] = rtw_tiles_for_rank(W, H, r, nranks);
+    for (uint32_t T : order) {
+        uint32_t best = nranks;
+        for (uint32_t r = 0; r < nranks; ++r)
+            if (room[r] && (best == nranks || load[r] < load[best])) best = r;
+        tile_rank[T] = best;
+        load[best] += tile_cost[T];
+        --room[best];
+    }
+    return RTW_OK;
+}
+}  // extern "C"
+
+namespace {
+// the split (and its costs) on one rank context; tile_rank NULL: the round robin
+int apply_split(rtw_ctx* c, uint32_t W, uint32_t H, uint32_t nranks, const uint32_t* tile_rank,
+                const uint32_t* tile_cost, bool automatic, const rtw_camera* cam) {
+    if (!tile_rank) {
+        c->split_rank.clear();
+        c->split_cost.clear();
+        c->split_W = c->split_H = c->split_n = 0;
+        c->split_auto = false;
+        return RTW_OK;
+    }
+    const uint64_t n = n_tiles_of(W, H);
+    c->split_rank.assign(tile_rank, tile_rank + n);
+    if (tile_cost) c->split_cost.assign(tile_cost, tile_cost + n);
+    else c->split_cost.clear();
+    c->split_W = W;
+    c->split_H = H;
+    c->split_n = nranks;
+    ++c->split_serial;
+    c->split_auto = automatic;
+    if (cam) c->split_cam = *cam;
+    c->split_scene = c->scene_serial;
+    return RTW_OK;
+}
+
+int check_split(uint32_t W, uint32_t H, uint32_t nranks, const uint32_t* tile_rank) {
+    if (nranks == 0 || nranks > RTW_MAX_RANKS) return RTW_E_INVALID;
+    const uint64_t n = n_tiles_of(W, H);
+    if (n > 0xFFFFFFFFull / nranks) return RTW_E_UNSUPPORTED;
+    if (!tile_rank) return RTW_OK;
+    std::vector<uint32_t> cnt(nranks, 0);
+    for (uint64_t T = 0; T < n; ++T) {
+        if (tile_rank[T] >= nranks) return RTW_E_INVALID;
+        ++cnt[tile_rank[T]];
+    }
+    for (uint32_t r = 0; r < nranks; ++r)
+        if (cnt[r] != rtw_tiles_for_rank(W, H, r, nranks)) return RTW_E_INVALID;
+    return RTW_OK;
+}
+
+// The tile costs the context counted for (cam, rank, nranks) under its split,
+// scattered into cost[global tile]; waits for a pending counting render.
+int tile_costs_of(rtw_ctx* c, const rtw_camera* cam, uint32_t rank, uint32_t nranks, uint32_t* cost) {
+    if (!lpt_has(c, cam, rank, nranks))
+        return fail(c, RTW_E_INVALID, "no tile costs for this camera, scene and rank split: render once with "
+                                      "tuning lpt on and spp >= lpt_min_spp first");
+    HIP_TRY(c, hipSetDevice(c->device));
+    const uint32_t W = cam->image_width, H = cam->image_height;
+    std::vector<uint32_t> tiles;
+    local_tiles(c, W, H, rank, nranks, tiles);
+    if (c->lpt_pending) {
+        const int rc = lpt_readback(c, (uint32_t)tiles.size());
+        if (rc) return rc;
+    }
+    if (c->h_lpt_cost.size() != tiles.size()) return fail(c, RTW_E_INVALID, "tile cost count mismatch");
+    for (size_t k = 0; k < tiles.size(); ++k) cost[tiles[k]] = c->h_lpt_cost[k];
+    return RTW_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int rtw_set_split(rtw_ctx* c, uint32_t W, uint32_t H, uint32_t nranks, const uint32_t* tile_rank,
+                  const uint32_t* tile_cost) {
+    if (!c) return RTW_E_INVALID;
+    const int rc = check_split(W, H, nranks, tile_rank);
+    if (rc) return fail(c, rc, "bad split: every tile needs a rank < nranks, and rank r exactly "
+                               "rtw_tiles_for_rank(W, H, r, nranks) tiles");
+    for (uint32_t k = 0; k < rtw_device_count(c); ++k)   // multi-device: every rank alike
+        apply_split(rtw_device_ctx(c, k), W, H, nranks, tile_rank, tile_cost, false, nullptr);
+    return RTW_OK;
+}
+
+int rtw_get_split(rtw_ctx* c, uint32_t W, uint32_t H, uint32_t nranks, uint32_t* tile_rank) {
+    if (!c || nranks == 0) return RTW_E_INVALID;
+    if (!split_active(c, W, H, nranks)) return 0;
+    if (tile_rank) memcpy(tile_rank, c->split_rank.data(), c->split_rank.size() * sizeof(uint32_t));
+    return c->split_auto ? 2 : 1;
+}
+
+int rtw_tile_costs(rtw_ctx* c, const rtw_camera* cam, uint32_t rank, uint32_t nranks, uint32_t* tile_cost) {
+    if (!c || !cam || !tile_cost || nranks == 0 || rank >= nranks) return fail(c, RTW_E_INVALID, "bad argument");
+    return tile_costs_of(c, cam, rank, nranks, tile_cost);
+}
+
 int rtw_assemble_tiles(rtw_ctx* c, const void* d_ranks, size_t rank_stride_bytes, uint32_t nranks, uint32_t W,
                        uint32_t H, void* d_image, void* stream) {
     if (!c || nranks == 0) return fail(c, RTW_E_INVALID, "bad argument");
@@ -1667,11 +1944,18 @@ int rtw_assemble_tiles(rtw_ctx* c, const void* d_ranks, size_t rank_stride_bytes
     HIP_TRY(c, hipSetDevice(c->device));
     hipStream_t s = resolve_stream(c, stream);
     const size_t stride = rank_stride_bytes / esz;
+    // a dealt split: each tile's slot from its map (null: the round robin)
+    const uint32_t* slot = nullptr;
+    if (split_active(c, W, H, nranks)) {
+        const int mrc = ensure_tile_slot(c, W, H, nranks);
+        if (mrc) return mrc;
+        slot = reinterpret_cast<const uint32_t*>(c->d_tile_slot);
+    }
     const int rc = c->precision == RTW_F32
                        ? rtw::launch_assemble_f32(reinterpret_cast<const float*>(d_ranks), stride, nranks, W, H,
-                                                  reinterpret_cast<float*>(d_image), s)
+                                                  slot, reinterpret_cast<float*>(d_image), s)
                        : rtw::launch_assemble_f64(reinterpret_cast<const double*>(d_ranks), stride, nranks, W, H,
-                                                  reinterpret_cast<double*>(d_image), s);
+                                                  slot, reinterpret_cast<double*>(d_image), s);
     if (rc) return fail(c, RTW_E_DEVICE, std::string("assemble launch failed: ") + hipGetErrorString(hipGetLastError()));
     return RTW_OK;
 }
@@ -1713,6 +1997,30 @@ int rtw_render_image_device(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, vo
         rc = rtw_render_device(c, cam, seed, 0, 1, c->d_out, c->out_cap, stream);
         if (rc) return rc;
         return img ? rtw_assemble_tiles(c, c->d_out, c->out_cap, 1, W, H, d_image, stream) : RTW_OK;
+    }
+    // Balance (tuning "balance"): once every rank has counted its tiles' costs
+    // for this camera and scene (the first render of a key counts them), deal
+    // the tiles to the ranks by those costs (rtw_split_deal) -- the reference
+    // balances its pixels dynamically over the host cores, camera.rs:340-353.
+    // The image does not depend on the split (every pixel's samples are its own).
+    const bool have = split_active(c, W, H, n);
+    if (c->balance && n > 1 && img &&
+        (!have || (c->split_auto && (c->split_scene != c->scene_serial ||
+                                     memcmp(&c->split_cam, cam, sizeof *cam) != 0)))) {
+        bool all = true;
+        for (uint32_t k = 0; k < n && all; ++k) all = lpt_has(rtw_device_ctx(c, k), cam, k, n);
+        if (all) {
+            std::vector<uint32_t> cost(n_tiles_of(W, H), 0), owner(cost.size(), 0);
+            for (uint32_t k = 0; k < n; ++k) {
+                rtw_ctx* ck = rtw_device_ctx(c, k);
+                const int rc = tile_costs_of(ck, cam, k, n, cost.data());
+                if (rc) return k ? fail(c, rc, ck->err) : rc;
+            }
+            int rc = rtw_split_deal(cost.data(), W, H, n, owner.data());
+            if (rc) return fail(c, rc, "rtw_split_deal failed");
+            for (uint32_t k = 0; k < n; ++k)
+                apply_split(rtw_device_ctx(c, k), W, H, n, owner.data(), cost.data(), true, cam);
+        }
     }
     HIP_TRY(c, hipSetDevice(c->device));
     // (the previous call's gather + assembly, possibly on another stream: rank

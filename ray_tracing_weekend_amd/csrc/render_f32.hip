@@ -11,8 +11,8 @@ int launch_render_f32(const KParams<float>& p, int world, size_t lds_bytes, floa
 }
 
 int launch_assemble_f32(const float* ranks, size_t rank_stride, uint32_t nranks, uint32_t W, uint32_t H,
-                        float* img, hipStream_t stream) {
-    return launch_assemble_impl<float>(ranks, rank_stride, nranks, W, H, img, stream);
+                        const uint32_t* slot, float* img, hipStream_t stream) {
+    return launch_assemble_impl<float>(ranks, rank_stride, nranks, W, H, slot, img, stream);
 }
 
 }  // namespace rtw

@@ -11,8 +11,8 @@ int launch_render_f64(const KParams<double>& p, int world, size_t lds_bytes, dou
 }
 
 int launch_assemble_f64(const double* ranks, size_t rank_stride, uint32_t nranks, uint32_t W, uint32_t H,
-                        double* img, hipStream_t stream) {
-    return launch_assemble_impl<double>(ranks, rank_stride, nranks, W, H, img, stream);
+                        const uint32_t* slot, double* img, hipStream_t stream) {
+    return launch_assemble_impl<double>(ranks, rank_stride, nranks, W, H, slot, img, stream);
 }
 
 }  // namespace rtw

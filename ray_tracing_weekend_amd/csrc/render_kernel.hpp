@@ -2335,6 +2335,13 @@ __device__ V3<R> tex_colour(const DevScene<R>& sc, uint32_t tid, R u, R v, V3<R>
 enum : int { kOptRobust = 1, kOptLightBvh = 2, kOptTex = 4, kOptPrims = 8, kOptHit64 = 16 };
 // subtree stealing in the f32 while-while kernels (bvh_traverse_steal); 0
 // builds them without it (timing comparisons, tools/variants.sh)
+// render_kernel: issue priorities in rotation (see the trip loop)
+#ifndef RTW_PRIO_ROTATE
+#define RTW_PRIO_ROTATE 1
+#endif
+#ifndef RTW_PRIO_SHIFT
+#define RTW_PRIO_SHIFT 8
+#endif
 #ifndef RTW_STEAL
 #define RTW_STEAL 1
 #endif
@@ -2548,7 +2555,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
             c_begin = cg * k->group;
             glen = min(c_begin + k->group, k->n_chunks) - c_begin;
         }
-        const uint32_t T = lt * k->nranks + k->rank;
+        const uint32_t T = k->tile_map ? k->tile_map[lt] : lt * k->nranks + k->rank;   // (global_tile)
         ty = T / k->tiles_x;
         tx = T - ty * k->tiles_x;
         n_items = 64u * glen;
@@ -2611,6 +2618,10 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
     // segments and Lambertian bounces are counted per wave (scalar: a ballot's
     // popcount per trip), node visits and sphere tests per lane (the tile costs)
     uint32_t segs = 0, lambs = 0, nvis = 0, ntest = 0;
+    // (counting renders with KParams::cost_time) the clock at the last trip's
+    // start and its lanes
+    uint64_t trip_clk = 0;
+    uint32_t trip_lanes = 0;
     bool active = false, need = true;
     // kCoopGrid (f32 kernels with the light grid, KParams::grid_piece > 0): a
     // Lambertian bounce's light pdf is left pending (`pend`) for the wave's
@@ -2627,7 +2638,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
         // its end minus at its start -- subtracted here, added at the end (a
         // u32 sum: exact modulo 2^32, no register kept)
         if (k->tile_cost) {
-            if (s < k->cost_spp) atomicSub(k->tile_cost + (slot >> 6), nvis + ntest);
+            if (s < k->cost_spp && !k->cost_time) atomicSub(k->tile_cost + (slot >> 6), nvis + ntest);
         }
         // Camera::get_ray, camera.rs:274-293 + ray_colour_call, camera.rs:439-457
         const uint32_t i = ij & 0xffffu, j = ij >> 16;
@@ -2705,10 +2716,43 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
     // the first 64 items of the first task go to lanes 0..63 in order
     acquire();
     RTW_PROBE_CLK(0);
+#if RTW_PRIO_ROTATE
+    // Issue priority in rotation.  A SIMD's arbiter favours its oldest wave:
+    // with persistent waves, whose ages never change, the wave in slot 0 ran
+    // at 1.46x and the one in slot 3 at 0.53x the mean rate (lane-segments per
+    // us, profiles/r06c_timeline.jsonl), and the launch ended on slot-3 waves
+    // finishing a task taken long before (an 8-rank C2 share: 1 ms after the
+    // median wave).  Each wave takes priority (clock / 2^RTW_PRIO_SHIFT + its
+    // slot) mod 4 at every trip, so at any time the waves of a SIMD hold
+    // different priorities and each holds the highest a quarter of the time.
+    uint32_t prio_slot;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(prio_slot));
+    prio_slot &= 3u;
+#endif
 
     for (;;) {
         const uint64_t live = __ballot(active);
         if (live == 0) break;
+        if (kargs()->cost_time) {
+            // wave-time tile costs (counting renders): the last trip's clock cycles,
+            // shared by its lanes, added for each lane running a counted sample now
+            // (a trip lasts about as long as the one before it)
+            const KArgs* k = kargs();
+            const uint64_t now = clock64();
+            if (trip_lanes && active && s < k->cost_spp)
+                atomicAdd(k->tile_cost + (slot >> 6), (uint32_t)(now - trip_clk) / trip_lanes);
+            trip_clk = now;
+            trip_lanes = (uint32_t)__popcll(live);
+        }
+#if RTW_PRIO_ROTATE
+        {
+            const uint32_t pr = ((uint32_t)(wall_clock64() >> RTW_PRIO_SHIFT) + prio_slot) & 3u;
+            if (pr == 0) __builtin_amdgcn_s_setprio(0);
+            else if (pr == 1) __builtin_amdgcn_s_setprio(1);
+            else if (pr == 2) __builtin_amdgcn_s_setprio(2);
+            else __builtin_amdgcn_s_setprio(3);
+        }
+#endif
         segs += (uint32_t)__popcll(live);   // every active lane runs one segment of this trip
         bool lamb = false;                  // the lane's segment ended in a Lambertian scatter
         // (kCoopGrid) this trip's pending light pdf and the bounce's weights: set by
@@ -3196,7 +3240,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                 dst[1] = part.y;
                 dst[2] = part.z;
                 if (k->tile_cost) {   // tile costs for the task order: this sample's work
-                    if (s < k->cost_spp)
+                    if (s < k->cost_spp && !k->cost_time)
                         atomicAdd(k->tile_cost + (slot >> 6), nvis + ntest + kCostPerSegment * (k->max_depth - depth + 1u));
                 }
                 ++s;
@@ -3387,7 +3431,7 @@ __global__ void __launch_bounds__(64) reduce_chunks_kernel(const KParams<R> p, R
     // each lane folds its pixel's row in chunk order
     __shared__ R win[64 * kFoldRow];
     const uint32_t lt = blockIdx.x, lane = threadIdx.x;
-    const uint32_t T = lt * p.nranks + p.rank;
+    const uint32_t T = global_tile(p, lt);
     const uint32_t ty = T / p.tiles_x, tx = T - ty * p.tiles_x;
     const uint32_t i = tx * kTile + (lane & 7), j = ty * kTile + (lane >> 3);
     const size_t row_len = (size_t)p.n_chunks * 3;
@@ -3433,12 +3477,14 @@ __global__ void __launch_bounds__(64) reduce_chunks_kernel(const KParams<R> p, R
 }
 
 // Un-interleave the ranks' packed tiles into the image [H][W][3]: one thread
-// per pixel slot of every global tile T (rank T % nranks, its local tile
-// T / nranks).  ranks = nranks buffers, rank_stride elements apart.
+// per pixel slot of every global tile T (v = slot[T], or T for the round
+// robin: rank v % nranks, its local tile v / nranks).  ranks = nranks
+// buffers, rank_stride elements apart.
 template <typename R>
 __global__ void __launch_bounds__(256) assemble_tiles_kernel(const R* __restrict__ ranks, size_t rank_stride,
                                                              uint32_t nranks, uint32_t W, uint32_t H,
                                                              uint32_t tiles_x, uint32_t n_tiles,
+                                                             const uint32_t* __restrict__ slot,
                                                              R* __restrict__ img) {
     const uint32_t gid = blockIdx.x * 256 + threadIdx.x;
     const uint32_t T = gid >> 6, lane = gid & 63;
@@ -3446,7 +3492,8 @@ __global__ void __launch_bounds__(256) assemble_tiles_kernel(const R* __restrict
     const uint32_t ty = T / tiles_x, tx = T - ty * tiles_x;
     const uint32_t i = tx * kTile + (lane & 7), j = ty * kTile + (lane >> 3);
     if (i >= W || j >= H) return;
-    const uint32_t k = T % nranks, lt = T / nranks;
+    const uint32_t v = slot ? slot[T] : T;
+    const uint32_t k = v % nranks, lt = v / nranks;
     const R* src = ranks + k * rank_stride + ((size_t)lt * 64 + lane) * 3;
     R* dst = img + ((size_t)j * W + i) * 3;
     dst[0] = src[0];
@@ -3611,12 +3658,12 @@ inline int launch_render_impl(const KParams<R>& p, int world, size_t lds_bytes, 
 
 template <typename R>
 inline int launch_assemble_impl(const R* ranks, size_t rank_stride, uint32_t nranks, uint32_t W, uint32_t H,
-                                R* img, hipStream_t stream) {
+                                const uint32_t* slot, R* img, hipStream_t stream) {
     const uint32_t tiles_x = (W + kTile - 1) / kTile, n_tiles = tiles_x * ((H + kTile - 1) / kTile);
     const uint32_t blocks = (uint32_t)(((uint64_t)n_tiles * 64 + 255) / 256);
     if (blocks) {
         hipLaunchKernelGGL((dev::assemble_tiles_kernel<R>), dim3(blocks), dim3(256), 0, stream, ranks, rank_stride,
-                           nranks, W, H, tiles_x, n_tiles, img);
+                           nranks, W, H, tiles_x, n_tiles, slot, img);
         if (hipGetLastError() != hipSuccess) return -1;
     }
     return 0;

@@ -239,11 +239,22 @@ struct KParams {
     const uint32_t* task_table;       // non-null: task t = {local tile, first chunk | chunks << 20}
                                       // at [2t, 2t + 1] (longest tiles first, sized by a pilot
                                       // render's costs); null: t = tile * n_groups + group
-    uint32_t* tile_cost;              // non-null: [local tile] += segments of each sample s < cost_spp
+    uint32_t* tile_cost;              // non-null: [local tile] += the cost of each sample s < cost_spp
     uint32_t cost_spp;                //   (a pilot render, or the first render of a split)
+    uint32_t cost_time;               //   ... the cost: 1 the sample's share of its wave's clock
+                                      //   cycles (each trip's / its lanes); 0 node visits + sphere
+                                      //   tests + kCostPerSegment per segment
     uint32_t grid_piece;              // f32 light grid: cells per piece of the wave-cooperative
                                       // walk (lights_pdf_grid_coop); 0: one lane per ray
+    const uint32_t* tile_map;         // non-null: local tile lt -> global tile (a dealt split,
+                                      // rtw_set_split); null: lt * nranks + rank (the round robin)
 };
+
+// the global 8x8 tile of local tile lt
+template <typename R>
+__host__ __device__ inline uint32_t global_tile(const KParams<R>& p, uint32_t lt) {
+    return p.tile_map ? p.tile_map[lt] : lt * p.nranks + p.rank;
+}
 
 // The cost of a sample for the task order (KParams::tile_cost): its BVH node
 // visits + sphere tests + this many per segment (a segment's hit record and
@@ -260,10 +271,11 @@ int launch_render_f32(const KParams<float>& p, int world, size_t lds_bytes, floa
 int launch_render_f64(const KParams<double>& p, int world, size_t lds_bytes, double* out,
                       hipStream_t stream, hipEvent_t mid);
 // The ranks' packed tiles (nranks buffers, rank_stride elements apart) -> the
-// image [H][W][3] (rtw_assemble_tiles).
+// image [H][W][3] (rtw_assemble_tiles).  slot (may be null: the round robin,
+// T itself): global tile T -> lt * nranks + rank of a dealt split.
 int launch_assemble_f32(const float* ranks, size_t rank_stride, uint32_t nranks, uint32_t W, uint32_t H,
-                        float* img, hipStream_t stream);
+                        const uint32_t* slot, float* img, hipStream_t stream);
 int launch_assemble_f64(const double* ranks, size_t rank_stride, uint32_t nranks, uint32_t W, uint32_t H,
-                        double* img, hipStream_t stream);
+                        const uint32_t* slot, double* img, hipStream_t stream);
 
 }  // namespace rtw

@@ -83,32 +83,38 @@
 #endif
 
 #ifdef RTW_TIMELINE
-// tools/share_timeline.py: per wave {begin, end} wall-clock ticks (100 MHz) and
-// its task count, read back with rtw_probe_timeline_read
-constexpr uint32_t kTlWaves = 1 << 16;
-static __device__ unsigned long long g_tl[kTlWaves * 4];
+// tools/share_timeline.py: per wave kTlWords words -- {begin, end} wall-clock
+// ticks (100 MHz), task count | last task << 32, XCC id | HW_ID << 32, the
+// wave's lane-segments, the tick it took its last task -- read back with
+// rtw_probe_timeline_read
+constexpr uint32_t kTlWaves = 1 << 16, kTlWords = 6;
+static __device__ unsigned long long g_tl[kTlWaves * kTlWords];
 #define RTW_PROBE_WAVE_BEGIN() \
-    uint64_t tl_begin_ = wall_clock64(); \
+    uint64_t tl_begin_ = wall_clock64(), tl_last_t_ = tl_begin_; \
     uint32_t tl_tasks_ = 0, tl_last_ = 0
-#define RTW_PROBE_WAVE_TASK() (++tl_tasks_, tl_last_ = t)
+#define RTW_PROBE_WAVE_TASK() (++tl_tasks_, tl_last_ = t, tl_last_t_ = wall_clock64())
 #define RTW_PROBE_WAVE_END() \
     do { \
         const uint32_t w_ = blockIdx.x * kWavesPerBlock + wave; \
         if (lane == 0 && w_ < kTlWaves) { \
-            unsigned xcc_; \
+            unsigned xcc_, hw_; \
             asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc_)); \
-            g_tl[4 * w_] = tl_begin_; \
-            g_tl[4 * w_ + 1] = wall_clock64(); \
-            g_tl[4 * w_ + 2] = tl_tasks_ | ((unsigned long long)tl_last_ << 32); \
-            g_tl[4 * w_ + 3] = xcc_ & 0xf; \
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw_)); \
+            unsigned long long* r_ = g_tl + (size_t)kTlWords * w_; \
+            r_[0] = tl_begin_; \
+            r_[1] = wall_clock64(); \
+            r_[2] = tl_tasks_ | ((unsigned long long)tl_last_ << 32); \
+            r_[3] = (xcc_ & 0xf) | ((unsigned long long)hw_ << 32); \
+            r_[4] = segs; \
+            r_[5] = tl_last_t_; \
         } \
     } while (0)
 extern "C" int rtw_probe_timeline_read(unsigned long long* out, size_t n, int reset) {
-    n = n < (size_t)kTlWaves * 4 ? n : (size_t)kTlWaves * 4;
+    n = n < (size_t)kTlWaves * kTlWords ? n : (size_t)kTlWaves * kTlWords;
     if (hipDeviceSynchronize() != hipSuccess) return -1;
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tl), n * sizeof(unsigned long long)) != hipSuccess) return -1;
     if (reset) {
-        static unsigned long long zero[kTlWaves * 4];
+        static unsigned long long zero[kTlWaves * kTlWords];
         if (hipMemcpyToSymbol(HIP_SYMBOL(g_tl), zero, sizeof zero) != hipSuccess) return -1;
     }
     return (int)n;

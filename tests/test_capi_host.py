@@ -33,7 +33,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert rtw._lib.rtw_abi_version() == rtw._capi.ABI_VERSION == 9
+    assert rtw._lib.rtw_abi_version() == rtw._capi.ABI_VERSION == 10
 
 
 def test_camera_builder_defaults_match_reference():

@@ -198,3 +198,105 @@ def test_virtual_ranks_light_grid_counters():
         assert (r.stats.light_tests, r.stats.grid_cells, r.stats.segments) == st
     ok = ~np.isnan(ref)
     assert np.array_equal(np.isnan(img), np.isnan(ref)) and np.array_equal(img[ok], ref[ok])
+
+
+# ---- the cost-dealt rank split (ABI 10) ------------------------------------
+
+
+@pytest.mark.parametrize("prec", [rtw.RTW_F64, rtw.RTW_F32])
+@pytest.mark.parametrize("n", [2, 3, 8])
+def test_virtual_ranks_balance_deals_by_cost_bit_identical(prec, n):
+    """A multi-device context deals its tiles by their counted costs by
+    itself (tuning "balance"): the first render of the camera counts (round
+    robin), the second deals (rtw_get_split kind 2, each rank keeping its
+    round-robin tile count) and renders balanced; every image bit-identical
+    to a one-rank render, the summed counters too."""
+    scene, cam = _cam(w=120, h=72, spp=40)
+    W, H = cam.image_width, cam.image_height
+    with rtw.Renderer(device=0, precision=prec) as r:
+        r.set_tuning("lpt_min_spp", 8)
+        r.set_scene(scene)
+        ref = r.render(cam, 9)
+        ref_segments = r.stats.segments
+    ok = ~np.isnan(ref)
+    with rtw.Renderer(device=0, precision=prec, virtual_ranks=n) as r:
+        r.set_tuning("lpt_min_spp", 8)
+        r.set_scene(scene)
+        imgs = [r.render(cam, 9)]
+        assert r.get_split(W, H, n)[0] == 0                 # counted under the round robin
+        imgs.append(r.render(cam, 9))
+        kind, split = r.get_split(W, H, n)
+        assert kind == 2
+        assert np.bincount(split, minlength=n).tolist() == [rtw.tiles_for_rank(W, H, k, n) for k in range(n)]
+        rr = np.arange(split.size) % n
+        assert not np.array_equal(split, rr)
+        assert r.stats.segments == ref_segments
+        assert sum(r.rank_view(k).get_stats().samples for k in range(n)) == W * H * cam.samples_per_pixel
+        imgs.append(r.render(cam, 9))                       # steady state on the dealt split
+        for k in range(n):                                  # every rank holds the same split
+            assert np.array_equal(r.rank_view(k).get_split(W, H, n)[1], split)
+    for img in imgs:
+        assert np.array_equal(np.isnan(img), np.isnan(ref)) and np.array_equal(img[ok], ref[ok])
+
+
+def test_virtual_ranks_balance_off_keeps_round_robin():
+    scene, cam = _cam(w=64, h=48, spp=40)
+    with rtw.Renderer(device=0, precision=rtw.RTW_F64, virtual_ranks=2) as r:
+        r.set_tuning("lpt_min_spp", 8)
+        r.set_tuning("balance", 0)
+        r.set_scene(scene)
+        r.render(cam, 1)
+        r.render(cam, 1)
+        assert r.get_split(cam.image_width, cam.image_height, 2)[0] == 0
+
+
+@pytest.mark.parametrize("prec", [rtw.RTW_F64, rtw.RTW_F32])
+def test_explicit_split_render_device_and_assemble(prec):
+    """rtw_set_split + rtw_render_device(rank, n) + rtw_assemble_tiles on one
+    context: each rank's packed buffer holds exactly its dealt tiles in
+    increasing tile order (sharding.pack with the split), the assembled
+    image equals a plain render bit for bit; tile costs from the counting
+    render of each rank cover exactly its tiles."""
+    from ray_tracing_weekend_amd import sharding
+    scene, cam = _cam(w=77, h=45, spp=33)             # ragged tiles
+    W, H, n = cam.image_width, cam.image_height, 3
+    tdt = torch.float64 if prec == rtw.RTW_F64 else torch.float32
+    with rtw.Renderer(device=0, precision=prec) as r:
+        r.set_scene(scene)
+        ref = r.render(cam, 5)
+        per = rtw.tiles_for_rank(W, H, 0, n) * 64 * 3
+        bufs = torch.full((n, per), float("nan"), dtype=tdt, device="cuda:0")
+        with pytest.raises(rtw.RenderError):
+            r.tile_costs(cam, 0, n)                         # nothing counted for this split yet
+        costs = np.zeros(rtw.n_tiles(W, H), np.uint32)
+        r.set_tuning("lpt_min_spp", 8)
+        for k in range(n):                                  # counting renders (round robin)
+            r.render_device(cam, 5, bufs[k].data_ptr(), per * bufs.element_size(), rank=k, nranks=n)
+            before = costs.copy()
+            r.tile_costs(cam, k, n, out=costs)
+            changed = np.nonzero(costs != before)[0]
+            assert set(changed.tolist()) <= set(sharding.rank_tiles(W, H, k, n))
+        assert (costs > 0).mean() > 0.9
+        split = rtw.split_deal(costs, W, H, n)
+        bad = split.copy()
+        bad[0] = (bad[0] + 1) % n                           # one rank a tile too many
+        with pytest.raises(rtw.RenderError):
+            r.set_split(W, H, n, bad)
+        r.set_split(W, H, n, split, costs)
+        assert r.get_split(W, H, n)[0] == 1
+        assert r.get_split(W, H, n + 1)[0] == 0             # other rank counts: the round robin
+        for k in range(n):
+            r.render_device(cam, 5, bufs[k].data_ptr(), per * bufs.element_size(), rank=k, nranks=n)
+        img = torch.empty((H, W, 3), dtype=tdt, device="cuda:0")
+        r.assemble_tiles(bufs.data_ptr(), bufs.stride(0) * bufs.element_size(), n, W, H, img.data_ptr())
+        torch.cuda.synchronize()
+        got = img.cpu().double().numpy()
+        full = torch.from_numpy(ref.astype(np.float32 if prec == rtw.RTW_F32 else np.float64))
+        for k in range(n):
+            p = sharding.pack(full, k, n, split).reshape(-1)
+            b = bufs[k].cpu()[: p.numel()]
+            assert torch.equal(torch.nan_to_num(b, nan=-1.0), torch.nan_to_num(p.to(b.dtype), nan=-1.0))
+        r.set_split(W, H, n, None)                          # back to the round robin
+        assert r.get_split(W, H, n)[0] == 0
+    ok = ~np.isnan(ref)
+    assert np.array_equal(np.isnan(got), np.isnan(ref)) and np.array_equal(got[ok], ref[ok])

@@ -5,10 +5,13 @@ GPU (each rank's share rendered in turn with rtw_render_device(rank, nranks)):
 the compute part of the strong-scaling curve the driver's N-GPU bench measures
 (it adds the barrier and the one RCCL gather).  Prints one JSON line per N.
 
-Per rank: the first render of a split ("cold": tile index order while it
-counts the tile costs -- or, with tuning lpt_inline=0, a 2-spp pilot render
-first) and the best of --reps steady renders (longest tiles first; the first
-of them reads the counts back and builds the task table).  Per N the projected frame time adds, for N > 1, an estimate
+Per rank: the first render of a split ("cold": the round robin in tile index
+order while it counts the tile costs -- or, with tuning lpt_inline=0, a 2-spp
+pilot render first) and the best of --reps steady renders (longest tiles
+first).  With --split cost (the default, what a multi-device context does by
+itself) the steady renders follow the split dealt from ALL ranks' counted
+costs (rtw_split_deal; each rank keeps its round-robin tile count); with
+--split rr they stay on the round robin.  Per N the projected frame time adds, for N > 1, an estimate
 of the one gather of the packed tiles to rank 0 (each rank's buffer over its
 own xGMI link in parallel: 25 us + bytes / 50 GB/s, a conservative share of a
 link's ~153 GB/s) and the measured device assemble of N buffers on rank 0.
@@ -24,6 +27,7 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
+import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 import ray_tracing_weekend_amd as rtw  # noqa: E402
@@ -37,6 +41,9 @@ def main():
     ap.add_argument("--size", default="1200x800", help="WxH (C4: 3840x2160)")
     ap.add_argument("--spp", type=int, default=500)
     ap.add_argument("--ranks", default="", help="only these ranks of each N (e.g. 0 for one C4 share)")
+    ap.add_argument("--split", default="cost", choices=["cost", "rr"],
+                    help="cost: the steady renders follow the tiles dealt by the cold renders' counted costs "
+                         "(rtw_split_deal, the multi-device default); rr: the round robin T mod N")
     ap.add_argument("--precision", default="f64", choices=["f32", "f64"],
                     help="f64: the headline parity mode (default); f32: the hit64 speed mode")
     a = ap.parse_args()
@@ -59,6 +66,8 @@ def main():
     for n in (int(x) for x in a.ns.split(",")):
         per_rank, kern, rend, cold, cold_rend = [], [], [], [], []
         only = [int(x) for x in a.ranks.split(",")] if a.ranks else range(n)
+        costs = np.zeros(rtw.n_tiles(W, H), np.uint32)
+        r.set_split(W, H, n, None)     # the cold renders: the round robin, counting the tile costs
         for rank in only:
             r.set_scene(scene)   # drops the cached task order: the next render counts the tile costs
             torch.cuda.synchronize()
@@ -67,6 +76,13 @@ def main():
             torch.cuda.synchronize()
             cold.append((time.perf_counter() - t0) * 1e3)
             cold_rend.append(r.get_timings(1)[0][0])   # the cold render's own kernel
+            if a.split == "cost" and n > 1:
+                r.tile_costs(cam, rank, n, out=costs)
+        split = None
+        if a.split == "cost" and n > 1 and not a.ranks:
+            split = rtw.split_deal(costs, W, H, n)
+            r.set_split(W, H, n, split, costs)
+        for rank in only:
             best = float("inf")
             for _ in range(a.reps):
                 torch.cuda.synchronize()
@@ -97,7 +113,12 @@ def main():
         frame_cold = max(cold) + gather_ms + assemble_ms
         base_frame = base_frame if n != 1 else frame
         base_cold = base_cold or frame_cold
+        cost_share = None
+        if split is not None:
+            cost_share = [round(float(costs[split == k].astype(np.float64).sum() / costs.astype(np.float64).sum()) * n, 4)
+                          for k in range(n)]
         print(json.dumps({"size": a.size, "spp": SPP, "tuning": a.tuning, "nranks": n, "ranks": list(only),
+                          "split": a.split if split is not None else "rr", "dealt_cost_share_x_n": cost_share,
                           "chunk": int(st.chunk), "max_rank_ms": round(slowest, 2), "min_rank_ms": round(min(per_rank), 2),
                           "max_rank_cold_ms": round(max(cold), 2),
                           "max_rank_cold_render_kernel_ms": round(max(cold_rend), 2), "gather_est_ms": round(gather_ms, 3),
