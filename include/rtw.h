@@ -186,7 +186,11 @@ typedef struct rtw_stats {
      * light pdf -- every Lambertian bounce x every light for the linear list
      * loop (hittable_list.rs:408-412), the lights of the big list, the visited
      * grid cells or light-BVH leaves for the light grid / BVH (counted by the
-     * kernel); grid_cells = light-grid cells those walks visited */
+     * kernel); grid_cells = light-grid cells those walks visited.  For the
+     * light grid these are WALK-WORK counters, not properties of the samples:
+     * the cooperative walks visit a piece boundary's cell twice, size pieces
+     * by the wave's pending cells and count a re-walk again, so they depend
+     * on how rays are grouped into waves (the image does not). */
     uint64_t light_tests, grid_cells;
 } rtw_stats;
 

@@ -106,7 +106,9 @@ struct rtw_ctx {
     // longest-first task list with guided sizes (lpt_tasks; guide_div 0: equal-cost
     // tasks of max_group chunks at most): a task costs the remaining work / guide_div,
     // at least total / guide_floor, at most guide_max chunks
-    uint32_t guide_div = 8192, guide_max = 4095;
+    // (C2 f64, max of 8 rank shares, 3 runs each: 16.32 ms vs equal-cost tasks 16.79;
+    // one GPU 117.35 vs 118.46 ms; profiles/r06i_ab_split.jsonl)
+    uint32_t guide_div = 16384, guide_max = 128;
     uint32_t cost_time = 1;           // tile costs in wave-time shares (KParams::cost_time); 0: work counts
     uint64_t guide_floor = 1u << 18;
     void* d_lpt = nullptr;            // pilot: [tile cost | chunk sums | tiles]
@@ -1190,10 +1192,10 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
             else if (light_stack <= rtw::kBvhStack) p.light_bvh = 1;  // light BVH
         }
         // the light grid's cooperative walk parks path state in the stack area
-        // (f64: kCoop64PieceIds + 1 words per piece of the walk -- [count, list
-        // indices] -- after the kCoopStash64-word stash: >= 64 pieces per round)
+        // (f64: one kCoop64Slot-word slot per piece of the walk -- [count, list
+        // indices] -- after the kCoopStash64-word stash: 64 pieces per round)
         const uint32_t min_stack = p.light_bvh == 1 ? light_stack
-                                   : (p.light_bvh == 2 ? (sizeof(R) == 8 ? rtw::kCoopStash64 + rtw::kCoop64PieceIds + 2u
+                                   : (p.light_bvh == 2 ? (sizeof(R) == 8 ? rtw::kCoopStash64 + rtw::kCoop64Slot
                                                                          : rtw::kCoopStash + 1u)
                                                        : 1u);
         // binary traversal pushes at most one entry per inner level: a leaf at
@@ -1235,11 +1237,10 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
     if (p.sc.mat_tex && (world == rtw::kWorldBvh4 || world == rtw::kWorldBvh)) {
         world = rtw::kWorldBvhWW;
         bvh_width = 2;
-        // (the light grid's walk area as above)
-        p.stack = std::max(p.sc.bvh_depth, p.light_bvh == 1   ? p.sc.lbvh_depth + 1
-                                           : p.light_bvh == 2 ? (sizeof(R) == 8 ? rtw::kCoopStash64 + rtw::kCoop64PieceIds + 2u
-                                                                                : rtw::kCoopStash + 1u)
-                                                              : 1u);
+        // Textured kernels carry kOptPrims, so their light-grid walk is the
+        // per-lane one (no cooperative walk, no stash or piece slots): only the
+        // light BVH's walk uses the per-lane stack
+        p.stack = std::max(p.sc.bvh_depth, p.light_bvh == 1 ? p.sc.lbvh_depth + 1 : 1u);
         if (p.stack > rtw::kBvhStack) return fail(c, RTW_E_UNSUPPORTED, "BVH deeper than the kernel's traversal stack");
     }
     // f64 hit points: the f32 kernels of sphere + plane scenes (the launch

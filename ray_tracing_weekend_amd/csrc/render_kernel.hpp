@@ -1920,8 +1920,7 @@ __device__ __forceinline__ R lights_pdf_grid_coop_list(const DevScene<float>& g,
                                                        PdfAt&& pdf_at, Mark&& mark) {
     // a piece's slot: [count, ids...] padded to 8 words (the owner reads it as two
     // 16-byte LDS loads)
-    constexpr uint32_t kPieceIds = kCoop64PieceIds, kSlot = 8, kMax = RTW_COOP64_MAX;
-    static_assert(kPieceIds + 1 <= kSlot, "slot = count + ids");
+    constexpr uint32_t kPieceIds = kCoop64PieceIds, kSlot = kCoop64Slot, kMax = RTW_COOP64_MAX;
     const uint32_t cap = cap_words / (kSlot * 64) * 64;   // pieces per round
     // (the host sizes the stack area for at least one round of 64 pieces, so a
     // smaller area is a host error: every pending ray ends NaN, never a loop
@@ -2340,7 +2339,7 @@ enum : int { kOptRobust = 1, kOptLightBvh = 2, kOptTex = 4, kOptPrims = 8, kOptH
 #define RTW_PRIO_ROTATE 1
 #endif
 #ifndef RTW_PRIO_SHIFT
-#define RTW_PRIO_SHIFT 8
+#define RTW_PRIO_SHIFT 12
 #endif
 #ifndef RTW_STEAL
 #define RTW_STEAL 1
@@ -2516,8 +2515,8 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
     // the wave's current task (wave-uniform): local tile lt = global 8x8 tile
     // T = lt * nranks + rank at (tx, ty) -- the ranks take the image's tiles
     // round-robin (rtw_tiles_for_rank) -- and chunks [c_begin, c_begin +
-    // glen): a pool of n_items (pixel, chunk) items
-    uint32_t lt = 0, tx = 0, ty = 0, c_begin = 0, glen = 0, n_items = 0;
+    // glen): a pool of 64 glen (pixel, chunk) items
+    uint32_t lt = 0, tx = 0, ty = 0, c_begin = 0, glen = 0;
     uint32_t glen_m = 0;          // glen > 1: ceil(2^32 / glen), q / glen = umulhi(q, glen_m) for q < 64 glen
                                   // (2^32 does not fit: glen == 1 is special-cased)
     // The camera, the background and the task parameters are read where they
@@ -2558,7 +2557,6 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
         const uint32_t T = k->tile_map ? k->tile_map[lt] : lt * k->nranks + k->rank;   // (global_tile)
         ty = T / k->tiles_x;
         tx = T - ty * k->tiles_x;
-        n_items = 64u * glen;
         glen_m = glen > 1 ? (uint32_t)((0xFFFFFFFFull + glen) / glen) : 0u;
     };
     // p.persist: every wave takes tasks from a global counter until none are
@@ -2667,6 +2665,8 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
         self_s = -1;
         self_iso = false;
     };
+    // (wave-uniform) the end of the items this wave may hand out: its task's 64 glen
+    uint32_t claim_end = p.persist ? 0u : 64u * glen;
     // Give every lane that needs one a valid item: from the current pool, then
     // (p.persist) from the next task's; none once no task is left.
     auto acquire = [&]() {
@@ -2674,7 +2674,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
         for (;;) {
             const uint64_t want = __ballot(need);
             if (want == 0) break;
-            if (next_q >= n_items) {
+            if (next_q >= claim_end) {
                 uint32_t t = 0xffffffffu;
                 if (more) {
                     const uint64_t live = __ballot(true);
@@ -2690,13 +2690,14 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                 set_task(t);
                 RTW_PROBE_WAVE_TASK();
                 next_q = 0;
+                claim_end = 64u * glen;
                 continue;
             }
             if (need) {
                 const uint32_t below = __builtin_amdgcn_mbcnt_hi(
                     (uint32_t)(want >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)want, 0u));
                 q = next_q + below;
-                if (q < n_items) {
+                if (q < claim_end) {
                     uint32_t px;
                     decode(q, px, c);
                     const uint32_t i = tx * kTile + (px & 7u), j = ty * kTile + (px >> 3);
@@ -3385,7 +3386,6 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
         acquire();
         RTW_PROBE_CLK(0);
     }
-
     RTW_PROBE_CLK(10);
     RTW_PROBE_CLK_END();
     RTW_PROBE_WAVE_END();

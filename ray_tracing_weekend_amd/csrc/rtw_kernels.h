@@ -190,6 +190,13 @@ constexpr uint32_t kCoopStash64 = RTW_STASH64_EXTRA ? 34u : 20u;
 #define RTW_COOP64_MAX 8
 #endif
 constexpr uint32_t kCoop64PieceIds = RTW_COOP64_PIECE_IDS;
+// ... and the LDS words of one piece's slot per round: [count, list indices],
+// padded to 8 (16-byte reads).  The host gives the f64 light-grid kernels
+// kCoopStash64 + kCoop64Slot words per lane, so that a round holds >= 64
+// pieces (the walk has no per-lane fallback)
+constexpr uint32_t kCoop64Slot = 8;
+static_assert(kCoop64PieceIds + 1 <= kCoop64Slot, "a piece's slot holds its count and ids");
+static_assert(kCoopStash64 + kCoop64Slot <= kWalkStashMax, "the walk's LDS area fits the host's bound");
 // Subtree stealing in the while-while traversal (render_kernel.hpp
 // bvh_traverse_steal): per wave the result slots of its 64 rays (f32: a u64
 // key; f64: u64 t bits + u32 id) and 64 rendezvous bytes, in LDS right after

@@ -148,27 +148,30 @@ def test_virtual_ranks_bit_identical(prec, n):
         assert np.array_equal(np.isnan(img), np.isnan(ref)) and np.array_equal(img[ok], ref[ok])
 
 
-def test_virtual_ranks_image_device_streams_and_stats():
+@pytest.mark.parametrize("prec", [rtw.RTW_F64, rtw.RTW_F32])
+def test_virtual_ranks_image_device_streams_and_stats(prec):
     """rtw_render_image_device of a virtual 3-rank context on two different
     torch streams back to back (the second call's renders wait for the first
     call's gather + assembly), then rtw_render_device on the same context:
-    its stats are rank 0's alone."""
+    its stats are rank 0's alone.  (The RCCL transport's cross-device event
+    wait has the same order but runs only on >= 2 GPUs.)"""
     scene, cam = _cam(w=64, h=48, spp=6)
-    ref, samples, _ = _single(scene, cam, rtw.RTW_F64, seed=4)
-    with rtw.Renderer(device=0, precision=rtw.RTW_F64, virtual_ranks=3) as r:
+    ref, samples, _ = _single(scene, cam, prec, seed=4)
+    tdt = torch.float64 if prec == rtw.RTW_F64 else torch.float32
+    with rtw.Renderer(device=0, precision=prec, virtual_ranks=3) as r:
         r.set_scene(scene)
         imgs = []
         for k in range(2):
             s = torch.cuda.Stream()
             with torch.cuda.stream(s):
-                img = torch.full((cam.image_height, cam.image_width, 3), float("nan"), dtype=torch.float64,
+                img = torch.full((cam.image_height, cam.image_width, 3), float("nan"), dtype=tdt,
                                  device="cuda:0")
-                r.render_image_device(cam, 4, img.data_ptr(), img.numel() * 8)
-                imgs.append(img.cpu().numpy())
+                r.render_image_device(cam, 4, img.data_ptr(), img.numel() * img.element_size())
+                imgs.append(img.cpu().double().numpy())
         assert r.get_stats().samples == samples
         n0 = rtw.tiles_for_rank(cam.image_width, cam.image_height, 0, 1) * 64 * 3
-        out = torch.zeros(n0, dtype=torch.float64, device="cuda:0")
-        r.render_device(cam, 4, out.data_ptr(), out.numel() * 8)
+        out = torch.zeros(n0, dtype=tdt, device="cuda:0")
+        r.render_device(cam, 4, out.data_ptr(), out.numel() * out.element_size())
         torch.cuda.synchronize()
         assert r.get_stats().samples == samples      # one rank rendered everything: rank 0's stats
         v = r.rank_view(1)
@@ -180,9 +183,14 @@ def test_virtual_ranks_image_device_streams_and_stats():
 
 
 def test_virtual_ranks_light_grid_counters():
-    """A scene whose light pdf takes the light grid (>= 64 lights): the light
-    tests and grid cells counted by the kernel (ABI 9) are properties of the
-    samples, so a 3-rank render sums to the one-rank counts; the image too."""
+    """A scene whose light pdf takes the light grid (>= 64 lights): the image
+    and the segments of a 3-rank render equal the one-rank render's.  The
+    light tests and grid cells (ABI 9) are WALK-WORK counters of the
+    cooperative walks -- a boundary cell is visited by both adjacent pieces,
+    the piece length adapts to the wave's pending cells, a re-walk counts its
+    cells again -- so they depend on how rays are grouped into waves: the
+    3-rank sums agree with the one-rank counts within a few percent, not bit
+    for bit."""
     scene, b = rtw.scenes.simple_soa(SEED, n=20)
     cam = b.with_image_width(48).with_image_height(32).with_samples_per_pixel(4).with_max_depth(50).build()
     assert np.asarray(scene.lights).reshape(-1, 4).shape[0] >= 64
@@ -195,7 +203,8 @@ def test_virtual_ranks_light_grid_counters():
     with rtw.Renderer(device=0, precision=rtw.RTW_F64, virtual_ranks=3) as r:
         r.set_scene(scene)
         img = r.render(cam, 2)
-        assert (r.stats.light_tests, r.stats.grid_cells, r.stats.segments) == st
+        assert r.stats.segments == st[2]
+        assert abs(r.stats.light_tests / st[0] - 1) < 0.05 and abs(r.stats.grid_cells / st[1] - 1) < 0.05
     ok = ~np.isnan(ref)
     assert np.array_equal(np.isnan(img), np.isnan(ref)) and np.array_equal(img[ok], ref[ok])
 

@@ -778,3 +778,30 @@ def test_task_table_with_4096_chunk_groups_keeps_every_chunk():
     img, _, cv = _render_gpu(soa, cam, 131, rtw.RTW_F32,
                              tuning={"group": 4096, "lpt_min_spp": 1, "chunk": 1}, renders=2)
     assert _same(base, img) and cb == cv
+
+
+@pytest.mark.parametrize("kind", [0, 2, 3])
+def test_textured_light_grid_scene_every_bvh_kind(kind):
+    """an f64 textured scene whose light list takes the light grid
+    (>= 64 sphere lights) renders under every BVH kind -- the textured kernels'
+    per-lane grid walk needs no stash or piece slots, so the remapped binary
+    kernels must not ask for them -- bit-identical to the oracle."""
+    soa, b = _scene(20)
+    assert np.asarray(soa.lights).reshape(-1, 4).shape[0] >= 64
+    nm = len(soa.mat_type)
+    soa.tex_type = np.array([rtw.RTW_TEX_SOLID] * (nm + 2) + [rtw.RTW_TEX_CHECKER], np.uint32)
+    soa.tex_params = np.array([list(soa.mat_params[m][:3]) + [0.0] for m in range(nm)] +
+                              [[0.2, 0.3, 0.1, 0.0], [0.9, 0.9, 0.9, 0.0], [0.0, 0.0, 0.0, 1.0 / 0.32]], np.float64)
+    soa.tex_refs = np.array([[0, 0]] * (nm + 2) + [[nm, nm + 1]], np.uint32)
+    mat_tex = np.arange(nm, dtype=np.uint32)
+    mat_tex[soa.plane_mat[0]] = nm + 2                      # the ground: a checker
+    soa.mat_tex = mat_tex
+    cam = b.with_image_width(40).with_image_height(24).with_samples_per_pixel(4).with_max_depth(50).build()
+    # (textured scenes run the binary while-while kernel for kinds 0 and 2)
+    gpu, chunk, (segs, lambs) = _render_gpu(soa, cam, 5, rtw.RTW_F64, accel=rtw.RTW_ACCEL_BVH,
+                                            tuning={"bvh_kind": kind, "bvh_lds_max": 64 * 1024})
+    assert LAST["kernel"] in (K_BVH_WW, K_BVH_LDS)
+    ref, st = _render_oracle(soa, cam, 5, chunk)
+    mae, exact = _compare_f64(gpu, ref, 4)
+    assert mae < F64_MAE_TOL and exact > 0.999
+    assert segs == st.segments and lambs == st.lambertian
