@@ -125,12 +125,25 @@ def kernel_identity(r, precision):
     return isa.render_kernel_name(precision, *v), isa.kernel_isa_sha(isa.render_kernel_symbol(precision, *v))
 
 
-def attach_pmc(roof, workload, kname, sha, chunk_sum_bytes=None):
+HBM_PEAK_GBS = 8000.0        # MI355X HBM3E (MI355X_MICROARCH.md)
+MALL_GATHER_GBS = 8600.0     # Infinity Cache, uniformly random rows gathered (MI355X_MICROARCH.md "Indexed rows")
+L2_GATHER_GBS = 17000.0      # an XCD's L2, rows shared by every workgroup (ibid., 16.8-18.8 TB/s)
+
+
+def attach_pmc(roof, workload, kname, sha, chunk_sum_bytes=None, kernel_ms=None):
     """traffic + PMC fractions into a roofline dict, only from a profile of
     the same machine code (else null).  scratch_write_frac = (WRITE_SIZE -
     the chunk sums the kernel must write) / WRITE_SIZE: the share of the
     kernel's writes that is register spill (scratch write-back) or other
-    waste; `chunk_sum_bytes` = n_chunks x pixels x 3 x element bytes."""
+    waste; `chunk_sum_bytes` = n_chunks x pixels x 3 x element bytes.
+    Beside the line's own `frac` it prints what the PMC says bounds the
+    kernel: `valu_lane_frac` = VALU issue x lanes active
+    (the share of the SIMDs' lane-cycles doing VALU work), the measured HBM
+    rate of `traffic` against 8 TB/s, and `bound_pmc` -- "latency" when the
+    waves wait on memory more than 40 % of their cycles while HBM moves less
+    than 20 % of its peak, "valu" when the VALU issues on more than 60 % of
+    the cycles, else "issue" (neither saturated: divergence / dependency
+    stalls)."""
     t = pmc_traffic(workload, kname, sha)
     roof["isa_sha"] = sha
     roof["traffic"] = t["bytes_per_launch"] if t else None
@@ -142,6 +155,17 @@ def attach_pmc(roof, workload, kname, sha, chunk_sum_bytes=None):
     roof["chunk_sum_bytes"] = chunk_sum_bytes
     roof["scratch_write_frac"] = (round(max(0.0, wb - chunk_sum_bytes) / wb, 4)
                                   if wb and chunk_sum_bytes is not None else None)
+    vi, la, mw = roof["valu_issue_frac"], roof["lanes_active_frac"], roof["mem_wait_frac"]
+    roof["valu_lane_frac"] = round(vi * la, 4) if vi is not None and la is not None else None
+    hbm = (roof["traffic"] / (kernel_ms * 1e-3) / 1e9) if roof["traffic"] and kernel_ms else None
+    roof["hbm_measured_gbs"] = round(hbm, 1) if hbm is not None else None
+    roof["hbm_measured_frac"] = round(hbm / HBM_PEAK_GBS, 4) if hbm is not None else None
+    if mw is not None and hbm is not None and mw > 0.4 and hbm / HBM_PEAK_GBS < 0.2:
+        roof["bound_pmc"] = "latency"
+    elif vi is not None:
+        roof["bound_pmc"] = "valu" if vi > 0.6 else "issue"
+    else:
+        roof["bound_pmc"] = None
     return roof
 
 
@@ -203,6 +227,11 @@ def cpu_baseline(scene, row_step):
                      f"restated incl. per-visit node-AABB recomputation (bvh.rs:147-152), {threads} threads",
            "host": info}
     out["value_bvh_cached"] = round(res["bvh_cached"][0], 4)
+    # each leg's samples and seconds, and the threads the host allowed
+    out["legs"] = {name: {"msamples_s": round(v_, 4), "samples": int(n_), "s": round(dt_, 2)}
+                   for name, (v_, n_, dt_) in res.items()}
+    out["threads_note"] = (f"{threads} threads = this process's CPU share (affinity {info.get('affinity_cpus')}, "
+                           f"cgroup quota {info.get('cgroup_cpu_quota')}) of a {info.get('os_cpu_count')}-CPU host")
     out["parity"] = parity_on_sample(scene, rows, 99, ref_img)
     return out
 
@@ -297,7 +326,7 @@ def mode_line(scene, cam, precision, tuning, steps, warmup, dev):
             "segments_per_sample": round(st.segments / max(st.samples, 1), 4)}
     esz = 4 if prec == rtw.RTW_F32 else 8
     attach_pmc(line["roofline"], f"book1_simple_{W}x{H}_{SPP}spp_depth{DEPTH}", kname, sha,
-               chunk_sum_bytes=W * H * -(-SPP // int(st.chunk)) * 3 * esz)
+               chunk_sum_bytes=W * H * -(-SPP // int(st.chunk)) * 3 * esz, kernel_ms=avg_ms)
     return line
 
 
@@ -442,13 +471,21 @@ def config_line(name, precision, dev):
         cell_b, light_b = 8, (16 if prec == rtw.RTW_F32 else 32)
         req = st.node_visits * node_b + st.sphere_tests * sph_b + st.grid_cells * cell_b + st.light_tests * light_b
         rate = req / (avg_ms * 1e-3) / 1e9
-        line["roofline"] = {"bound": "hbm", "achieved": round(rate, 2), "peak": 8000.0, "unit": "GB/s",
-                            "frac": round(rate / 8000.0, 4), "bytes_per_launch": int(req),
+        # the requests are gathered rows served by the L2 / Infinity Cache (the working set fits the
+        # 256 MB MALL): priced against the MALL's random-row gather rate, the L2's beside it; the
+        # PMC-measured HBM rate and bound are attached by attach_pmc
+        line["roofline"] = {"bound": "latency", "achieved": round(rate, 2), "peak": MALL_GATHER_GBS, "unit": "GB/s",
+                            "frac": round(rate / MALL_GATHER_GBS, 4), "l2_frac": round(rate / L2_GATHER_GBS, 4),
+                            "bytes_per_launch": int(req),
                             "basis": f"requests from the counters: node_visits x {node_b} B + sphere_tests x {sph_b} B "
-                                     f"+ grid_cells x {cell_b} B + light_tests x {light_b} B (served by L2 / MALL: "
-                                     "the working set fits the 256 MB MALL)",
+                                     f"+ grid_cells x {cell_b} B + light_tests x {light_b} B, served by L2 / MALL "
+                                     "(peak: the Infinity Cache's random-row gather rate, 8.6 TB/s; l2_frac against "
+                                     "the L2's 17 TB/s); bound: latency (waves waiting on memory, HBM far from its "
+                                     "peak: bound_pmc)",
                             "counters": counters_of(st)}
-        attach_pmc(line["roofline"], workload, kname, sha, chunk_sum_bytes=csum)
+        attach_pmc(line["roofline"], workload, kname, sha, chunk_sum_bytes=csum, kernel_ms=avg_ms)
+        if line["roofline"]["bound_pmc"] not in (None, "latency"):
+            line["roofline"]["bound"] = line["roofline"]["bound_pmc"]
     else:
         flops = exe_flops_of(st, n_pl)
         peak = PEAK_FP32_TFLOPS if prec == rtw.RTW_F32 else PEAK_FP64_TFLOPS
@@ -456,7 +493,7 @@ def config_line(name, precision, dev):
         line["roofline"] = {"bound": "valu", "achieved": round(rate, 3), "peak": peak, "unit": "TFLOP/s",
                             "frac": round(rate / peak, 4), "flops_per_launch": int(flops),
                             "flops_basis": FLOPS_BASIS, "counters": counters_of(st)}
-        attach_pmc(line["roofline"], workload, kname, sha, chunk_sum_bytes=csum)
+        attach_pmc(line["roofline"], workload, kname, sha, chunk_sum_bytes=csum, kernel_ms=avg_ms)
     return line
 
 
@@ -634,7 +671,8 @@ def main():
     if plan is not None:
         out["config"]["split_plan"] = plan
     attach_pmc(out["roofline"], out["config"]["workload"], kname, sha,
-               chunk_sum_bytes=W * H * -(-SPP // int(st.chunk)) * 3 * (4 if prec == rtw.RTW_F32 else 8) // world_size)
+               chunk_sum_bytes=W * H * -(-SPP // int(st.chunk)) * 3 * (4 if prec == rtw.RTW_F32 else 8) // world_size,
+               kernel_ms=avg_ms)
     if world_size == 1 and not a.no_modes:
         # the same workload in the other arithmetic modes (single GPU, after the timed region)
         out["modes"] = {}

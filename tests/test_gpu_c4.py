@@ -119,3 +119,35 @@ def test_c4_shares_cost_alike():
     _, _, ms0 = _share(rtw.RTW_F32, 512, 0, 3)
     _, _, ms7 = _share(rtw.RTW_F32, 512, 7, 3)
     assert abs(ms7 / ms0 - 1) < 0.10, (ms0, ms7)
+
+
+def test_c4_share_chunked_fold_vs_sequential_fold_f64():
+    """The parity basis at chunk > 1: the f64 C4 share's
+    chunk sums exceed partial_max at one sample per item, so its items are
+    chunks of st.chunk samples and the fold is chunk-associated -- bit-identical
+    to the oracle WITH that chunk (test above), not to the reference's
+    sample-by-sample fold (camera.rs:322-336).  The two folds differ at
+    rounding level only: the first tile's first row against the oracle's
+    sequential fold (chunk 1), per-pixel MAE of sum/spp well below 1e-5."""
+    tiles, st, _ = _share(rtw.RTW_F64, 4096, 0, 9)
+    assert st.chunk > 1
+    cam = _cam(4096)
+    soa = rtw.scenes.simple_soa(0x5EED0001)[0]
+    # the image's centre tile (over the sphere field; the corner tiles see only
+    # the background, whose samples are all exactly 1 and sum alike in any
+    # order): tx 240, ty 135 -> T = 65040, rank 0's local tile T / 8
+    tx, ty = 240, 135
+    T = ty * (W // 8) + tx
+    assert T % N == 0
+    j, i0 = ty * 8, tx * 8
+    seq, _ = O.render(_ocam(cam), O.Scene(**soa.__dict__), 9, chunk=1, accel=O.ACCEL_BVH_CACHED,
+                      rows=(j, j + 1, 1), cols=(i0, i0 + 8))
+    g, o = tiles[T // N, 0:8], seq[j, i0:i0 + 8]
+    assert np.array_equal(np.isnan(g), np.isnan(o))
+    assert not (o[~np.isnan(o)] == 4096.0).all()          # not background-only samples
+    ok = ~np.isnan(o)
+    mae = float(np.abs(g[ok] - o[ok]).mean() / 4096)
+    print(f"C4 chunk {st.chunk} vs sequential fold: per-pixel MAE {mae:.3e}, "
+          f"bit-identical components {float((g[ok] == o[ok]).mean()):.3f}")
+    assert mae < 1e-5
+    assert mae < 1e-12                  # rounding level: the reassociation of ~4096 adds
