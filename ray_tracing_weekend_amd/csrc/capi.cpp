@@ -110,7 +110,7 @@ struct rtw_ctx {
     // one GPU 117.35 vs 118.46 ms; profiles/r06i_ab_split.jsonl)
     uint32_t guide_div = 16384, guide_max = 128;
     uint32_t cost_time = 1;           // tile costs in wave-time shares (KParams::cost_time); 0: work counts
-    uint64_t guide_floor = 1u << 18;
+    uint64_t guide_floor = 1u << 20;
     void* d_lpt = nullptr;            // pilot: [tile cost | chunk sums | tiles]
     size_t lpt_cap = 0;
     bool lpt_valid = false;           // h_lpt_cost is the pilot of (lpt_cam, lpt_serial, rank split, precision)

@@ -49,6 +49,8 @@ namespace dev {
 #define RTW_PROBE_CLK_END()
 #define RTW_PROBE_WAVE_BEGIN()
 #define RTW_PROBE_WAVE_TASK()
+#define RTW_PROBE_WAVE_DRY()
+#define RTW_PROBE_WAVE_TRIP()
 #define RTW_PROBE_WAVE_END()
 #define RTW_PROBE_PLANES()
 #define RTW_PROBE_CLOSEST()
@@ -2683,6 +2685,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                     t = (uint32_t)__shfl((int)t, (int)leader);
                 }
                 if (t >= k->n_tasks) {   // every task is taken: these lanes are done
+                    RTW_PROBE_WAVE_DRY();
                     more = false;
                     need = false;
                     break;
@@ -2755,6 +2758,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
         }
 #endif
         segs += (uint32_t)__popcll(live);   // every active lane runs one segment of this trip
+        RTW_PROBE_WAVE_TRIP();
         bool lamb = false;                  // the lane's segment ended in a Lambertian scatter
         // (kCoopGrid) this trip's pending light pdf and the bounce's weights: set by
         // the Lambertian branch, consumed by the walk at the end of the same trip --

@@ -85,14 +85,17 @@
 #ifdef RTW_TIMELINE
 // tools/share_timeline.py: per wave kTlWords words -- {begin, end} wall-clock
 // ticks (100 MHz), task count | last task << 32, XCC id | HW_ID << 32, the
-// wave's lane-segments, the tick it took its last task -- read back with
+// wave's lane-segments, the tick it took its last task, the tick it found the
+// task counter dry and its trips after that -- read back with
 // rtw_probe_timeline_read
-constexpr uint32_t kTlWaves = 1 << 16, kTlWords = 6;
+constexpr uint32_t kTlWaves = 1 << 16, kTlWords = 8;
 static __device__ unsigned long long g_tl[kTlWaves * kTlWords];
 #define RTW_PROBE_WAVE_BEGIN() \
-    uint64_t tl_begin_ = wall_clock64(), tl_last_t_ = tl_begin_; \
-    uint32_t tl_tasks_ = 0, tl_last_ = 0
+    uint64_t tl_begin_ = wall_clock64(), tl_last_t_ = tl_begin_, tl_dry_t_ = 0; \
+    uint32_t tl_tasks_ = 0, tl_last_ = 0, tl_dry_trips_ = 0
 #define RTW_PROBE_WAVE_TASK() (++tl_tasks_, tl_last_ = t, tl_last_t_ = wall_clock64())
+#define RTW_PROBE_WAVE_DRY() (tl_dry_t_ = tl_dry_t_ ? tl_dry_t_ : wall_clock64())
+#define RTW_PROBE_WAVE_TRIP() (tl_dry_trips_ += tl_dry_t_ ? 1u : 0u)
 #define RTW_PROBE_WAVE_END() \
     do { \
         const uint32_t w_ = blockIdx.x * kWavesPerBlock + wave; \
@@ -107,6 +110,8 @@ static __device__ unsigned long long g_tl[kTlWaves * kTlWords];
             r_[3] = (xcc_ & 0xf) | ((unsigned long long)hw_ << 32); \
             r_[4] = segs; \
             r_[5] = tl_last_t_; \
+            r_[6] = tl_dry_t_; \
+            r_[7] = tl_dry_trips_; \
         } \
     } while (0)
 extern "C" int rtw_probe_timeline_read(unsigned long long* out, size_t n, int reset) {
@@ -122,6 +127,8 @@ extern "C" int rtw_probe_timeline_read(unsigned long long* out, size_t n, int re
 #else
 #define RTW_PROBE_WAVE_BEGIN()
 #define RTW_PROBE_WAVE_TASK()
+#define RTW_PROBE_WAVE_DRY()
+#define RTW_PROBE_WAVE_TRIP()
 #define RTW_PROBE_WAVE_END()
 #endif
 

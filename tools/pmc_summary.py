@@ -53,6 +53,26 @@ if len(sys.argv) > 3 and sys.argv[2] == "--traffic":
         d["wave_wait_frac"] = round(avg("SQ_WAIT_INST_ANY") / avg("SQ_WAVE_CYCLES"), 4)
     if agg.get("SQ_WAIT_ANY") and agg.get("SQ_WAVE_CYCLES"):
         d["mem_wait_frac"] = round(avg("SQ_WAIT_ANY") / avg("SQ_WAVE_CYCLES"), 4)
+    # where the wave-cycles go (the attribution passes of tools/profile.sh):
+    # cycles issuing each instruction type and waiting, as shares of
+    # SQ_WAVE_CYCLES, and the mean cycles an instruction of each memory kind
+    # is outstanding (SQ_INST_LEVEL_* / SQ_INSTS_*, Little's law)
+    if agg.get("SQ_WAVE_CYCLES"):
+        wc = avg("SQ_WAVE_CYCLES")
+        att = {}
+        for k in ("SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_SCA", "SQ_ACTIVE_INST_LDS",
+                  "SQ_ACTIVE_INST_VMEM", "SQ_ACTIVE_INST_MISC", "SQ_ACTIVE_INST_FLAT", "SQ_WAIT_ANY",
+                  "SQ_WAIT_INST_ANY", "SQ_WAIT_INST_LDS"):
+            if agg.get(k):
+                att[k.replace("SQ_", "").lower() + "_frac"] = round(avg(k) / wc, 4)
+        for lvl, n in (("SQ_INST_LEVEL_VMEM", "SQ_INSTS_VMEM"), ("SQ_INST_LEVEL_LDS", "SQ_INSTS_LDS"),
+                       ("SQ_INST_LEVEL_SMEM", "SQ_INSTS_SMEM")):
+            if agg.get(lvl) and agg.get(n):
+                att[n.replace("SQ_INSTS_", "").lower() + "_cycles_outstanding"] = round(avg(lvl) / avg(n), 1)
+        if agg.get("SQ_INSTS_BRANCH") and agg.get("SQ_INSTS_VALU"):
+            att["branches_per_valu"] = round(avg("SQ_INSTS_BRANCH") / avg("SQ_INSTS_VALU"), 4)
+        if att:
+            d["attribution"] = att
     d["pmc_source"] = root
     names = set()
     for f in glob.glob(f"{root}/pmc*/pmc_counter_collection.csv"):

@@ -18,7 +18,10 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$TAG" -o trace 
   -- python3 "$PROG" $ARGS > "$OUT/prof_${TAG}_trace.log" 2>&1
 rc=$?; echo "trace rc=$rc"; if bad $rc; then exit $rc; fi
 # counter sets separated by ';' (PMC_SETS overrides the default list)
-SETS="${PMC_SETS:-FETCH_SIZE;WRITE_SIZE;SQ_WAVES SQ_INSTS_VALU SQ_THREAD_CYCLES_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY;SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE}"
+# (the last two sets attribute the wave-cycles: cycles issuing each
+# instruction type, LDS waits, branches; outstanding-instruction levels for
+# the memory latencies -- tools/pmc_summary.py --attrib)
+SETS="${PMC_SETS:-FETCH_SIZE;WRITE_SIZE;SQ_WAVES SQ_INSTS_VALU SQ_THREAD_CYCLES_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY;SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE;SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_MISC SQ_ACTIVE_INST_FLAT SQ_WAIT_INST_LDS SQ_INSTS_BRANCH;SQ_INST_LEVEL_VMEM SQ_INSTS_VMEM SQ_INST_LEVEL_LDS SQ_INST_LEVEL_SMEM SQ_INSTS_SMEM SQ_INST_CYCLES_SMEM SQ_INSTS_FLAT SQ_WAVE_CYCLES}"
 i=0
 IFS=';' read -ra SETLIST <<< "$SETS"
 for set in "${SETLIST[@]}"; do

@@ -45,7 +45,7 @@ def run(a):
     import ray_tracing_weekend_amd as rtw
     rd = rtw._lib.rtw_probe_timeline_read
     rd.argtypes = [C.POINTER(C.c_ulonglong), C.c_size_t, C.c_int]
-    n_tl = (1 << 16) * 6
+    n_tl = (1 << 16) * 8
     buf_tl = (C.c_ulonglong * n_tl)()
     W, H, SPP = 1200, 800, 500
     if a.config:
@@ -76,13 +76,13 @@ def run(a):
         torch.cuda.synchronize()
         kern = r.get_timings(1)[0][0]
         rd(buf_tl, n_tl, 1)
-        t = np.frombuffer(buf_tl, dtype=np.uint64).reshape(-1, 6).astype(np.int64)
+        t = np.frombuffer(buf_tl, dtype=np.uint64).reshape(-1, 8).astype(np.int64)
         t = t[t[:, 1] > 0]
         last_task = t[:, 2] >> 32
         t[:, 2] &= 0xFFFFFFFF
         hw = t[:, 3] >> 32
         t[:, 3] &= 0xF
-        segs, last_t = t[:, 4], t[:, 5]
+        segs, last_t, dry_t, dry_trips = t[:, 4], t[:, 5], t[:, 6], t[:, 7]
         t0 = t[:, 0].min()
         beg, end = (t[:, 0] - t0) / 100.0, (t[:, 1] - t0) / 100.0     # microseconds
         span = end.max()
@@ -107,6 +107,11 @@ def run(a):
             "last10_seg_rate_vs_median": [round(float(x), 3) for x in
                                           (segs / (end - beg) / np.median(segs / (end - beg)))[np.argsort(end)[-10:]]],
             "last10_wave_slot": [int(x & 0xF) for x in hw[np.argsort(end)[-10:]]],
+            # when each of the 10 last waves found the task counter dry (ms), and its trips after that
+            "last10_dry_ms": [round(float(x - t0) / 1e5, 3) if x else None for x in dry_t[np.argsort(end)[-10:]]],
+            "last10_trips_after_dry": [int(x) for x in dry_trips[np.argsort(end)[-10:]]],
+            "dry_ms_p1_p50_max": [round(float(np.percentile(dry_t[dry_t > 0] - t0, p)) / 1e5, 3) for p in (1, 50, 100)],
+            "trips_after_dry_p50_p99_max": [int(np.percentile(dry_trips, p)) for p in (50, 99, 100)],
             "last10_simd": [int((x >> 4) & 3) for x in hw[np.argsort(end)[-10:]]],
             # per wave slot: mean lane-segments per us relative to the mean, and tasks taken
             "seg_rate_by_wave_slot": {int(s_): round(float((segs / (end - beg))[(hw & 0xF) == s_].mean() /
