@@ -273,7 +273,7 @@ int rtw_set_accel(rtw_ctx *ctx, int accel);
  * "max_group" (longest-first task list: at most this many chunks per task, default 32),
  * "grid_piece" (f32 light-grid walks: cells per piece of the wave's cooperative walk,
  * default by grid size: its widest side / 14, 4..16; 0 = every lane walks its own ray),
- * "light_leaf" (light spheres per light-BVH leaf, 1..15; 0 = 4), "partial_max" (bytes of chunk sums an auto chunk may use, default 24 GiB),
+ * "light_leaf" (light spheres per light-BVH leaf, 1..15; 0 = 4), "partial_max" (bytes of chunk sums an auto chunk may use, default 128 GiB, at most half the device's memory; an auto chunk doubles if the allocation fails),
  * "bvh_kind" (3 = binary while-while on the tree staged in LDS, the
  * default, 1 = binary while-while from L1/L2, 2 = 4-wide octant BVH, 0 =
  * binary single loop), "bvh_lds_max" (LDS bytes per workgroup bvh_kind 3 may

@@ -29,10 +29,15 @@ struct rtw_ctx {
     uint32_t chunk = 0;           // samples per item (0 = auto_chunk)
     uint32_t auto_chunk = 1;      // one sample per item: the chunk fold is then the reference's
                                   // sample-by-sample fold exactly
-    // cap of the chunk-sum buffer (the auto chunk grows beyond it): 24 GiB of the
-    // 288 GB of HBM keeps every one-GPU BASELINE config at one sample per item --
-    // the reference's fold order exactly (C2 f64: 11.5 GB)
-    size_t partial_max = (size_t)24 << 30;
+    // cap of the chunk-sum buffer (the auto chunk grows beyond it), at most half
+    // the device's memory: 128 GiB of the 288 GB of HBM keeps every BASELINE
+    // config at one sample per item -- the reference's fold order exactly (C2
+    // f64: 11.5 GB, C3 f64 51 GB, a C4 f64 8-way share 102 GB).  Chunk 1 is
+    // also the faster form: a chunk > 1 reads its running sum back at every
+    // sample's end (C3 f64 1083 vs 1121 ms at chunk 2, a C4 share 958 vs 993
+    // ms at chunk 4, profiles/r06h_ab_chunk.jsonl, r06i_ab_c4_chunk.jsonl)
+    size_t partial_max = (size_t)128 << 30;
+    size_t dev_total = 0;         // the device's memory (hipMemGetInfo), 0 until asked
     uint32_t group = 0;           // chunks per wave task (0 = from target_tasks)
     uint64_t target_tasks = 0;   // auto chunks-per-task: about this many tasks (0: 2^19 with
                                  // persistent waves, 2^17 without), 4..32 chunks per task
@@ -1127,13 +1132,38 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
     // wavefront's dynamic item pool.  Small chunks balance the lanes of a
     // wave; enough tasks keep the dispatcher fed to the end of the launch.
     uint32_t chunk = c->chunk ? c->chunk : c->auto_chunk;
+    const size_t per_chunk = (size_t)p.n_local_tiles * 64 * 3 * sizeof(R);
     if (!c->chunk && p.spp) {
-        // keep the chunk sums within partial_max: bytes = ceil(spp/chunk) * tiles * 64 * 3 * sizeof(R)
-        const size_t per_chunk = (size_t)p.n_local_tiles * 64 * 3 * sizeof(R);
-        const size_t max_chunks = std::max<size_t>(1, c->partial_max / std::max<size_t>(per_chunk, 1));
+        // keep the chunk sums within partial_max and half the device's memory
+        // (deterministic: the chunk, and so the fold order, never depends on
+        // what else holds memory): bytes = ceil(spp/chunk) * tiles * 64 * 3 * sizeof(R)
+        size_t pmax = c->partial_max;
+        if (!c->dev_total) {
+            size_t fr = 0, tot = 0;
+            if (hipMemGetInfo(&fr, &tot) == hipSuccess) c->dev_total = tot;
+        }
+        if (c->dev_total) pmax = std::min(pmax, c->dev_total / 2);
+        const size_t max_chunks = std::max<size_t>(1, pmax / std::max<size_t>(per_chunk, 1));
         while ((p.spp + chunk - 1) / chunk > max_chunks) ++chunk;
     }
     chunk = std::max<uint32_t>(1, std::min<uint32_t>(chunk, std::max<uint32_t>(p.spp, 1)));
+    // the chunk-sum buffer; when the device cannot hold it (other allocations)
+    // an auto chunk doubles instead of failing -- stats.chunk reports it, the
+    // fold is then chunk-associated (rounding level)
+    for (;;) {
+        const uint32_t nc = p.spp ? (p.spp + chunk - 1) / chunk : 0;
+        const size_t bytes = std::max<size_t>((size_t)nc * per_chunk, 64);
+        if (c->partial_cap >= bytes) break;
+        if (c->d_partial) (void)hipFree(c->d_partial);
+        c->d_partial = nullptr;
+        c->partial_cap = 0;
+        const hipError_t e = hipMalloc(&c->d_partial, bytes);
+        if (e == hipSuccess) { c->partial_cap = bytes; break; }
+        c->d_partial = nullptr;
+        (void)hipGetLastError();
+        if (c->chunk || chunk >= p.spp || e != hipErrorOutOfMemory) return hip_fail(c, e, "hipMalloc(chunk sums)");
+        chunk = std::min<uint32_t>(chunk * 2, p.spp);
+    }
     p.chunk = chunk;
     p.n_chunks = p.spp ? (p.spp + chunk - 1) / chunk : 0;
     uint32_t group = c->group;
@@ -1158,9 +1188,7 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
     p.n_tasks = p.n_local_tiles * p.n_groups;
     p.item_order = c->item_order;
     p.persist = c->persist;
-    const size_t partial_bytes = std::max<size_t>((size_t)p.n_chunks * p.n_local_tiles * 64 * 3 * sizeof(R), 64);
-    int rc = ensure(c, &c->d_partial, &c->partial_cap, partial_bytes);
-    if (rc) return rc;
+    int rc = RTW_OK;
     p.partial = reinterpret_cast<R*>(c->d_partial);
     p.counters = c->d_counters;
     HIP_TRY(c, hipMemsetAsync(c->d_counters, 0, rtw_ctx::kCounters * sizeof(unsigned long long), stream));

@@ -3,13 +3,15 @@ split over 8 GPUs by 8x8 tiles (tile T -> rank T % 8) and gathered.
 
 The full C4 render is 34 G samples; on one GPU these tests run
   * the full 3840x2160 frame at 2 spp in f64, rows pinned to the oracle;
-  * rank 0's 1/8 share (16 200 tiles) at the full 4096 spp in f32 -- the
-    chunk sums of that share (4096 x 1.04 M pixels x 12 B = 51 GB at one
-    sample per item) exceed partial_max (24 GiB), so the auto chunk grows
-    and the chunk sums are folded in double (reduce_chunks_kernel);
-  * the same share's first tile in f64 at 4096 spp against the oracle with
-    the same chunk (bit for bit), and rank 7's share in f32 against rank 0's
-    cost (balance).
+  * rank 0's 1/8 share (16 200 tiles) at the full 4096 spp in f32 -- its
+    chunk sums at one sample per item (4096 x 1.04 M pixels x 12 B = 51 GB)
+    fit the default partial_max (128 GiB, at most half the device), so the
+    share runs at chunk 1; under a 24 GiB budget the auto chunk grows and the
+    chunk sums are folded in double (reduce_chunks_kernel);
+  * the same share in f64 at 4096 spp (102 GB of one-sample sums, chunk 1)
+    against the oracle's sequential fold bit for bit, and at a forced chunk > 1
+    against the same fold to rounding level (the parity basis at chunk > 1);
+    rank 7's share in f32 against rank 0's cost (balance).
 """
 import numpy as np
 import pytest
@@ -73,12 +75,12 @@ def share0():
     return _share(rtw.RTW_F32, 4096, 0, 7)
 
 
-def test_c4_share_at_4096_spp_grows_the_chunk(share0):
+def test_c4_share_at_4096_spp_runs_one_sample_per_item(share0):
     tiles, st, ms = share0
     assert tiles.shape[0] == 16200
     assert st.samples == 16200 * 64 * 4096
-    # 51 GB of one-sample chunk sums would exceed partial_max: the chunk grew
-    assert st.chunk > 1 and (4096 + st.chunk - 1) // st.chunk * 16200 * 64 * 12 <= 24 << 30
+    # 51 GB of one-sample chunk sums fit the default budget: the reference's fold order
+    assert st.chunk == 1 and 4096 * 16200 * 64 * 12 <= 128 << 30
     sums = tiles.reshape(-1, 3)
     fin = np.isfinite(sums).all(-1)
     assert fin.mean() > 0.5
@@ -87,30 +89,32 @@ def test_c4_share_at_4096_spp_grows_the_chunk(share0):
     print(f"C4 rank-0 share: {ms:.1f} ms, chunk {st.chunk}, {st.samples / ms / 1e3:.0f} Msamples/s")
 
 
+def test_c4_share_grows_the_chunk_under_a_smaller_budget(share0):
+    """partial_max 24 GiB (the round-5 default): 51 GB of one-sample sums do
+    not fit, the auto chunk grows until they do; the sums agree with chunk 1's
+    to f32 summation rounding."""
+    tiles, _, _ = share0
+    other, st, _ = _share(rtw.RTW_F32, 4096, 0, 7, tuning={"partial_max": 24 << 30})
+    assert st.chunk > 1 and (4096 + st.chunk - 1) // st.chunk * 16200 * 64 * 12 <= 24 << 30
+    a, b = tiles.reshape(-1, 3), other.reshape(-1, 3)
+    assert np.array_equal(np.isfinite(a).all(-1), np.isfinite(b).all(-1))
+    ok = np.isfinite(a).all(-1)
+    rel = np.abs(a[ok] - b[ok]) / np.maximum(np.abs(a[ok]), 1.0)
+    assert rel.max() < 1e-4, rel.max()
+
+
 def test_c4_share_chunk_does_not_change_the_samples(share0):
     """Chunking only regroups the fold of each pixel's samples: the share's
-    sums with a 4x larger chunk agree with the auto-chunk sums to f32
-    summation rounding (the paths are the same RNG words)."""
+    sums at chunk 4 agree with chunk 1's to f32 summation rounding (the paths
+    are the same RNG words)."""
     tiles, st, _ = share0
-    other, st2, _ = _share(rtw.RTW_F32, 4096, 0, 7, tuning={"chunk": int(st.chunk) * 4})
-    assert st2.chunk == st.chunk * 4
+    other, st2, _ = _share(rtw.RTW_F32, 4096, 0, 7, tuning={"chunk": 4})
+    assert st2.chunk == 4
     a, b = tiles.reshape(-1, 3), other.reshape(-1, 3)
     ok = np.isfinite(a).all(-1) & np.isfinite(b).all(-1)
     assert np.array_equal(np.isfinite(a).all(-1), np.isfinite(b).all(-1))
     rel = np.abs(a[ok] - b[ok]) / np.maximum(np.abs(a[ok]), 1.0)
     assert rel.max() < 1e-4, rel.max()
-
-
-def test_c4_share_first_tile_f64_matches_oracle_at_4096_spp():
-    tiles, st, _ = _share(rtw.RTW_F64, 4096, 0, 9)
-    cam = _cam(4096)
-    soa = rtw.scenes.simple_soa(0x5EED0001)[0]
-    # rank 0's first tile is global tile 0: pixels i 0..7, j 0..7; check row j = 0
-    ref, _ = O.render(_ocam(cam), O.Scene(**soa.__dict__), 9, chunk=int(st.chunk), accel=O.ACCEL_BVH_CACHED,
-                      rows=(0, 1, 1), cols=(0, 8))
-    g = tiles[0, 0:8]
-    o = ref[0, 0:8]
-    assert np.array_equal(np.nan_to_num(g, nan=-7), np.nan_to_num(o, nan=-7))
 
 
 def test_c4_shares_cost_alike():
@@ -121,31 +125,70 @@ def test_c4_shares_cost_alike():
     assert abs(ms7 / ms0 - 1) < 0.10, (ms0, ms7)
 
 
-def test_c4_share_chunked_fold_vs_sequential_fold_f64():
-    """The parity basis at chunk > 1: the f64 C4 share's
-    chunk sums exceed partial_max at one sample per item, so its items are
-    chunks of st.chunk samples and the fold is chunk-associated -- bit-identical
-    to the oracle WITH that chunk (test above), not to the reference's
-    sample-by-sample fold (camera.rs:322-336).  The two folds differ at
-    rounding level only: the first tile's first row against the oracle's
-    sequential fold (chunk 1), per-pixel MAE of sum/spp well below 1e-5."""
-    tiles, st, _ = _share(rtw.RTW_F64, 4096, 0, 9)
-    assert st.chunk > 1
-    cam = _cam(4096)
-    soa = rtw.scenes.simple_soa(0x5EED0001)[0]
-    # a tile over a diffuse or metal surface: the first of the share whose first
-    # row's sums are all finite and none an integer (the background and paths
-    # through glass only are samples of exactly 1, which sum alike in any order)
+@pytest.fixture(scope="module")
+def share0_f64():
+    return _share(rtw.RTW_F64, 4096, 0, 9)
+
+
+@pytest.fixture(scope="module")
+def share0_f64_chunked():
+    return _share(rtw.RTW_F64, 4096, 0, 9, tuning={"partial_max": 24 << 30})
+
+
+def _surface_row(tiles):
+    """A tile over a diffuse or metal surface: the first of the share whose
+    first row's sums are all finite and none an integer (the background and
+    paths through glass only are samples of exactly 1, which sum alike in any
+    order).  Returns (local tile, image row j, first column i0)."""
     row0 = tiles[:, 0:8]
     good = np.isfinite(row0).all(axis=(1, 2)) & (row0 != np.round(row0)).all(axis=(1, 2))
     lt = int(np.argmax(good))
     assert good[lt]
     T = lt * N                                  # rank 0's local tile lt is global tile lt * 8
     tx, ty = T % (W // 8), T // (W // 8)
-    j, i0 = ty * 8, tx * 8
+    return lt, ty * 8, tx * 8
+
+
+def test_c4_share_f64_at_chunk_1_is_the_sequential_fold(share0_f64):
+    """The f64 share at the default budget runs one sample per item (102 GB of
+    sums): bit-identical to the oracle's sequential fold (camera.rs:322-336)
+    on a surface tile's row."""
+    tiles, st, _ = share0_f64
+    assert st.chunk == 1
+    lt, j, i0 = _surface_row(tiles)
+    cam = _cam(4096)
+    soa = rtw.scenes.simple_soa(0x5EED0001)[0]
     seq, _ = O.render(_ocam(cam), O.Scene(**soa.__dict__), 9, chunk=1, accel=O.ACCEL_BVH_CACHED,
                       rows=(j, j + 1, 1), cols=(i0, i0 + 8))
-    g, o = tiles[lt, 0:8], seq[j, i0:i0 + 8]
+    assert np.array_equal(np.nan_to_num(tiles[lt, 0:8], nan=-7), np.nan_to_num(seq[j, i0:i0 + 8], nan=-7))
+
+
+def test_c4_share_f64_chunked_matches_oracle_with_its_chunk(share0_f64, share0_f64_chunked):
+    """At chunk > 1 the render is bit-identical to the oracle's
+    chunk-associated fold (rtw_oracle.c, `chunk`) with the same chunk."""
+    tiles, st, _ = share0_f64_chunked
+    assert st.chunk > 1
+    lt, j, i0 = _surface_row(share0_f64[0])
+    cam = _cam(4096)
+    soa = rtw.scenes.simple_soa(0x5EED0001)[0]
+    ref, _ = O.render(_ocam(cam), O.Scene(**soa.__dict__), 9, chunk=int(st.chunk), accel=O.ACCEL_BVH_CACHED,
+                      rows=(j, j + 1, 1), cols=(i0, i0 + 8))
+    assert np.array_equal(np.nan_to_num(tiles[lt, 0:8], nan=-7), np.nan_to_num(ref[j, i0:i0 + 8], nan=-7))
+
+
+def test_c4_share_chunked_fold_vs_sequential_fold_f64(share0_f64, share0_f64_chunked):
+    """The parity basis at chunk > 1: under a 24 GiB budget
+    the f64 share's items are chunks of st.chunk samples and the fold is
+    chunk-associated -- bit-identical to the oracle WITH that chunk (test
+    above), not to the
+    reference's sample-by-sample fold.  The two folds differ at rounding level
+    only: a surface tile's row against the sequential fold (the chunk-1
+    render), per-pixel MAE of sum/spp well below 1e-5."""
+    seq_tiles, _, _ = share0_f64
+    tiles, st, _ = share0_f64_chunked
+    assert st.chunk > 1
+    lt, _, _ = _surface_row(seq_tiles)
+    g, o = tiles[lt, 0:8], seq_tiles[lt, 0:8]
     assert np.array_equal(np.isnan(g), np.isnan(o))
     ok = ~np.isnan(o)
     mae = float(np.abs(g[ok] - o[ok]).mean() / 4096)
@@ -153,3 +196,8 @@ def test_c4_share_chunked_fold_vs_sequential_fold_f64():
           f"bit-identical components {float((g[ok] == o[ok]).mean()):.3f}")
     assert mae < 1e-5
     assert mae < 1e-12                  # rounding level: the reassociation of ~4096 adds
+    # the whole share: every pixel within rounding of the sequential fold
+    a, b = tiles.reshape(-1, 3), seq_tiles.reshape(-1, 3)
+    fin = np.isfinite(b).all(-1)
+    assert np.array_equal(np.isfinite(a).all(-1), fin)
+    assert float(np.abs(a[fin] - b[fin]).mean() / 4096) < 1e-12
