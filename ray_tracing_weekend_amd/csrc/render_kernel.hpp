@@ -346,6 +346,21 @@ struct LightPre {
     }
 };
 
+// Inserts x into ids[0..kMax) (ascending; empty entries ~0u) by one
+// compare-exchange pass with static indices -- a shifting insertion's dynamic
+// register indices compile to 8-way select chains per step -- and returns the
+// value that fell off the end (~0u: none did).
+template <uint32_t kMax>
+__device__ __forceinline__ uint32_t sorted_insert(uint32_t (&ids)[kMax], uint32_t x) {
+#pragma unroll
+    for (uint32_t q = 0; q < kMax; ++q) {
+        const uint32_t a = ids[q];
+        ids[q] = min(a, x);
+        x = max(a, x);
+    }
+    return x;
+}
+
 // HittableList::pdf_value's sum over the hit lights in LIST order (f64) when
 // an acceleration structure finds them in another order: `walk(lo, add)` calls
 // add(id) once for every light the ray hits, in any order, and each pass keeps
@@ -360,24 +375,15 @@ __device__ __forceinline__ R lights_sum_ids_in_list_order(Walk&& walk, Pdf&& pdf
     uint32_t lo = 0;
     for (;;) {
         uint32_t ids[kMax];
-        uint32_t n = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < kMax; ++q) ids[q] = 0xffffffffu;
         bool dropped = false;
         walk([&](uint32_t id) {
             if (id < lo) return;
-            if (n == kMax) {
-                dropped = true;
-                if (id > ids[kMax - 1]) return;
-                --n;                       // the largest gives way
-            }
-            uint32_t q = n;                // insertion by list index
-            while (q > 0 && ids[q - 1] > id) {
-                ids[q] = ids[q - 1];
-                --q;
-            }
-            ids[q] = id;
-            ++n;
+            // by list index; when full the largest gives way
+            if (sorted_insert(ids, id) != 0xffffffffu) dropped = true;
         });
-        for (uint32_t q = 0; q < n; ++q) acc = acc + pdf(ids[q]);
+        for (uint32_t q = 0; q < kMax && ids[q] != 0xffffffffu; ++q) acc = acc + pdf(ids[q]);
         if (!dropped) return acc;
         lo = ids[kMax - 1] + 1u;
     }
@@ -1984,8 +1990,14 @@ __device__ __forceinline__ R lights_pdf_grid_coop_list(const DevScene<float>& g,
             const bool mine = more && (kp ? first >= B && first + kp <= B + cap : B == 0);   // the ray is in the round
             const uint64_t later = __ballot(kp && first >= B && !mine);
             const uint32_t Bn = later ? (uint32_t)__shfl((int)first, (int)__builtin_ctzll(later)) : total;
+            // a round of at most 64 pieces (the usual case: cap is 64 at the
+            // host's minimum stack) keeps the mask of its pieces that hold a
+            // candidate, so that an owner's merge reads only those slots
+            const bool one_pass = RTW_COOP_HELD && Bn - B <= 64u;
+            uint64_t held = ~0ull;
             for (uint32_t r = B; r < Bn; r += 64) {
                 const uint32_t gi = r + lane;
+                bool has = false;
                 uint32_t own = 0;
 #pragma unroll
                 for (uint32_t step = 32; step; step >>= 1) {
@@ -2043,7 +2055,10 @@ __device__ __forceinline__ R lights_pdf_grid_coop_list(const DevScene<float>& g,
                     }, &lw.cells);
 #endif
                     ent[-1] = cnt;
+                    has = cnt != 0;
                 }
+                const uint64_t h = __ballot(has);
+                if (one_pass) held = h;
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
@@ -2062,23 +2077,14 @@ __device__ __forceinline__ R lights_pdf_grid_coop_list(const DevScene<float>& g,
             bool owning = mine;
             while (RTW_COOP_DEAL ? __any(owning) : owning) {
                 uint32_t ids[kMax];
+#pragma unroll
+                for (uint32_t q = 0; q < kMax; ++q) ids[q] = 0xffffffffu;
                 uint32_t n = 0, bp = 0xffffffffu, bound = 0xffffffffu;   // bp: below a piece's dropped candidates
                 if (owning) {
                     RTW_PROBE_LANES(13);
                     bool dropped = false;
                     auto add = [&](uint32_t id) {   // the kMax smallest list indices (lights_sum_in_list_order)
-                        if (n == kMax) {
-                            dropped = true;
-                            if (id > ids[kMax - 1]) return;
-                            --n;
-                        }
-                        uint32_t q = n;
-                        while (q > 0 && ids[q - 1] > id) {
-                            ids[q] = ids[q - 1];
-                            --q;
-                        }
-                        ids[q] = id;
-                        ++n;
+                        if (sorted_insert(ids, id) != 0xffffffffu) dropped = true;
                     };
                     // the big list's candidates, tested once per walk (bigc below)
                     if (!big_over) {
@@ -2090,7 +2096,7 @@ __device__ __forceinline__ R lights_pdf_grid_coop_list(const DevScene<float>& g,
                             if (id >= lo && big_hit(g.lg_sph[q])) add(id);
                         }
                     }
-                    for (uint32_t gi = first; gi < first + kp; ++gi) {
+                    auto merge_piece = [&](uint32_t gi) {
                         typedef uint32_t u4 __attribute__((ext_vector_type(4)));
                         const u4* sl = reinterpret_cast<const u4*>(slots + (gi - B) * kSlot);
                         RTW_PROBE_LANES(14);
@@ -2101,8 +2107,18 @@ __device__ __forceinline__ R lights_pdf_grid_coop_list(const DevScene<float>& g,
                         for (uint32_t q = 0; q < kPieceIds; ++q)
                             if (q < cnt && e[q] >= lo) add(e[q]);
                         if (cnt > kPieceIds) bp = min(bp, e[kPieceIds - 1]);
+                    };
+                    if (one_pass) {
+                        // only the ray's pieces with a candidate (first - B + kp <= 64)
+                        uint64_t m = kp ? held >> (first - B) : 0ull;
+                        if (kp < 64u) m &= (1ull << kp) - 1ull;
+                        for (; m; m &= m - 1ull) merge_piece(first + (uint32_t)__builtin_ctzll(m));
+                    } else {
+                        for (uint32_t gi = first; gi < first + kp; ++gi) merge_piece(gi);
                     }
                     bound = dropped ? min(bp, ids[kMax - 1]) : bp;
+#pragma unroll
+                    for (uint32_t q = 0; q < kMax; ++q) n += ids[q] != 0xffffffffu ? 1u : 0u;
                 }
                 mark(16);
                 if constexpr (RTW_COOP_DEAL != 0) {

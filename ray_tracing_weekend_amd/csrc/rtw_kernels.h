@@ -186,6 +186,11 @@ constexpr uint32_t kCoopStash64 = RTW_STASH64_EXTRA ? 34u : 20u;
 #ifndef RTW_COOP64_PIECE_IDS
 #define RTW_COOP64_PIECE_IDS 6
 #endif
+// the f64 list walk's owners merge only the pieces that hold a candidate
+// (a ballot mask per round of <= 64 pieces); 0: every piece's slot
+#ifndef RTW_COOP_HELD
+#define RTW_COOP_HELD 1
+#endif
 #ifndef RTW_COOP64_MAX
 #define RTW_COOP64_MAX 8
 #endif
