@@ -228,9 +228,8 @@ __host__ __device__ inline void light_grid_walk_piece_rec(const DevScene<R>& sc,
                                                           const R4<float>* __restrict__ items, V3<R> o, V3<R> d, R ix,
                                                           R iy, R iz, R t0, R t1, bool head, bool tail, Item&& item,
                                                           uint32_t* ncell = nullptr, uint32_t* ntest = nullptr) {
-    light_grid_walk_cells(sc, o, d, ix, iy, iz, t0, t1, head, tail, [&](uint32_t c, R te, R tx) {
-        const R4<float>* r = rec + (size_t)kGridRecSlots * c;
-        const R4<float> s0 = r[0], s1 = r[1], s2 = r[2], s3 = r[3];
+    auto tests = [&](uint32_t c, R te, R tx, const R4<float>& s0, const R4<float>& s1, const R4<float>& s2,
+                     const R4<float>& s3) {
         const bool link = grid_rec_bits(s3.z) == kGridRecLink;
         const uint32_t lb = grid_rec_bits(s3.x), ln = link ? grid_rec_bits(s3.y) : 0u;
         if (ncell) ++*ncell;
@@ -240,7 +239,35 @@ __host__ __device__ inline void light_grid_walk_piece_rec(const DevScene<R>& sc,
         item(s2, [&]() { return sc.lg_start[c] + 2u; }, te, tx);
         item(s3, [&]() { return sc.lg_start[c] + 3u; }, te, tx);
         for (uint32_t q = lb; q < lb + ln; ++q) item(items[q], [q]() { return q; }, te, tx);
+    };
+#if RTW_GRID_PF
+    // one cell ahead: a cell's record is loaded before the previous cell's
+    // tests run, so two of a lane's record loads are in flight
+    bool have = false;
+    uint32_t pc = 0;
+    R pte = 0, ptx = 0;
+    R4<float> p0{}, p1{}, p2{}, p3{};
+    light_grid_walk_cells(sc, o, d, ix, iy, iz, t0, t1, head, tail, [&](uint32_t c, R te, R tx) {
+        const R4<float>* r = rec + (size_t)kGridRecSlots * c;
+        const R4<float> s0 = r[0], s1 = r[1], s2 = r[2], s3 = r[3];
+        if (have) tests(pc, pte, ptx, p0, p1, p2, p3);
+        have = true;
+        pc = c;
+        pte = te;
+        ptx = tx;
+        p0 = s0;
+        p1 = s1;
+        p2 = s2;
+        p3 = s3;
     });
+    if (have) tests(pc, pte, ptx, p0, p1, p2, p3);
+#else
+    light_grid_walk_cells(sc, o, d, ix, iy, iz, t0, t1, head, tail, [&](uint32_t c, R te, R tx) {
+        const R4<float>* r = rec + (size_t)kGridRecSlots * c;
+        const R4<float> s0 = r[0], s1 = r[1], s2 = r[2], s3 = r[3];
+        tests(c, te, tx, s0, s1, s2, s3);
+    });
+#endif
 }
 
 }  // namespace dev

@@ -2019,6 +2019,12 @@ __device__ __forceinline__ R lights_pdf_grid_coop_list(const DevScene<float>& g,
                     const float ra = len2_f32(rd);
                     uint32_t* ent = slots + (gi - B) * kSlot + 1;
                     uint32_t cnt = 0;
+#if RTW_PIECE_REG
+                    // (RTW_PIECE_REG: the candidates in registers, the slot written once)
+                    uint32_t pid[kPieceIds];
+#pragma unroll
+                    for (uint32_t q = 0; q < kPieceIds; ++q) pid[q] = 0xffffffffu;
+#endif
                     // a light of the piece: a candidate (its list index kept) when the
                     // test may hit it in the cell's interval; idx(): its lg_id slot
                     auto test = [&](const R4<float>& L, auto&& idx, float te, float tx) {
@@ -2029,6 +2035,11 @@ __device__ __forceinline__ R lights_pdf_grid_coop_list(const DevScene<float>& g,
                             const uint32_t id = lg_id[idx()];
                             if (id >= rlo) {
                                 // the piece's kPieceIds smallest, sorted (rare: a candidate)
+#if RTW_PIECE_REG
+                                ++cnt;
+                                (void)sorted_insert(pid, id);
+                                return;
+#endif
                                 uint32_t m = min(cnt, kPieceIds);
                                 ++cnt;
                                 if (m == kPieceIds) {
@@ -2054,7 +2065,20 @@ __device__ __forceinline__ R lights_pdf_grid_coop_list(const DevScene<float>& g,
                         test(g.lg_sph[q], [q]() { return q; }, te, tx);
                     }, &lw.cells);
 #endif
+#if RTW_PIECE_REG
+                    {
+                        typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+                        static_assert(kPieceIds <= 7 && kSlot == 8, "the slot as two 16-byte stores");
+                        uint32_t w[7];
+#pragma unroll
+                        for (uint32_t q = 0; q < 7; ++q) w[q] = q < kPieceIds ? pid[q < kPieceIds ? q : 0] : 0xffffffffu;
+                        u4* sl = reinterpret_cast<u4*>(ent - 1);
+                        sl[0] = u4{cnt, w[0], w[1], w[2]};
+                        sl[1] = u4{w[3], w[4], w[5], w[6]};
+                    }
+#else
                     ent[-1] = cnt;
+#endif
                     has = cnt != 0;
                 }
                 const uint64_t h = __ballot(has);

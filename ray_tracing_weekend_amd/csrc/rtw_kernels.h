@@ -191,6 +191,17 @@ constexpr uint32_t kCoopStash64 = RTW_STASH64_EXTRA ? 34u : 20u;
 #ifndef RTW_COOP_HELD
 #define RTW_COOP_HELD 1
 #endif
+// the f64 list walk's pieces keep their candidates in registers (one
+// compare-exchange insert each) and write their slot once (C5 f64 1527 ->
+// 1460 ms, C3 1042 -> 1004, profiles/r06m_ab_piece_reg.jsonl); 0: insertion in LDS
+#ifndef RTW_PIECE_REG
+#define RTW_PIECE_REG 1
+#endif
+// the light grid's piece walks load each cell's record one cell ahead of its
+// tests (two loads in flight per lane); 0: load, then test
+#ifndef RTW_GRID_PF
+#define RTW_GRID_PF 0
+#endif
 #ifndef RTW_COOP64_MAX
 #define RTW_COOP64_MAX 8
 #endif
