@@ -265,8 +265,8 @@ int rtw_set_accel(rtw_ctx *ctx, int accel);
  * "lpt_pilot_spp" (samples per pixel counted, default 2), "lpt_pilot_depth" (the
  * separate pilot's max depth, 0 = the camera's),
  * "lpt_min_spp" (renders of fewer samples per pixel keep the index order, default 32),
- * "bvh_leaf" (spheres per BVH leaf, 1..15; 0 = auto, the default: 4, or 8 for
- * scenes of >= 100k spheres; takes effect at the
+ * "bvh_leaf" (spheres per BVH leaf, 1..15; 0 = auto, the default: 4, 8 for
+ * scenes of >= 100k spheres, 2 for f64 contexts on scenes of 4096..100k; takes effect at the
  * next rtw_set_scene), "light_bvh_min" (light lists this long or longer take the light grid
  * or light BVH in the BVH kernels, default 64), "light_grid" (light-grid resolution in
  * 1/16 cells per light, default 8; 0 = the light BVH instead; next rtw_set_scene),

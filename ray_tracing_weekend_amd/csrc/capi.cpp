@@ -53,7 +53,8 @@ struct rtw_ctx {
     int robust = 2;                   // f32 closest-approach tests: 1 on, 0 off, 2 by scene scale
     double scene_extent = 0.0, min_radius = 0.0;   // of the staged scene (robust = 2)
     uint32_t bvh_leaf = 0;            // spheres per BVH leaf (set before rtw_set_scene); 0 = auto:
-                                      // 4, or 8 for scenes of >= 100k spheres (C5: +12 %)
+                                      // 4, 8 for scenes of >= 100k spheres (C5: +12 %), 2 for
+                                      // f64 scenes of 4096..100k (rtw_set_scene)
     uint32_t persist = rtw::kPersistResident;   // workgroups of persistent waves (tasks from a
                                       // counter; default: as many as are resident at once);
                                       // 0: one task per wave
@@ -1821,7 +1822,14 @@ int rtw_set_scene(rtw_ctx* c, const rtw_scene* s) {
     // EVERY pointer member of DevScene must be listed in its `rebase`)
     rtw::DevScene<float> tmp32{};
     rtw::DevScene<double> tmp64{};
-    const uint32_t leaf = c->bvh_leaf ? c->bvh_leaf : (s->n_spheres >= 100000 ? 8u : 4u);
+    // auto leaf size: 4; 8 from 100k spheres (C5: +12 %); f64 with a tree too
+    // large for LDS (>= 4096 spheres): 2 -- its sphere tests are f64, its node
+    // tests f32 (C3 f64 1006 -> 998 ms: 2.8 -> 1.7 sphere tests and 7.2 -> 7.9
+    // node visits per segment; 3: 1003; C2's LDS tree and f32 lose with 2,
+    // profiles/r06t_ab_leaf_c3_f64.jsonl, r06u_ab_leaf.jsonl)
+    const uint32_t leaf = c->bvh_leaf ? c->bvh_leaf
+                                      : (s->n_spheres >= 100000 ? 8u
+                                         : (c->precision == RTW_F64 && s->n_spheres >= 4096 ? 2u : 4u));
     const uint32_t light_leaf = c->light_leaf ? c->light_leaf : rtw::kLeafMax;
     // the light grid only for light lists long enough to skip the linear loop
     const double grid = s->n_lights >= c->light_bvh_min ? c->light_grid / 16.0 : 0.0;
