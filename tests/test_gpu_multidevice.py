@@ -107,11 +107,15 @@ def test_n_device_context_is_bit_identical(prec):
     ref, samples, _ = _single(scene, cam, prec, seed=9)
     n = torch.cuda.device_count()
     with rtw.Renderer(precision=prec, devices=list(range(n))) as r:
+        r.set_tuning("lpt_min_spp", 2)
         r.set_scene(scene)
-        img = r.render(cam, 9)
+        img = r.render(cam, 9)                   # counting render (the round robin)
+        assert r.stats.samples == samples
+        dealt = r.render(cam, 9)                 # the tiles dealt by their costs (ABI 10)
         assert r.stats.samples == samples
     ok = ~np.isnan(ref)
-    assert np.array_equal(np.isnan(img), np.isnan(ref)) and np.array_equal(img[ok], ref[ok])
+    for a in (img, dealt):
+        assert np.array_equal(np.isnan(a), np.isnan(ref)) and np.array_equal(a[ok], ref[ok])
 
 
 # ---- the n-rank path on one GPU: rtw_create_virtual (ABI 9, test mode) ------
