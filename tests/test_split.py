@@ -31,7 +31,8 @@ def _costs(w, h, seed, heavy=0.1):
 
 
 @pytest.mark.parametrize("w,h,n", [(1200, 800, 8), (1200, 800, 2), (37, 23, 3), (120, 72, 8), (5, 5, 2),
-                                   (8, 8, 3), (64, 40, 1), (200, 120, 7)])
+                                   (8, 8, 3), (64, 40, 1), (200, 120, 7),
+                                   (1200, 800, 256), (2048, 8, 256)])
 def test_deal_matches_restatement_and_keeps_counts(w, h, n):
     c = _costs(w, h, w * 31 + h + n)
     a = rtw.split_deal(c, w, h, n)
