@@ -1404,7 +1404,7 @@ __device__ __forceinline__ V3<R> from64(V3<double> v) { return mk((R)v.x, (R)v.y
 __device__ __forceinline__ V3<double> unit64(V3<double> d) {
 #pragma clang fp contract(off)
     const double l = __builtin_sqrt(d.x * d.x + d.y * d.y + d.z * d.z);
-    return V3<double>{d.x / l, d.y / l, d.z / l};
+    return div3(d.x, d.y, d.z, l);
 }
 // Metal::scatter's direction (material.rs:407-421) in f64, no FMA, from the
 // unit direction u: reflect(u, n) + us * fuzz, with reflect(v, n) = v - (n * 2)
@@ -1510,7 +1510,7 @@ __device__ __forceinline__ V3<double> specular_dir64(bool metal, V3<double> d, V
 // the outward normal (p - c) / radius, sphere.rs:82-83 (f64, no FMA)
 __device__ __forceinline__ V3<double> sphere_normal64(V3<double> p, const R4<double>& S) {
 #pragma clang fp contract(off)
-    return V3<double>{(p.x - S.x) / S.w, (p.y - S.y) / S.w, (p.z - S.z) / S.w};
+    return div3(p.x - S.x, p.y - S.y, p.z - S.z, S.w);
 }
 __device__ __forceinline__ bool front64(V3<double> d, V3<double> n) {
 #pragma clang fp contract(off)

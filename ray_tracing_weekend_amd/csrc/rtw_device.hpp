@@ -48,6 +48,51 @@ __device__ __forceinline__ V3<R> cross(V3<R> a, V3<R> b) {
 template <typename R>
 struct P;
 
+// ---------------------------------------------------------------------------
+// Exact f64 quotients that share a divisor (Vec3 / scalar, Vec3::normalize)
+// ---------------------------------------------------------------------------
+// The compiler's IEEE a / b on gfx950 is
+//   B = div_scale(b, b, a); y = rcp(B); A, vcc = div_scale(a, b, a);
+//   y = fma(y, fma(-B, y, 1), y) twice; q = A y; r = fma(-B, q, A);
+//   fixup(div_fmas(r, y, q, vcc), b, a).
+// div_scale returns its operand unchanged with vcc = 0 unless a, b or a / b
+// is near the ends of the exponent range (or b = 0: then the fixup alone
+// decides); with both exponents in [-382, 384] it never rescales, so the
+// sequence is fixup(fma(r, y, q), b, a) with y a function of b alone -- the
+// SAME instructions on the same values, hence the same bits.  Three
+// quotients by one b then pay for one reciprocal instead of three (and no
+// div_scale), 17 f64 instructions instead of 33.  Zeros, infinities and NaNs
+// pass the range test (frexp_exp gives 0) and are decided by div_fixup from
+// a and b alone, as in the full sequence; any lane outside the range takes
+// the full division (a wave-uniform skip when none is).  RTW_FASTDIV 0: the
+// plain `/` everywhere.
+#ifndef RTW_FASTDIV
+#define RTW_FASTDIV 1
+#endif
+__device__ __forceinline__ double recip_nr(double b) {
+    double y = __builtin_amdgcn_rcp(b);
+    y = __builtin_fma(y, __builtin_fma(-b, y, 1.0), y);
+    return __builtin_fma(y, __builtin_fma(-b, y, 1.0), y);
+}
+__device__ __forceinline__ double div_by(double a, double b, double y) {
+    const double q = a * y;
+    const double r = __builtin_fma(-b, q, a);
+    return __builtin_amdgcn_div_fixup(__builtin_fma(r, y, q), b, a);
+}
+// frexp exponent + 382, as unsigned: <= 766 iff the exponent is in [-382, 384]
+__device__ __forceinline__ uint32_t div_rng(double x) { return (uint32_t)(__builtin_amdgcn_frexp_exp(x) + 382); }
+// {x, y, z} / b, each quotient the IEEE one bit for bit
+__device__ __forceinline__ V3<double> div3(double x, double y, double z, double b) {
+#if RTW_FASTDIV
+    const uint32_t m = max(max(div_rng(x), div_rng(y)), max(div_rng(z), div_rng(b)));
+    if (__builtin_expect(m <= 766u, 1)) {
+        const double yb = recip_nr(b);
+        return V3<double>{div_by(x, b, yb), div_by(y, b, yb), div_by(z, b, yb)};
+    }
+#endif
+    return V3<double>{x / b, y / b, z / b};
+}
+
 // The sin / cos kernel coefficients (P<double>::k_sin / k_cos) and rt_sin's reduction constants are fdlibm's:
 //   Copyright (C) 1993 by Sun Microsystems, Inc. All rights reserved.
 //   Developed at SunSoft, a Sun Microsystems, Inc. business.
@@ -61,16 +106,24 @@ struct P<double> {
     static constexpr double kEpsF64 = 2.220446049250313080847e-16;
     __device__ static __forceinline__ double sqrt_(double x) { return __builtin_sqrt(x); }
     __device__ static __forceinline__ double div_(double a, double b) { return a / b; }
-    __device__ static __forceinline__ double over_pi(double a) { return a / kPi; }
+    __device__ static __forceinline__ double over_pi(double a) {
+#if RTW_FASTDIV >= 2
+        // (experiment) the fast quotient with a constant reciprocal of pi: the compiler folds
+        // rcp(pi) to RN(1 / pi), so the result is the IEEE one by Markstein's theorem
+        // (y = RN(1 / b), q = RN(a y) within an ulp: RN(q + (a - b q) y) = RN(a / b))
+        if (__builtin_expect(div_rng(a) <= 766u, 1)) return div_by(a, kPi, recip_nr(kPi));
+#endif
+        return a / kPi;
+    }
     __device__ static __forceinline__ double min_(double a, double b) { return __builtin_fmin(a, b); }
     __device__ static __forceinline__ double max_(double a, double b) { return __builtin_fmax(a, b); }
     // vec.rs:86-94: self / self.length()
     __device__ static __forceinline__ V3<double> normalize(V3<double> a) {
         double l = sqrt_(dot(a, a));
-        return {a.x / l, a.y / l, a.z / l};
+        return div3(a.x, a.y, a.z, l);
     }
     __device__ static __forceinline__ V3<double> divs(V3<double> a, double s) {
-        return {a.x / s, a.y / s, a.z / s};
+        return div3(a.x, a.y, a.z, s);
     }
     // rand 0.8.6 Standard for f64: (v >> 11) * 2^-53
     __device__ static __forceinline__ double u_std(uint64_t v) {
