@@ -1232,7 +1232,15 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
         const uint32_t bin_stack = std::max(p.sc.bvh_depth, min_stack);
         // kWorldBvhLds layout: stacks + stealing area (+ light-work counters) (traversal_lds) | f32 nodes
         // (bvh32) | leaf spheres | ids (padded to 8) | lights | (f32) light pairs | (f64) the lights rounded to f32
-        const size_t tree_lds = rtw::traversal_lds<R>(bin_stack, p.light_bvh != 0) +
+        // wide workgroups (rtw_kernels.h block_waves): the f64 kernel of sphere + plane
+        // scenes with a linear light list -- 16 waves share one copy, which then also
+        // holds the f64 leaf spheres (32 B each, 32-B aligned)
+        const bool wide = sizeof(R) == 8 && p.light_bvh == 0 && !p.sc.mat_tex &&
+                          !(p.sc.n_quads || p.sc.n_boxes || p.sc.lref || p.sc.emissive) &&
+                          rtw::block_waves(true) == rtw::kWavesWide;
+        const uint32_t block_waves = rtw::block_waves(wide);
+        const size_t tree_lds = rtw::traversal_lds<R>(bin_stack, p.light_bvh != 0, block_waves) +
+                                (wide ? 32 + (size_t)p.sc.n_sph * sizeof(rtw::R4<double>) : 0) +
                                 (size_t)p.sc.n_nodes * sizeof(rtw::BvhNode<float>) +
                                 (size_t)p.sc.n_sph * sizeof(rtw::R4<float>) +
                                 (size_t)((p.sc.n_sph + 7u) & ~7u) * sizeof(uint32_t) +
@@ -1251,7 +1259,9 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
             // for a larger per-lane area (its LDS stash + piece slots)
             p.stack = bin_stack;
             bvh_width = 2;
-            const size_t lds_max = c->bvh_lds_max ? c->bvh_lds_max : (sizeof(R) == 4 ? 36 * 1024 : 52 * 1024);
+            // (4-wave workgroups: four copies per CU; wide: one copy per CU of 160 KiB)
+            const size_t lds_max = c->bvh_lds_max ? c->bvh_lds_max
+                                                  : (sizeof(R) == 4 ? 36 * 1024 : (wide ? 128 * 1024 : 52 * 1024));
             if (c->bvh_kind == 3 && tree_lds <= lds_max) {
                 world = rtw::kWorldBvhLds;
                 launch_lds = tree_lds;

@@ -751,7 +751,19 @@ __device__ __forceinline__ void test_leaf(const DevScene<R>& sc, int32_t base, i
         while (mask) {
             const uint32_t k = (uint32_t)__builtin_ctz(mask);
             mask &= mask - 1u;
+#if RTW_EXP_LEAF64_LOAD2
+            // (timing experiment) the candidate loaded twice, the second load's
+            // address depending on the first's value: the price of one dependent
+            // global load in the leaf loop (same values, same image)
+            {
+                const R4<double> s1 = sc.bsph[first + k];
+                uint32_t z;
+                asm volatile("v_and_b32 %0, 0, %1" : "=v"(z) : "v"((uint32_t)__double_as_longlong(s1.x)));
+                T.test(sc.bsph[first + k + z], base + (int32_t)sc.bid[first + k]);
+            }
+#else
             T.test(sc.bsph[first + k], base + (int32_t)sc.bid[first + k]);
+#endif
         }
         ntest += cnt;
         return;
@@ -2374,6 +2386,14 @@ __device__ V3<R> tex_colour(const DevScene<R>& sc, uint32_t tid, R u, R v, V3<R>
 //   kOptHit64    (f32 kernels of sphere + plane scenes) f64 ray origin, own-sphere re-hit test,
 //                hit t and hit point (sphere_t_ref64): the reference's self-intersection odds
 enum : int { kOptRobust = 1, kOptLightBvh = 2, kOptTex = 4, kOptPrims = 8, kOptHit64 = 16 };
+// the kernels with wide workgroups (rtw_kernels.h block_waves): f64, tree in
+// LDS, spheres + planes, linear light list
+template <typename R, int kWorld, int kOpt>
+constexpr bool kernel_wide() {
+    return sizeof(R) == 8 && kWorld == kWorldBvhLds && (kOpt & (kOptLightBvh | kOptPrims | kOptTex)) == 0;
+}
+template <typename R, int kWorld, int kOpt>
+constexpr uint32_t kernel_waves() { return block_waves(kernel_wide<R, kWorld, kOpt>()); }
 // subtree stealing in the f32 while-while kernels (bvh_traverse_steal); 0
 // builds them without it (timing comparisons, tools/variants.sh)
 // render_kernel: issue priorities in rotation (see the trip loop)
@@ -2444,7 +2464,7 @@ template <typename R, int kWorld, int kOpt>
 #ifndef RTW_WAVES_H64_LBVH
 #define RTW_WAVES_H64_LBVH 4
 #endif
-__global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ? ((kOpt & kOptLightBvh) ? RTW_WAVES_H64_LBVH
+__global__ void __launch_bounds__((64 * kernel_waves<R, kWorld, kOpt>()), sizeof(R) == 4 ? ((kOpt & kOptHit64) ? ((kOpt & kOptLightBvh) ? RTW_WAVES_H64_LBVH
                                                                                                       : RTW_WAVES_H64)
                                                                              : RTW_WAVES)
                                                          : ((kOpt & (kOptPrims | kOptTex)) ? 1
@@ -2452,6 +2472,8 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                                                                                      : RTW_WAVES_F64)))
     render_kernel(const KParams<R> p) {
     using PR = P<R>;
+    constexpr uint32_t kWB = kernel_waves<R, kWorld, kOpt>();   // waves per workgroup
+    constexpr uint32_t kBlk = 64 * kWB;
     constexpr bool kRobust = (kOpt & kOptRobust) != 0;
     constexpr bool kLightBvh = (kOpt & kOptLightBvh) != 0 && kWorld >= kWorldBvh;
     constexpr bool kTex = (kOpt & kOptTex) != 0;
@@ -2467,8 +2489,8 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
         // Stage the sphere list {c, r^2} and the light list into LDS once per
         // workgroup: every lane of every wave then reads sphere k at the same
         // LDS address (a broadcast read) during its closest-hit sweep.
-        for (uint32_t k = threadIdx.x; k < p.sc.n_sph; k += kBlock) s_sph[k] = p.sc.sph[k];
-        for (uint32_t k = threadIdx.x; k < p.sc.n_lights; k += kBlock) s_li[k] = p.sc.lights[k];
+        for (uint32_t k = threadIdx.x; k < p.sc.n_sph; k += kBlk) s_sph[k] = p.sc.sph[k];
+        for (uint32_t k = threadIdx.x; k < p.sc.n_lights; k += kBlk) s_li[k] = p.sc.lights[k];
         __syncthreads();
     }
     const R4<R>* __restrict__ sph = kWorld == kWorldLds ? s_sph : p.sc.sph;
@@ -2476,13 +2498,14 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
     R4<R>* l_li = nullptr;   // kWorldBvhLds: the light list in LDS
     R4<R>* l_lp = nullptr;   // kWorldBvhLds, f32: the light list as pairs in LDS
     R4<float>* l_li32 = nullptr;   // kWorldBvhLds, f64: the lights rounded to f32 (light pre-pass)
+    R4<R>* l_bsph64 = nullptr;     // kWorldBvhLds, f64, wide workgroups: the f64 leaf spheres
     // World view of the closest-hit query.  kWorldBvhLds: the BVH nodes and
     // the leaf-ordered spheres + ids are copied into LDS once per workgroup
     // (after the traversal stacks), so traversal fetches go to the LDS
     // instead of the vector-memory (TA/L1) path the shading loads use.
     DevScene<R> scw = p.sc;
     if constexpr (kWorld == kWorldBvhLds) {
-        unsigned char* base = smem + traversal_lds<R>(p.stack, kLightBvh);
+        unsigned char* base = smem + traversal_lds<R>(p.stack, kLightBvh, kWB);
         // the f32 tree (bvh32) in both precisions: the while-while traversal culls on it
         BvhNode<float>* l_nodes = reinterpret_cast<BvhNode<float>*>(base);
         // the leaf spheres {c, r^2} in f32 (f64: the pre-pass copy bsph32; the
@@ -2492,24 +2515,24 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
         static_assert(sizeof(BvhNode<float>) % 16 == 0, "nodes are copied in 16-B units");
         const uint4* g_nodes = reinterpret_cast<const uint4*>(cull_nodes(p.sc));
         constexpr uint32_t kNode16 = sizeof(BvhNode<float>) / 16;
-        for (uint32_t k = threadIdx.x; k < p.sc.n_nodes * kNode16; k += kBlock)
+        for (uint32_t k = threadIdx.x; k < p.sc.n_nodes * kNode16; k += kBlk)
             reinterpret_cast<uint4*>(l_nodes)[k] = g_nodes[k];
         const R4<float>* g_bsph32;
         if constexpr (sizeof(R) == 4) g_bsph32 = p.sc.bsph;
         else g_bsph32 = p.sc.bsph32;
-        for (uint32_t k = threadIdx.x; k < p.sc.n_sph; k += kBlock) {
+        for (uint32_t k = threadIdx.x; k < p.sc.n_sph; k += kBlk) {
             l_bsph[k] = g_bsph32[k];
             l_bid[k] = p.sc.bid[k];
         }
         // the light list follows, aligned to its element (read by the light pdf / sampling)
         l_li = reinterpret_cast<R4<R>*>((reinterpret_cast<uintptr_t>(l_bid + ((p.sc.n_sph + 7u) & ~7u)) +
                                          (sizeof(R4<R>) - 1)) & ~(uintptr_t)(sizeof(R4<R>) - 1));
-        for (uint32_t k = threadIdx.x; k < p.sc.n_lights; k += kBlock) l_li[k] = p.sc.lights[k];
+        for (uint32_t k = threadIdx.x; k < p.sc.n_lights; k += kBlk) l_li[k] = p.sc.lights[k];
         if constexpr (sizeof(R) == 4) {
             // and again as pairs for the packed light test (lights_pdf_sum_pk)
             l_lp = l_li + p.sc.n_lights;
             const uint32_t n = p.sc.n_lights;
-            for (uint32_t q = threadIdx.x; 2 * q < n; q += kBlock) {
+            for (uint32_t q = threadIdx.x; 2 * q < n; q += kBlk) {
                 const R4<R> A = p.sc.lights[2 * q];
                 const bool odd = 2 * q + 1 < n;
                 const R4<R> B = odd ? p.sc.lights[2 * q + 1] : R4<R>{0, 0, 0, 0};
@@ -2520,9 +2543,16 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
             // the lights rounded to f32 with |radius| (the f32 pre-pass of lights_pdf_sum;
             // a packed-FP32 pre-pass over light pairs measured 1.4 ms slower: r04)
             l_li32 = reinterpret_cast<R4<float>*>(l_li + p.sc.n_lights);
-            for (uint32_t k = threadIdx.x; k < p.sc.n_lights; k += kBlock) {
+            for (uint32_t k = threadIdx.x; k < p.sc.n_lights; k += kBlk) {
                 const R4<R> L = p.sc.lights[k];
                 l_li32[k] = R4<float>{(float)L.x, (float)L.y, (float)L.z, fabsf((float)L.w)};
+            }
+            if constexpr (kernel_wide<R, kWorld, kOpt>()) {
+                // wide workgroups: the f64 leaf spheres too, 32-B aligned (the leaf
+                // loop's candidates, test_leaf: an LDS read instead of L1 / L2)
+                l_bsph64 = reinterpret_cast<R4<R>*>(
+                    (reinterpret_cast<uintptr_t>(l_li32 + p.sc.n_lights) + 31u) & ~(uintptr_t)31u);
+                for (uint32_t k = threadIdx.x; k < p.sc.n_sph; k += kBlk) l_bsph64[k] = p.sc.bsph[k];
             }
         }
         __syncthreads();
@@ -2532,6 +2562,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
         } else {
             scw.bvh32 = l_nodes;
             scw.bsph32 = l_bsph;
+            if constexpr (kernel_wide<R, kWorld, kOpt>()) scw.bsph = l_bsph64;
         }
         scw.bid = l_bid;
     }
@@ -2546,11 +2577,11 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
     // state loses more than the lanes gain (C3 852 -> 875 ms, C5 1536 -> 1751)
     constexpr bool kSteal = RTW_STEAL && kWorld == kWorldBvhLds;
     unsigned char* const steal_area =
-        smem + (size_t)kWavesPerBlock * p.stack * 64 * sizeof(int32_t) + wave * kStealLdsPerWave<R>;
+        smem + (size_t)kWB * p.stack * 64 * sizeof(int32_t) + wave * kStealLdsPerWave<R>;
     // the light BVH / grid kernels: the wave's light-work counters (u64 light
     // tests, grid cells), right after the traversal area
     unsigned long long* const wcnt =
-        reinterpret_cast<unsigned long long*>(smem + traversal_lds<R>(p.stack) + wave * kLightWorkBytes);
+        reinterpret_cast<unsigned long long*>(smem + traversal_lds<R>(p.stack, false, kWB) + wave * kLightWorkBytes);
     if constexpr (kLightBvh) {
         if (lane < 2) wcnt[lane] = 0ull;
     }
@@ -2607,7 +2638,7 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
     // staging) per resident workgroup.  Else one task per wave (static map).
     bool more = p.persist != 0;       // wave-uniform: the counter may hold tasks
     if (!p.persist) {
-        const uint32_t task = blockIdx.x * kWavesPerBlock + wave;
+        const uint32_t task = blockIdx.x * kWB + wave;
         if (task >= p.n_tasks) return;
         set_task(task);
     }
@@ -2999,7 +3030,15 @@ __global__ void __launch_bounds__(kBlock, sizeof(R) == 4 ? ((kOpt & kOptHit64) ?
                     const uint32_t mw = kargs()->sc.sph_mat[k];
                     m = mw & 0xffffffu;
                     mtype = (mw >> 24) & 0x7fu;
+#if RTW_EXP_HITREC_LOAD2
+                    {   // (timing experiment) the shading record's load made dependent on sph_mat's
+                        uint32_t z;
+                        asm volatile("v_and_b32 %0, 0, %1" : "=v"(z) : "v"(mw));
+                        mp = kargs()->sc.sph_shade[k + z];
+                    }
+#else
                     mp = kargs()->sc.sph_shade[k];
+#endif
                     next_self = (mw >> 31) ? (int32_t)k : -1;   // bit 31: isolated sphere
                     if constexpr (kHit64) {
                         next_self = (int32_t)k;
@@ -3565,7 +3604,8 @@ template <typename R, int kWorld, int kOpt>
 inline uint32_t resident_blocks(uint32_t blocks, size_t lds_bytes) {
     int per_cu = 0, dev = 0, cus = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &per_cu, reinterpret_cast<const void*>(&dev::render_kernel<R, kWorld, kOpt>), kBlock, lds_bytes) !=
+            &per_cu, reinterpret_cast<const void*>(&dev::render_kernel<R, kWorld, kOpt>),
+            64 * dev::kernel_waves<R, kWorld, kOpt>(), lds_bytes) !=
             hipSuccess ||
         hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || per_cu < 1 ||
@@ -3579,8 +3619,15 @@ constexpr int kVariantRan = 1 << 16;
 // that ran as kVariantRan | (world << 8) | options (the brute-force worlds drop
 // the light BVH, textured scenes map to the while-while BVH).
 template <typename R, int kOpt>
-inline int launch_world(const KParams<R>& p, int world, size_t lds_bytes, uint32_t blocks,
-                        hipStream_t stream) {
+inline int launch_world(const KParams<R>& p, int world, size_t lds_bytes, hipStream_t stream) {
+    // the grid: one task per wave (p.persist 0), a fixed grid (p.persist), or the
+    // resident workgroups (kPersistResident), in workgroups of the kernel's size
+    auto grid = [&](uint32_t waves) {
+        uint32_t b = (p.n_tasks + waves - 1) / waves;
+        if (p.persist && p.persist != kPersistResident) b = b < p.persist ? b : p.persist;
+        return b;
+    };
+    uint32_t blocks = 0;
     const size_t stacks = traversal_lds<R>(p.stack, (kOpt & dev::kOptLightBvh) != 0);
     const bool resident = p.persist == kPersistResident;
     constexpr int kBrute = kOpt & ~dev::kOptLightBvh;   // the light BVH needs the BVH kernels' stack
@@ -3592,38 +3639,48 @@ inline int launch_world(const KParams<R>& p, int world, size_t lds_bytes, uint32
     switch (world) {
     case kWorldLds:
         allow_lds<R, kWorldLds, kBrute>(lds_bytes);
+        blocks = grid(dev::kernel_waves<R, kWorldLds, kBrute>());
         if (resident) blocks = resident_blocks<R, kWorldLds, kBrute>(blocks, lds_bytes);
-        hipLaunchKernelGGL((dev::render_kernel<R, kWorldLds, kBrute>), dim3(blocks), dim3(kBlock), lds_bytes,
+        hipLaunchKernelGGL((dev::render_kernel<R, kWorldLds, kBrute>), dim3(blocks),
+                           dim3(64 * dev::kernel_waves<R, kWorldLds, kBrute>()), lds_bytes,
                            stream, p);
         return kVariantRan | (kWorldLds << 8) | kBrute;
     case kWorldBvhLds:
         allow_lds<R, kWorldBvhLds, kOpt>(lds_bytes);
+        blocks = grid(dev::kernel_waves<R, kWorldBvhLds, kOpt>());
         if (resident) blocks = resident_blocks<R, kWorldBvhLds, kOpt>(blocks, lds_bytes);
-        hipLaunchKernelGGL((dev::render_kernel<R, kWorldBvhLds, kOpt>), dim3(blocks), dim3(kBlock), lds_bytes,
+        hipLaunchKernelGGL((dev::render_kernel<R, kWorldBvhLds, kOpt>), dim3(blocks),
+                           dim3(64 * dev::kernel_waves<R, kWorldBvhLds, kOpt>()), lds_bytes,
                            stream, p);
         return kVariantRan | (kWorldBvhLds << 8) | kOpt;
     case kWorldBvh4:
         if constexpr ((kOpt & dev::kOptTex) == 0) {
+            blocks = grid(dev::kernel_waves<R, kWorldBvh4, kOpt>());
             if (resident) blocks = resident_blocks<R, kWorldBvh4, kOpt>(blocks, stacks);
-            hipLaunchKernelGGL((dev::render_kernel<R, kWorldBvh4, kOpt>), dim3(blocks), dim3(kBlock), stacks,
-                               stream, p);
+            hipLaunchKernelGGL((dev::render_kernel<R, kWorldBvh4, kOpt>), dim3(blocks),
+                               dim3(64 * dev::kernel_waves<R, kWorldBvh4, kOpt>()), stacks, stream, p);
         }
         return kVariantRan | (kWorldBvh4 << 8) | kOpt;
     case kWorldBvhWW:
+        blocks = grid(dev::kernel_waves<R, kWorldBvhWW, kOpt>());
         if (resident) blocks = resident_blocks<R, kWorldBvhWW, kOpt>(blocks, stacks);
-        hipLaunchKernelGGL((dev::render_kernel<R, kWorldBvhWW, kOpt>), dim3(blocks), dim3(kBlock), stacks,
+        hipLaunchKernelGGL((dev::render_kernel<R, kWorldBvhWW, kOpt>), dim3(blocks),
+                           dim3(64 * dev::kernel_waves<R, kWorldBvhWW, kOpt>()), stacks,
                            stream, p);
         return kVariantRan | (kWorldBvhWW << 8) | kOpt;
     case kWorldBvh:
         if constexpr ((kOpt & dev::kOptTex) == 0) {
+            blocks = grid(dev::kernel_waves<R, kWorldBvh, kOpt>());
             if (resident) blocks = resident_blocks<R, kWorldBvh, kOpt>(blocks, stacks);
-            hipLaunchKernelGGL((dev::render_kernel<R, kWorldBvh, kOpt>), dim3(blocks), dim3(kBlock), stacks,
-                               stream, p);
+            hipLaunchKernelGGL((dev::render_kernel<R, kWorldBvh, kOpt>), dim3(blocks),
+                               dim3(64 * dev::kernel_waves<R, kWorldBvh, kOpt>()), stacks, stream, p);
         }
         return kVariantRan | (kWorldBvh << 8) | kOpt;
     default:
+        blocks = grid(dev::kernel_waves<R, kWorldGlobal, kBrute>());
         if (resident) blocks = resident_blocks<R, kWorldGlobal, kBrute>(blocks, 0);
-        hipLaunchKernelGGL((dev::render_kernel<R, kWorldGlobal, kBrute>), dim3(blocks), dim3(kBlock), 0, stream,
+        hipLaunchKernelGGL((dev::render_kernel<R, kWorldGlobal, kBrute>), dim3(blocks),
+                           dim3(64 * dev::kernel_waves<R, kWorldGlobal, kBrute>()), 0, stream,
                            p);
         return kVariantRan | (kWorldGlobal << 8) | kBrute;
     }
@@ -3635,11 +3692,8 @@ inline int launch_world(const KParams<R>& p, int world, size_t lds_bytes, uint32
 template <typename R>
 inline int launch_render_impl(const KParams<R>& p, int world, size_t lds_bytes, R* out,
                               hipStream_t stream, hipEvent_t mid) {
-    uint32_t blocks = (p.n_tasks + kWavesPerBlock - 1) / kWavesPerBlock;
     int ran = 0;
-    if (p.persist && p.persist != kPersistResident)
-        blocks = blocks < p.persist ? blocks : p.persist;   // fixed grid, tasks from the counter
-    if (blocks) {
+    if (p.n_tasks) {
         const bool robust = sizeof(R) == 4 && p.sc.robust;
         const bool lbvh = p.light_bvh != 0;
         // kOptPrims: always for textured kernels; the Book-1 kernels go
@@ -3649,32 +3703,32 @@ inline int launch_render_impl(const KParams<R>& p, int world, size_t lds_bytes, 
         constexpr int T = dev::kOptTex | dev::kOptPrims, Pr = dev::kOptPrims;
         if (p.sc.mat_tex) {
             if constexpr (sizeof(R) == 4) {
-                if (robust && lbvh) ran = launch_world<R, T | dev::kOptRobust | dev::kOptLightBvh>(p, world, lds_bytes, blocks, stream);
-                else if (robust) ran = launch_world<R, T | dev::kOptRobust>(p, world, lds_bytes, blocks, stream);
-                else if (lbvh) ran = launch_world<R, T | dev::kOptLightBvh>(p, world, lds_bytes, blocks, stream);
-                else ran = launch_world<R, T>(p, world, lds_bytes, blocks, stream);
+                if (robust && lbvh) ran = launch_world<R, T | dev::kOptRobust | dev::kOptLightBvh>(p, world, lds_bytes, stream);
+                else if (robust) ran = launch_world<R, T | dev::kOptRobust>(p, world, lds_bytes, stream);
+                else if (lbvh) ran = launch_world<R, T | dev::kOptLightBvh>(p, world, lds_bytes, stream);
+                else ran = launch_world<R, T>(p, world, lds_bytes, stream);
             } else {
-                if (lbvh) ran = launch_world<R, T | dev::kOptLightBvh>(p, world, lds_bytes, blocks, stream);
-                else ran = launch_world<R, T>(p, world, lds_bytes, blocks, stream);
+                if (lbvh) ran = launch_world<R, T | dev::kOptLightBvh>(p, world, lds_bytes, stream);
+                else ran = launch_world<R, T>(p, world, lds_bytes, stream);
             }
         } else if constexpr (sizeof(R) == 4) {
             if (prims) {
-                if (robust && lbvh) ran = launch_world<R, Pr | dev::kOptRobust | dev::kOptLightBvh>(p, world, lds_bytes, blocks, stream);
-                else if (robust) ran = launch_world<R, Pr | dev::kOptRobust>(p, world, lds_bytes, blocks, stream);
-                else if (lbvh) ran = launch_world<R, Pr | dev::kOptLightBvh>(p, world, lds_bytes, blocks, stream);
-                else ran = launch_world<R, Pr>(p, world, lds_bytes, blocks, stream);
+                if (robust && lbvh) ran = launch_world<R, Pr | dev::kOptRobust | dev::kOptLightBvh>(p, world, lds_bytes, stream);
+                else if (robust) ran = launch_world<R, Pr | dev::kOptRobust>(p, world, lds_bytes, stream);
+                else if (lbvh) ran = launch_world<R, Pr | dev::kOptLightBvh>(p, world, lds_bytes, stream);
+                else ran = launch_world<R, Pr>(p, world, lds_bytes, stream);
             } else {
                 constexpr int H = dev::kOptHit64;
                 if (p.hit64) {
-                    if (robust && lbvh) ran = launch_world<R, H | dev::kOptRobust | dev::kOptLightBvh>(p, world, lds_bytes, blocks, stream);
-                    else if (robust) ran = launch_world<R, H | dev::kOptRobust>(p, world, lds_bytes, blocks, stream);
-                    else if (lbvh) ran = launch_world<R, H | dev::kOptLightBvh>(p, world, lds_bytes, blocks, stream);
-                    else ran = launch_world<R, H>(p, world, lds_bytes, blocks, stream);
+                    if (robust && lbvh) ran = launch_world<R, H | dev::kOptRobust | dev::kOptLightBvh>(p, world, lds_bytes, stream);
+                    else if (robust) ran = launch_world<R, H | dev::kOptRobust>(p, world, lds_bytes, stream);
+                    else if (lbvh) ran = launch_world<R, H | dev::kOptLightBvh>(p, world, lds_bytes, stream);
+                    else ran = launch_world<R, H>(p, world, lds_bytes, stream);
                 } else {
-                    if (robust && lbvh) ran = launch_world<R, dev::kOptRobust | dev::kOptLightBvh>(p, world, lds_bytes, blocks, stream);
-                    else if (robust) ran = launch_world<R, dev::kOptRobust>(p, world, lds_bytes, blocks, stream);
-                    else if (lbvh) ran = launch_world<R, dev::kOptLightBvh>(p, world, lds_bytes, blocks, stream);
-                    else ran = launch_world<R, 0>(p, world, lds_bytes, blocks, stream);
+                    if (robust && lbvh) ran = launch_world<R, dev::kOptRobust | dev::kOptLightBvh>(p, world, lds_bytes, stream);
+                    else if (robust) ran = launch_world<R, dev::kOptRobust>(p, world, lds_bytes, stream);
+                    else if (lbvh) ran = launch_world<R, dev::kOptLightBvh>(p, world, lds_bytes, stream);
+                    else ran = launch_world<R, 0>(p, world, lds_bytes, stream);
                 }
             }
         } else {
@@ -3682,11 +3736,11 @@ inline int launch_render_impl(const KParams<R>& p, int world, size_t lds_bytes, 
             // too (156 instead of 176 VGPRs: 3 waves per SIMD instead of 2)
             (void)robust;
             if (prims) {
-                if (lbvh) ran = launch_world<R, Pr | dev::kOptLightBvh>(p, world, lds_bytes, blocks, stream);
-                else ran = launch_world<R, Pr>(p, world, lds_bytes, blocks, stream);
+                if (lbvh) ran = launch_world<R, Pr | dev::kOptLightBvh>(p, world, lds_bytes, stream);
+                else ran = launch_world<R, Pr>(p, world, lds_bytes, stream);
             } else {
-                if (lbvh) ran = launch_world<R, dev::kOptLightBvh>(p, world, lds_bytes, blocks, stream);
-                else ran = launch_world<R, 0>(p, world, lds_bytes, blocks, stream);
+                if (lbvh) ran = launch_world<R, dev::kOptLightBvh>(p, world, lds_bytes, stream);
+                else ran = launch_world<R, 0>(p, world, lds_bytes, stream);
             }
         }
         if (hipGetLastError() != hipSuccess) return -1;

@@ -12,6 +12,20 @@ namespace rtw {
 constexpr uint32_t kTile = 8;          // 8 x 8 pixel tile = one wavefront of 64 lanes
 constexpr uint32_t kWavesPerBlock = 4; // 256-thread workgroups, one tile item per wave
 constexpr uint32_t kBlock = 64 * kWavesPerBlock;
+// Wide workgroups (round 6): the f64 sphere + plane kernel with the tree in
+// LDS runs 16 waves per workgroup -- the 4 waves per SIMD of one CU, so ONE
+// LDS copy of the scene per CU instead of four -- and spends the freed LDS on
+// the f64 leaf spheres, which the 4-wave layout had to read from L1 / L2 in
+// the leaf loop (a dependent global load per candidate).  0: 4 waves.
+#ifndef RTW_WIDE_F64
+#define RTW_WIDE_F64 1
+#endif
+constexpr uint32_t kWavesWide = 16;
+// waves per workgroup of a render kernel: `wide` = f64, tree in LDS, no
+// light BVH / grid, no quads / cuboids / textures (the Book-1 family)
+__host__ __device__ constexpr uint32_t block_waves(bool wide) {
+    return (RTW_WIDE_F64 != 0 && wide) ? kWavesWide : kWavesPerBlock;
+}
 
 // world query of the render kernel
 enum WorldMode : int {
@@ -228,8 +242,9 @@ constexpr uint32_t kLightWorkBytes = 16;
 // LDS of the traversal stacks + the stealing area of one workgroup (+ the
 // light-work counters when `light_work`)
 template <typename R>
-__host__ __device__ inline size_t traversal_lds(uint32_t stack, bool light_work = false) {
-    return (size_t)kWavesPerBlock * ((size_t)stack * 64 * sizeof(int32_t) + kStealLdsPerWave<R> +
+__host__ __device__ inline size_t traversal_lds(uint32_t stack, bool light_work = false,
+                                               uint32_t waves = kWavesPerBlock) {
+    return (size_t)waves * ((size_t)stack * 64 * sizeof(int32_t) + kStealLdsPerWave<R> +
                                      (light_work ? kLightWorkBytes : 0));
 }
 constexpr uint32_t kPersistResident = 0xFFFFFFFFu;   // KParams::persist: one resident grid

@@ -98,7 +98,7 @@ static __device__ unsigned long long g_tl[kTlWaves * kTlWords];
 #define RTW_PROBE_WAVE_TRIP() (tl_dry_trips_ += tl_dry_t_ ? 1u : 0u)
 #define RTW_PROBE_WAVE_END() \
     do { \
-        const uint32_t w_ = blockIdx.x * kWavesPerBlock + wave; \
+        const uint32_t w_ = blockIdx.x * kWB + wave; \
         if (lane == 0 && w_ < kTlWaves) { \
             unsigned xcc_, hw_; \
             asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc_)); \
@@ -313,7 +313,7 @@ extern "C" int RTW_CAT(rtw_probe_lanes_read_, RTW_PROF)(unsigned long long* out,
 constexpr int kClkParts = 20;
 static __device__ unsigned long long g_clk[kClkParts];
 #define RTW_PROBE_CLK_INIT() \
-    __shared__ unsigned long long clk_lds_[kWavesPerBlock][kClkParts]; \
+    __shared__ unsigned long long clk_lds_[kWB][kClkParts]; \
     if (lane < (uint32_t)kClkParts) clk_lds_[wave][lane] = 0; \
     uint64_t clk_t_ = __builtin_amdgcn_s_memtime()
 #define RTW_PROBE_CLK(id) \

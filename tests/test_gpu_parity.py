@@ -43,7 +43,6 @@ def _render_gpu(soa, cam, seed, precision, chunk=0, accel=rtw.RTW_ACCEL_AUTO, bv
             r.set_tuning(k, v)
         if bvh_kind is not None:
             r.set_tuning("bvh_kind", bvh_kind)
-            r.set_tuning("bvh_lds_max", 64 * 1024)    # the f64 tree needs > 32 KiB
         r.set_accel(accel)
         r.set_scene(soa)
         img = r.render(cam, seed)
