@@ -2482,7 +2482,7 @@ __global__ void __launch_bounds__((64 * kernel_waves<R, kWorld, kOpt>()), sizeof
     // DiffuseLight materials only in the kOptPrims / kOptTex kernels (the host
     // routes scenes with one there): the others know emitted() is black
     constexpr bool kEmit = kPrims || kTex;
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    extern __shared__ __attribute__((aligned(32))) unsigned char smem[];
     R4<R>* s_sph = reinterpret_cast<R4<R>*>(smem);
     R4<R>* s_li = s_sph + p.sc.n_sph;
     if constexpr (kWorld == kWorldLds) {
@@ -2525,8 +2525,14 @@ __global__ void __launch_bounds__((64 * kernel_waves<R, kWorld, kOpt>()), sizeof
             l_bid[k] = p.sc.bid[k];
         }
         // the light list follows, aligned to its element (read by the light pdf / sampling)
-        l_li = reinterpret_cast<R4<R>*>((reinterpret_cast<uintptr_t>(l_bid + ((p.sc.n_sph + 7u) & ~7u)) +
-                                         (sizeof(R4<R>) - 1)) & ~(uintptr_t)(sizeof(R4<R>) - 1));
+        // (offsets from smem, not integer casts of pointers: a pointer rebuilt from an
+        // integer loses its LDS address space, and every access through it became a
+        // flat instruction -- which waits on the vector-memory counter as well)
+        auto lds_after = [&](const void* end, size_t align) {
+            const size_t off = (size_t)(reinterpret_cast<const unsigned char*>(end) - smem);
+            return smem + ((off + align - 1) & ~(align - 1));
+        };
+        l_li = reinterpret_cast<R4<R>*>(lds_after(l_bid + ((p.sc.n_sph + 7u) & ~7u), sizeof(R4<R>)));
         for (uint32_t k = threadIdx.x; k < p.sc.n_lights; k += kBlk) l_li[k] = p.sc.lights[k];
         if constexpr (sizeof(R) == 4) {
             // and again as pairs for the packed light test (lights_pdf_sum_pk)
@@ -2550,8 +2556,7 @@ __global__ void __launch_bounds__((64 * kernel_waves<R, kWorld, kOpt>()), sizeof
             if constexpr (kernel_wide<R, kWorld, kOpt>()) {
                 // wide workgroups: the f64 leaf spheres too, 32-B aligned (the leaf
                 // loop's candidates, test_leaf: an LDS read instead of L1 / L2)
-                l_bsph64 = reinterpret_cast<R4<R>*>(
-                    (reinterpret_cast<uintptr_t>(l_li32 + p.sc.n_lights) + 31u) & ~(uintptr_t)31u);
+                l_bsph64 = reinterpret_cast<R4<R>*>(lds_after(l_li32 + p.sc.n_lights, 32));
                 for (uint32_t k = threadIdx.x; k < p.sc.n_sph; k += kBlk) l_bsph64[k] = p.sc.bsph[k];
             }
         }
