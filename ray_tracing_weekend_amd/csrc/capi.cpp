@@ -1240,7 +1240,7 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
                           rtw::block_waves(true) == rtw::kWavesWide;
         const uint32_t block_waves = rtw::block_waves(wide);
         const size_t tree_lds = rtw::traversal_lds<R>(bin_stack, p.light_bvh != 0, block_waves) +
-                                (wide ? 32 + (size_t)p.sc.n_sph * sizeof(rtw::R4<double>) : 0) +
+                                (wide ? 32 + (RTW_WIDE_SPH64 ? 2 : 1) * (size_t)p.sc.n_sph * sizeof(rtw::R4<double>) : 0) +
                                 (size_t)p.sc.n_nodes * sizeof(rtw::BvhNode<float>) +
                                 (size_t)p.sc.n_sph * sizeof(rtw::R4<float>) +
                                 (size_t)((p.sc.n_sph + 7u) & ~7u) * sizeof(uint32_t) +

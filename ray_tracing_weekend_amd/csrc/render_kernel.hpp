@@ -2499,6 +2499,7 @@ __global__ void __launch_bounds__((64 * kernel_waves<R, kWorld, kOpt>()), sizeof
     R4<R>* l_lp = nullptr;   // kWorldBvhLds, f32: the light list as pairs in LDS
     R4<float>* l_li32 = nullptr;   // kWorldBvhLds, f64: the lights rounded to f32 (light pre-pass)
     R4<R>* l_bsph64 = nullptr;     // kWorldBvhLds, f64, wide workgroups: the f64 leaf spheres
+    R4<R>* l_sph64 = nullptr;      // ... and the f64 spheres in id order (RTW_WIDE_SPH64)
     // World view of the closest-hit query.  kWorldBvhLds: the BVH nodes and
     // the leaf-ordered spheres + ids are copied into LDS once per workgroup
     // (after the traversal stacks), so traversal fetches go to the LDS
@@ -2558,6 +2559,11 @@ __global__ void __launch_bounds__((64 * kernel_waves<R, kWorld, kOpt>()), sizeof
                 // loop's candidates, test_leaf: an LDS read instead of L1 / L2)
                 l_bsph64 = reinterpret_cast<R4<R>*>(lds_after(l_li32 + p.sc.n_lights, 32));
                 for (uint32_t k = threadIdx.x; k < p.sc.n_sph; k += kBlk) l_bsph64[k] = p.sc.bsph[k];
+#if RTW_WIDE_SPH64
+                // and in id order (the own-sphere test at the traversal's start)
+                l_sph64 = l_bsph64 + p.sc.n_sph;
+                for (uint32_t k = threadIdx.x; k < p.sc.n_sph; k += kBlk) l_sph64[k] = p.sc.sph[k];
+#endif
             }
         }
         __syncthreads();
@@ -2567,7 +2573,10 @@ __global__ void __launch_bounds__((64 * kernel_waves<R, kWorld, kOpt>()), sizeof
         } else {
             scw.bvh32 = l_nodes;
             scw.bsph32 = l_bsph;
-            if constexpr (kernel_wide<R, kWorld, kOpt>()) scw.bsph = l_bsph64;
+            if constexpr (kernel_wide<R, kWorld, kOpt>()) {
+                scw.bsph = l_bsph64;
+                if (RTW_WIDE_SPH64) scw.sph = l_sph64;
+            }
         }
         scw.bid = l_bid;
     }

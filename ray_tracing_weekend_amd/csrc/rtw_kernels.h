@@ -20,6 +20,11 @@ constexpr uint32_t kBlock = 64 * kWavesPerBlock;
 #ifndef RTW_WIDE_F64
 #define RTW_WIDE_F64 1
 #endif
+// RTW_WIDE_SPH64: the wide kernel's LDS also holds the f64 spheres in id order
+// (the own-sphere test that starts each traversal)
+#ifndef RTW_WIDE_SPH64
+#define RTW_WIDE_SPH64 1
+#endif
 constexpr uint32_t kWavesWide = 16;
 // waves per workgroup of a render kernel: `wide` = f64, tree in LDS, no
 // light BVH / grid, no quads / cuboids / textures (the Book-1 family)
