@@ -3650,14 +3650,22 @@ inline int launch_world(const KParams<R>& p, int world, size_t lds_bytes, hipStr
     if constexpr ((kOpt & dev::kOptTex) != 0) {
         if (world == kWorldBvh4 || world == kWorldBvh) world = kWorldBvhWW;
     }
+    // (the light BVH / grid is only chosen with a BVH world: its brute-force
+    // cases are never reached, and instantiating them would put copies of the
+    // plain brute-force kernels into the f64 light-grid unit)
+    if constexpr ((kOpt & dev::kOptLightBvh) != 0) {
+        if (world == kWorldLds || world == kWorldGlobal) return -1;
+    }
     switch (world) {
     case kWorldLds:
-        allow_lds<R, kWorldLds, kBrute>(lds_bytes);
-        blocks = grid(dev::kernel_waves<R, kWorldLds, kBrute>());
-        if (resident) blocks = resident_blocks<R, kWorldLds, kBrute>(blocks, lds_bytes);
-        hipLaunchKernelGGL((dev::render_kernel<R, kWorldLds, kBrute>), dim3(blocks),
-                           dim3(64 * dev::kernel_waves<R, kWorldLds, kBrute>()), lds_bytes,
-                           stream, p);
+        if constexpr ((kOpt & dev::kOptLightBvh) == 0) {
+            allow_lds<R, kWorldLds, kBrute>(lds_bytes);
+            blocks = grid(dev::kernel_waves<R, kWorldLds, kBrute>());
+            if (resident) blocks = resident_blocks<R, kWorldLds, kBrute>(blocks, lds_bytes);
+            hipLaunchKernelGGL((dev::render_kernel<R, kWorldLds, kBrute>), dim3(blocks),
+                               dim3(64 * dev::kernel_waves<R, kWorldLds, kBrute>()), lds_bytes,
+                               stream, p);
+        }
         return kVariantRan | (kWorldLds << 8) | kBrute;
     case kWorldBvhLds:
         allow_lds<R, kWorldBvhLds, kOpt>(lds_bytes);
@@ -3691,12 +3699,30 @@ inline int launch_world(const KParams<R>& p, int world, size_t lds_bytes, hipStr
         }
         return kVariantRan | (kWorldBvh << 8) | kOpt;
     default:
-        blocks = grid(dev::kernel_waves<R, kWorldGlobal, kBrute>());
-        if (resident) blocks = resident_blocks<R, kWorldGlobal, kBrute>(blocks, 0);
-        hipLaunchKernelGGL((dev::render_kernel<R, kWorldGlobal, kBrute>), dim3(blocks),
-                           dim3(64 * dev::kernel_waves<R, kWorldGlobal, kBrute>()), 0, stream,
-                           p);
+        if constexpr ((kOpt & dev::kOptLightBvh) == 0) {
+            blocks = grid(dev::kernel_waves<R, kWorldGlobal, kBrute>());
+            if (resident) blocks = resident_blocks<R, kWorldGlobal, kBrute>(blocks, 0);
+            hipLaunchKernelGGL((dev::render_kernel<R, kWorldGlobal, kBrute>), dim3(blocks),
+                               dim3(64 * dev::kernel_waves<R, kWorldGlobal, kBrute>()), 0, stream,
+                               p);
+        }
         return kVariantRan | (kWorldGlobal << 8) | kBrute;
+    }
+}
+
+// The f64 kernels with the light BVH / grid are compiled in their own unit
+// (render_f64_lgrid.hip) without the shared-divisor quotients (RTW_FASTDIV
+// 0: C3 f64 +1.1 % with them, profiles/r06c3fd_ab.log); kOpt includes kOptLightBvh
+int launch_render_f64_lgrid(const KParams<double>& p, int world, size_t lds_bytes, hipStream_t stream, int kopt);
+// the f64 light-grid unit's body (instantiated there only)
+template <typename R>
+inline int launch_lgrid_impl(const KParams<R>& p, int world, size_t lds_bytes, hipStream_t stream, int kopt) {
+    constexpr int T = dev::kOptTex | dev::kOptPrims, Pr = dev::kOptPrims, L = dev::kOptLightBvh;
+    switch (kopt) {
+    case T | L: return launch_world<R, T | L>(p, world, lds_bytes, stream);
+    case Pr | L: return launch_world<R, Pr | L>(p, world, lds_bytes, stream);
+    case L: return launch_world<R, L>(p, world, lds_bytes, stream);
+    default: return -1;
     }
 }
 
@@ -3722,7 +3748,7 @@ inline int launch_render_impl(const KParams<R>& p, int world, size_t lds_bytes, 
                 else if (lbvh) ran = launch_world<R, T | dev::kOptLightBvh>(p, world, lds_bytes, stream);
                 else ran = launch_world<R, T>(p, world, lds_bytes, stream);
             } else {
-                if (lbvh) ran = launch_world<R, T | dev::kOptLightBvh>(p, world, lds_bytes, stream);
+                if (lbvh) ran = launch_render_f64_lgrid(p, world, lds_bytes, stream, T | dev::kOptLightBvh);
                 else ran = launch_world<R, T>(p, world, lds_bytes, stream);
             }
         } else if constexpr (sizeof(R) == 4) {
@@ -3750,10 +3776,10 @@ inline int launch_render_impl(const KParams<R>& p, int world, size_t lds_bytes, 
             // too (156 instead of 176 VGPRs: 3 waves per SIMD instead of 2)
             (void)robust;
             if (prims) {
-                if (lbvh) ran = launch_world<R, Pr | dev::kOptLightBvh>(p, world, lds_bytes, stream);
+                if (lbvh) ran = launch_render_f64_lgrid(p, world, lds_bytes, stream, Pr | dev::kOptLightBvh);
                 else ran = launch_world<R, Pr>(p, world, lds_bytes, stream);
             } else {
-                if (lbvh) ran = launch_world<R, dev::kOptLightBvh>(p, world, lds_bytes, stream);
+                if (lbvh) ran = launch_render_f64_lgrid(p, world, lds_bytes, stream, dev::kOptLightBvh);
                 else ran = launch_world<R, 0>(p, world, lds_bytes, stream);
             }
         }

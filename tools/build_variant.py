@@ -29,16 +29,18 @@ def main():
     var = os.path.join(ROOT, "build", "variants", a.name)
     os.makedirs(var, exist_ok=True)
     precs = [a.only] if a.only else ["f32", "f64"]
+    if "f64" in precs:
+        precs.append("f64_lgrid")   # the f64 light-grid kernels' unit (render_f64_lgrid.hip)
 
     def compile_one(prec):
-        contract = "off" if prec == "f64" else "on"
+        contract = "off" if prec.startswith("f64") else "on"
         subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "-fno-slp-vectorize",
                         "--offload-arch=gfx950", f"-I{CS}", f"-I{ROOT}/include", f"-ffp-contract={contract}",
                         *a.defines, "-c", f"{CS}/render_{prec}.hip", "-o", f"{var}/render_{prec}.o"], check=True)
 
-    with ThreadPoolExecutor(2) as ex:
+    with ThreadPoolExecutor(3) as ex:
         list(ex.map(compile_one, precs))
-    objs = [f"{var}/render_{p}.o" if p in precs else f"{OBJ}/render_{p}.o" for p in ("f32", "f64")]
+    objs = [f"{var}/render_{p}.o" if p in precs else f"{OBJ}/render_{p}.o" for p in ("f32", "f64", "f64_lgrid")]
     subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o", f"{var}/librtw.so",
                     *objs, f"{OBJ}/capi.o", f"{OBJ}/rtw_host.o", f"{OBJ}/bvh.o", "-ldl"], check=True)
     print("built", f"{var}/librtw.so")
