@@ -99,8 +99,8 @@ __device__ __forceinline__ void plane_uv(const R* pl, V3<R> pnt, R& u, R& v) {
 // here: it is NaN for every point of a mode-2 plane, (x, z) for mode 0, and a
 // rotation of the finite constants for mode 1 -- non-finite exactly when the
 // point is (up to overflow inside the rotation itself, |p| ~ 1e308).
-template <typename R>
-__device__ __forceinline__ bool plane_t(const R* pl, V3<R> o, V3<R> d, R tmin, R& t,
+template <typename R, typename PP>
+__device__ __forceinline__ bool plane_t(PP pl, V3<R> o, V3<R> d, R tmin, R& t,
                                         unsigned long long* panic) {
     V3<R> n = mk(pl[3], pl[4], pl[5]);
     R denom = dot(d, n);
@@ -122,8 +122,8 @@ __device__ __forceinline__ bool plane_t(const R* pl, V3<R> o, V3<R> d, R tmin, R
 // AABBox::hit, hittable.rs:291-339, over [rs, +inf]: the slab test the
 // reference runs before every object's own hit (bounded_hit).  Rust's f64
 // max/min ignore a NaN operand like fmax/fmin.
-template <typename R>
-__device__ __forceinline__ bool aabb_hit_ref(const R* lo, const R* hi, V3<R> o, V3<R> d, R rs) {
+template <typename R, typename PP>
+__device__ __forceinline__ bool aabb_hit_ref(PP lo, PP hi, V3<R> o, V3<R> d, R rs) {
     R t0 = P<R>::div_(lo[0] - o.x, d.x), t1 = P<R>::div_(hi[0] - o.x, d.x);
     if (__builtin_signbit(d.x)) { R q = t0; t0 = t1; t1 = q; }
     R tmin = t0, tmax = t1;
@@ -150,8 +150,8 @@ __device__ __forceinline__ bool aabb_hit_ref(const R* lo, const R* hi, V3<R> o, 
 // division; f32: a * rcp(b), whose infinities for a zero d_a or an infinite
 // a follow the same signs).  Anything else (a non-finite ray, other boxes)
 // takes aabb_hit_ref itself.
-template <typename R>
-__device__ __forceinline__ bool aabb_hit_plane(const R* lo, const R* hi, V3<R> o, V3<R> d, R rs) {
+template <typename R, typename PP>
+__device__ __forceinline__ bool aabb_hit_plane(PP lo, PP hi, V3<R> o, V3<R> d, R rs) {
     const bool fin = __builtin_isfinite(o.x) && __builtin_isfinite(o.y) && __builtin_isfinite(o.z) &&
                      __builtin_isfinite(d.x) && __builtin_isfinite(d.y) && __builtin_isfinite(d.z);
     int npin = 0, pin = 0;
@@ -2868,7 +2868,15 @@ __global__ void __launch_bounds__((64 * kernel_waves<R, kWorld, kOpt>()), sizeof
             RTW_PROBE_PLANES();
             for (int32_t k = 0; k < nplanes; ++k) {
                 R t;
-                const R* pl = kargs()->sc.planes + kPlaneR * k;
+                // f32 kernels: the plane record through a constant-address-space
+                // pointer -- its address is wave-uniform, so these are scalar loads
+                // (SGPR operands, the scalar cache) instead of a vector load per field
+                // whose latency started every segment (hit64 86.2 -> 85.7 ms, plain
+                // 58.0 -> 57.5, C3 f32 -1 %; profiles/r06pl_ab.jsonl).  The f64 kernels
+                // keep vector loads: the f64 record's SGPRs spilled (C2 f64 +0.3 %).
+                typedef const R __attribute__((address_space(4))) KR;
+                using PlanePtr = typename std::conditional<sizeof(R) == 4, KR*, const R*>::type;
+                PlanePtr pl = (PlanePtr)kargs()->sc.planes + kPlaneR * k;
                 // plane_t's one-sided test (plane.rs:62-63) first: it fails for every
                 // ray that leaves the Book-1 ground downwards, and then the box test
                 // (side-effect free, bounded_hit's first half) cannot change the outcome
