@@ -17,7 +17,7 @@ for e in $EXPS; do
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -fno-slp-vectorize --offload-arch=gfx950 -I$CS -I$ROOT/include \
     -ffp-contract=on -DRTW_EXP=$e -c $CS/render_f32.hip -o $D/render_f32.o || exit 1
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $D/librtw.so $D/render_f32.o \
-    $B/render_f64.o $B/capi.o $B/rtw_host.o $B/bvh.o || exit 1
+    $B/render_f64.o $B/render_f64_lgrid.o $B/capi.o $B/rtw_host.o $B/bvh.o || exit 1
 done
 for rd in 1 2; do
   echo "base"; timeout -k 10 300 python -u tools/bench_configs.py --configs C5 --spp-scale "$SCALE" || exit $?

@@ -35,8 +35,12 @@ def build():
                              f"{VAR}/render_f32.o"], check=True)
     subprocess.run(common + ["-ffp-contract=off", "-DRTW_CLOCK=f64", "-c", f"{cs}/render_f64.hip", "-o",
                              f"{VAR}/render_f64.o"], check=True)
+    # (the f64 light-grid kernels, render_f64_lgrid.hip, from the in-tree build: without
+    # probes -- their C3 / C5 f64 clock profiles need the probes in that unit, whose
+    # readers would clash with render_f64.hip's)
     subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o", f"{VAR}/librtw.so",
-                    f"{VAR}/render_f32.o", f"{VAR}/render_f64.o", f"{b}/capi.o", f"{b}/rtw_host.o", f"{b}/bvh.o",
+                    f"{VAR}/render_f32.o", f"{VAR}/render_f64.o", f"{b}/render_f64_lgrid.o", f"{b}/capi.o",
+                    f"{b}/rtw_host.o", f"{b}/bvh.o",
                     "-ldl"], check=True)
     print("built", f"{VAR}/librtw.so")
 

@@ -12,7 +12,7 @@ for e in ${EXPS:-1 2 3 4 5}; do
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -fno-slp-vectorize --offload-arch=gfx950 -I$CS -I$ROOT/include \
     -ffp-contract=on -DRTW_EXP=$e -c $CS/render_f32.hip -o $D/render_f32.o || exit 1
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $D/librtw.so $D/render_f32.o \
-    $ROOT/ray_tracing_weekend_amd/build/render_f64.o $ROOT/ray_tracing_weekend_amd/build/capi.o \
+    $ROOT/ray_tracing_weekend_amd/build/render_f64.o $ROOT/ray_tracing_weekend_amd/build/render_f64_lgrid.o $ROOT/ray_tracing_weekend_amd/build/capi.o \
     $ROOT/ray_tracing_weekend_amd/build/rtw_host.o $ROOT/ray_tracing_weekend_amd/build/bvh.o || exit 1
 done
 echo "base"; timeout -k 10 300 python tools/sweep.py --grid bvh_kind=3 --rounds 2 || exit $?

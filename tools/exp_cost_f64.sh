@@ -16,7 +16,7 @@ if [ "${1:-run}" = build ]; then
     D="$ROOT/build_exp/f64_exp$e"; mkdir -p "$D"
     /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -fno-slp-vectorize --offload-arch=gfx950 -I$CS -I$ROOT/include \
       -ffp-contract=off -DRTW_EXP=$e -c $CS/render_f64.hip -o $D/render_f64.o || exit 1
-    /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $D/librtw.so $B/render_f32.o $D/render_f64.o \
+    /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $D/librtw.so $B/render_f32.o $D/render_f64.o $B/render_f64_lgrid.o \
       $B/capi.o $B/rtw_host.o $B/bvh.o -ldl || exit 1
   done
   exit 0

@@ -34,7 +34,7 @@ def build():
                              f"{VAR}/render_f64.o"], check=True)
     subprocess.run(common + ["-ffp-contract=off", "-c", f"{cs}/capi.cpp", "-o", f"{VAR}/capi.o"], check=True)
     subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o", f"{VAR}/librtw.so",
-                    f"{VAR}/render_f32.o", f"{VAR}/render_f64.o", f"{VAR}/capi.o", f"{b}/rtw_host.o", f"{b}/bvh.o",
+                    f"{VAR}/render_f32.o", f"{VAR}/render_f64.o", f"{b}/render_f64_lgrid.o", f"{VAR}/capi.o", f"{b}/rtw_host.o", f"{b}/bvh.o",
                     "-ldl"], check=True)
     for f in ("render_f32.o", "render_f64.o", "capi.o"):
         os.remove(os.path.join(VAR, f))

@@ -32,7 +32,7 @@ def build():
     subprocess.run(common + ["-ffp-contract=off", "-DRTW_TRACE=f64", "-c", f"{cs}/render_f64.hip", "-o",
                              f"{VAR}/render_f64.o"], check=True)
     subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o", f"{VAR}/librtw.so",
-                    f"{VAR}/render_f32.o", f"{VAR}/render_f64.o", f"{b}/capi.o", f"{b}/rtw_host.o", f"{b}/bvh.o"],
+                    f"{VAR}/render_f32.o", f"{VAR}/render_f64.o", f"{b}/render_f64_lgrid.o", f"{b}/capi.o", f"{b}/rtw_host.o", f"{b}/bvh.o"],
                    check=True)
     print("built", f"{VAR}/librtw.so")
 
