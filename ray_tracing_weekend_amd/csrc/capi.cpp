@@ -1259,9 +1259,10 @@ int render_device_t(rtw_ctx* c, const rtw_camera* cam, uint64_t seed, uint32_t r
             // for a larger per-lane area (its LDS stash + piece slots)
             p.stack = bin_stack;
             bvh_width = 2;
-            // (4-wave workgroups: four copies per CU; wide: one copy per CU of 160 KiB)
+            // (4-wave workgroups: four copies per CU; wide: one workgroup per CU, which may
+            // take all of its 160 KiB -- the C2 scene needs 110, ~900 spheres fit)
             const size_t lds_max = c->bvh_lds_max ? c->bvh_lds_max
-                                                  : (sizeof(R) == 4 ? 36 * 1024 : (wide ? 128 * 1024 : 52 * 1024));
+                                                  : (sizeof(R) == 4 ? 36 * 1024 : (wide ? kLdsLimit : 52 * 1024));
             if (c->bvh_kind == 3 && tree_lds <= lds_max) {
                 world = rtw::kWorldBvhLds;
                 launch_lds = tree_lds;

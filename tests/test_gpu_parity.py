@@ -257,7 +257,7 @@ def _same(a, b):
 
 
 @pytest.mark.parametrize("prec", [rtw.RTW_F32, rtw.RTW_F64])
-@pytest.mark.parametrize("n", [11, 30])
+@pytest.mark.parametrize("n", [11, 14, 30])
 @pytest.mark.parametrize("kind", [3, 2, 1, 0])
 def test_bvh_equals_brute_force(prec, n, kind):
     """RTW_ACCEL_BVH only culls: the closest hit, hence every pixel, must be
@@ -274,6 +274,8 @@ def test_bvh_equals_brute_force(prec, n, kind):
                              tuning={"light_bvh_min": 1 << 30})
     if kind == 3 and n == 11:
         assert LAST["kernel"] == K_BVH_LDS          # the C1/C2 scene's tree fits in LDS
+    if kind == 3 and n == 14 and prec == rtw.RTW_F64:
+        assert LAST["kernel"] == K_BVH_LDS          # 784 spheres: the wide f64 workgroup's LDS (142 KiB)
     assert _same(brute, bvh)
     assert cb == cv
 
